@@ -1,0 +1,178 @@
+/*
+ * sblas.h -- C-ABI of the MI355X-native sparse-BLAS hot path (libsblas.so).
+ *
+ * Plain C: pointers, sizes and an int status.  No torch / HIP types appear in
+ * signatures (streams are passed as `void *` holding a hipStream_t; NULL is
+ * the device's null stream).  Every entry point returns SBLAS_OK (0) or a
+ * positive sblas_status; nothing calls exit().
+ *
+ * Two layers:
+ *  1. Reference operator API (drop-in, HOST pointers, ngpu devices, nothing
+ *     persists across calls) -- sblas_spMV_mgpu_*, sblas_csrmm_mgpu,
+ *     sblas_sptrsv_syncfree.  The exact C++-linkage names of the reference
+ *     (spMV_mgpu_baseline, ..., cusparse_mgpu_csrmm, sptrsv_syncfree_cuda) are
+ *     declared in sblas_refapi.h and forward here.
+ *  2. Persistent device API (DEVICE pointers, one device per object) used by
+ *     the benchmarks and by multi-process runs: upload once, run many times.
+ */
+#ifndef SBLAS_H
+#define SBLAS_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SBLAS_OK = 0,
+    SBLAS_ERR_INVALID = 1,     /* bad argument / shape */
+    SBLAS_ERR_HIP = 2,         /* HIP runtime failure (message: sblas_last_error) */
+    SBLAS_ERR_NOMEM = 3,       /* footprint > 0.8 x free device memory */
+    SBLAS_ERR_NODEV = 4,       /* no usable GPU */
+    SBLAS_ERR_UNSUPPORTED = 5, /* e.g. local nnz >= 2^31 */
+    SBLAS_ERR_RCCL = 6,
+    SBLAS_ERR_IO = 7           /* file could not be read / parsed */
+} sblas_status;
+
+/* Kernel selector; numbering follows test_spmv's `kernel` argument
+ * (spmv/test/dspmv_test.cu:80): 1 = csrmv (row split), 2 = csrmv_mp
+ * (nnz-balanced), 3 = CSR5 (disabled in the reference, enabled here). */
+typedef enum {
+    SBLAS_SPMV_ROWSPLIT = 1, /* CSR-adaptive row blocks, wave64, LDS stream */
+    SBLAS_SPMV_CSR5 = 2,     /* wave64 CSR5-style tiles, segmented sum */
+    SBLAS_SPMV_CSR5_ALT = 3  /* same kernel as 2 */
+} sblas_spmv_algo;
+
+const char *sblas_status_string(int status);
+const char *sblas_last_error(void);
+int sblas_version(void);
+int sblas_device_count(int *count);
+
+/* ------------------------------------------------------------------------ */
+/* 1. Reference operator API (host pointers).  Cites: spmv/include/
+ *    spmv_kernel.h:11-36, spmm/include/spmm_kernel.h:6-31,
+ *    sptrsv/sptrsv_v1/src/sptrsv_syncfree_cuda.h:287-300.  Devices are
+ *    ordinals 0..ngpu-1; if fewer physical GPUs exist the ordinals wrap
+ *    (d % count) so multi-partition logic can run on one GPU. Return: 0 ok,
+ *    -1 footprint > 0.8 x free memory (reference behaviour), >0 sblas_status. */
+int sblas_spMV_mgpu_baseline(int m, int n, long long nnz, double *alpha,
+                             double *csrVal, long long *csrRowPtr,
+                             int *csrColIndex, double *x, double *beta,
+                             double *y, int ngpu);
+int sblas_spMV_mgpu_v1(int m, int n, long long nnz, double *alpha,
+                       double *csrVal, long long *csrRowPtr, int *csrColIndex,
+                       double *x, double *beta, double *y, int ngpu,
+                       int kernel);
+int sblas_spMV_mgpu_v2(int m, int n, long long nnz, double *alpha,
+                       double *csrVal, long long *csrRowPtr, int *csrColIndex,
+                       double *x, double *beta, double *y, int ngpu,
+                       int kernel, long long nb, int copy_of_workspace);
+/* spmv_helper.cu:16-39 (fixed: last row r with rowptr[r] <= idx, Q5) */
+int sblas_get_row_from_index(int n, long long *a, long long idx);
+double sblas_get_time(void);                 /* spmv_helper.cu:41-48 */
+double sblas_get_gpu_availble_mem(int ngpu); /* spmv_helper.cu:51-76, GB */
+
+/* C = alpha*A*B + beta*C; A m x k CSR (int32); B k x n column-major (ld=k);
+ * C m x n column-major (ld=m).  Row-partitioned across ngpu devices. */
+int sblas_csrmm_mgpu(int m, int n, int k, const double *alpha, int nnz_A,
+                     int *csrRowPtr_A, int *csrColIndex_A, double *csrVal_A,
+                     const double *beta, double *B_dense, double *C_dense,
+                     int ngpu);
+
+/* Sync-free triangular solve, CSC input, x output; validates against x_ref
+ * when x_ref != NULL (rel-L1, prints like the reference) and reports gflops.
+ * substitution 0 forward (lower), 1 backward (upper). rhs must be 1. */
+int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx,
+                          const double *cscVal, int m, int n, int nnz,
+                          int substitution, int rhs, int opt, double *x,
+                          const double *b, const double *x_ref, double *gflops,
+                          int ngpu);
+
+/* ------------------------------------------------------------------------ */
+/* 2. Persistent device API. */
+typedef struct sblas_csr_s *sblas_csr;
+
+/* Upload rows [row_begin, row_end) of a HOST global CSR (int64 rowptr) whose
+ * element range is [idx_begin, idx_end) -- i.e. a spMV_mgpu_v1 slice: first
+ * and last rows may be partial (dspmv_mgpu_v1.cu:125-133).  The device copy
+ * uses an int32 local rowptr. */
+int sblas_csr_upload_slice(sblas_csr *out, int device, int n,
+                           const long long *rowptr, const int *col,
+                           const double *val, int row_begin, int row_end,
+                           long long idx_begin, long long idx_end,
+                           void *stream);
+/* Wrap DEVICE arrays (int32 rowptr[m+1], col[nnz], val[nnz]); the arrays are
+ * copied into padded storage owned by the handle. */
+int sblas_csr_from_device(sblas_csr *out, int device, int m, int n, int nnz,
+                          const int *d_rowptr, const int *d_col,
+                          const double *d_val, void *stream);
+int sblas_csr_destroy(sblas_csr A);
+int sblas_csr_info(sblas_csr A, int *m, int *n, long long *nnz);
+/* Build the analysis for an algorithm (row blocks / CSR5 tiles); run once. */
+int sblas_csr_analyse(sblas_csr A, int algo, void *stream);
+/* y = alpha*A*x + beta*y on the handle's device; x, y DEVICE pointers. */
+int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x,
+               double beta, double *d_y, void *stream);
+/* bytes the algorithm must move per call (DESIGN.md "Algorithmic bytes"). */
+long long sblas_spmv_algorithmic_bytes(sblas_csr A, int beta_nonzero);
+
+/* SpMM on a device handle: C(m x n, ldc) = alpha*A*B(k x n, ldb) + beta*C.
+ * b_layout 0 = column-major B (ld=ldb >= k), 1 = row-major B (ld >= n). */
+int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb,
+               int b_layout, double beta, double *d_C, int ldc, void *stream);
+
+/* Device CSR -> CSC transpose of a handle; outputs DEVICE arrays sized
+ * colptr[n+1], rowidx[nnz], cval[nnz]; row indices ascend within columns
+ * (bit-exact with tranpose.h:6-43). */
+int sblas_csr_transpose(sblas_csr A, int *d_colptr, int *d_rowidx,
+                        double *d_cval, void *stream);
+
+/* Triangular solve handle over a DEVICE lower/upper CSC matrix with the
+ * diagonal stored first (lower) / last (upper) in each column. */
+typedef struct sblas_trsv_s *sblas_trsv;
+int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz,
+                      const int *d_colptr, const int *d_rowidx,
+                      const double *d_val, int substitution, void *stream);
+/* algo 0 = sync-free CSC push (reference algorithm), 1 = CSR pull with ready
+ * flags (deterministic sums). */
+int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x,
+                     void *stream);
+int sblas_trsv_levels(sblas_trsv T, int *nlevel);
+int sblas_trsv_destroy(sblas_trsv T);
+
+/* Multi-partition y assembly after an allgather of padded slices: partition
+ * r's slice starts at d_gathered + r*stride; d_meta (DEVICE, 3*g ints) holds
+ * {row0, nrows, cont} per partition; cont = first row continues partition
+ * r-1 (its entry is added, in partition order). */
+int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
+                          const int *d_meta, double *d_y, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Host utilities (no GPU needed). */
+/* Matrix-Market: mode 0 = full mmio_data semantics (symmetric expansion,
+ * pattern -> 1.0); mode 1 = test_spmv 'f' loader (file order, Q1/Q2);
+ * mode 2 = test_spmv 'b' (values 1e-5).  Call with rowptr==NULL to size. */
+int sblas_mm_read(const char *path, int mode, int *m, int *n, long long *nnz,
+                  long long *rowptr, int *col, double *val);
+
+/* nnz-balanced partition of spMV_mgpu_v1 (dspmv_mgpu_v1.cu:60-94, Q5 fixed).
+ * Arrays of g entries. */
+int sblas_partition_nnz(int m, long long nnz, const long long *rowptr, int g,
+                        long long *start_idx, long long *end_idx,
+                        int *start_row, int *end_row, int *start_flag);
+/* row-block partition (dspmv_mgpu_baseline.cu:64-65); g+1 entries. */
+int sblas_partition_rowblock(int m, int g, int *row_start);
+
+/* Scaled synthetic of DESIGN.md: rows < n/8 have `heavy` nnz, others
+ * `light`; distinct uniform-random (or prefix) sorted columns; values U[0,1).
+ * Generates rows [row_begin,row_end) into caller arrays (rowptr is global,
+ * int64, all n+1 entries filled by sblas_gen_synth_rowptr). */
+int sblas_gen_synth_rowptr(int n, int heavy, int light, long long *rowptr);
+int sblas_gen_synth_rows(int n, int heavy, int light, int prefix_cols,
+                         unsigned long long seed, const long long *rowptr,
+                         int row_begin, int row_end, int *col, double *val);
+int sblas_gen_vector(int n, unsigned long long seed, double *v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,50 @@
+// assemble.hip -- device-side merge of the per-partition y slices after the
+// RCCL allgather (multi-GPU SpMV).
+//
+// Partition r owns rows [row0[r], row0[r]+nrows[r]); when cont[r] is set its
+// first row continues partition r-1's last row (an nnz-balanced split) and
+// its first entry is a partial alpha*p to be ADDED, in partition order, as the
+// reference's host fix-up does (spmv/src/dspmv_mgpu_v1.cu:235-248).  The
+// gathered buffer holds g slices of `stride` doubles (padded equal chunks, as
+// all_gather_into_tensor / ncclAllGather require).
+#include "sblas_internal.hpp"
+
+namespace sblas {
+
+__global__ void k_assemble_copy(const double *__restrict__ gathered, int g, long long stride,
+                                const int *__restrict__ meta, double *__restrict__ y)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)g * stride) return;
+    const int r = (int)(i / stride);
+    const int k = (int)(i - (long long)r * stride);
+    const int row0 = meta[3 * r], nrows = meta[3 * r + 1], cont = meta[3 * r + 2];
+    if (k >= nrows || (k == 0 && cont)) return;
+    y[row0 + k] = gathered[i];
+}
+
+__global__ void k_assemble_carry(const double *__restrict__ gathered, int g, long long stride,
+                                 const int *__restrict__ meta, double *__restrict__ y)
+{
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int r = 0; r < g; ++r)  // partition order: deterministic
+        if (meta[3 * r + 2] && meta[3 * r + 1] > 0) y[meta[3 * r]] += gathered[(long long)r * stride];
+}
+
+}  // namespace sblas
+
+using namespace sblas;
+
+extern "C" int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
+                                     const int *d_meta, double *d_y, void *stream)
+{
+    if (g <= 0 || stride < 0 || !d_meta || !d_y) return SBLAS_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    const long long total = (long long)g * stride;
+    if (total > 0)
+        hipLaunchKernelGGL(k_assemble_copy, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                           d_gathered, g, stride, d_meta, d_y);
+    hipLaunchKernelGGL(k_assemble_carry, dim3(1), dim3(64), 0, s, d_gathered, g, stride, d_meta, d_y);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}

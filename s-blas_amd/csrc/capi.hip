@@ -1,0 +1,242 @@
+// capi.hip -- persistent device API of libsblas (include/sblas.h, layer 2).
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "sblas_internal.hpp"
+
+namespace sblas {
+
+int resolve_device(int ordinal, int *phys)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("no HIP device available");
+        return SBLAS_ERR_NODEV;
+    }
+    *phys = ordinal % count;
+    return SBLAS_OK;
+}
+
+static int alloc_padded(sblas_csr_s &A, long long nnz)
+{
+    const long long cap = ((nnz + 3) & ~3LL) + 4;  // 16-B vector over-read pad
+    SBLAS_HIP(hipMalloc(&A.col, sizeof(int) * cap));
+    SBLAS_HIP(hipMalloc(&A.val, sizeof(double) * cap));
+    SBLAS_HIP(hipMemset(A.col + nnz, 0, sizeof(int) * (cap - nnz)));
+    SBLAS_HIP(hipMemset(A.val + nnz, 0, sizeof(double) * (cap - nnz)));
+    SBLAS_HIP(hipMalloc(&A.rowptr, sizeof(int) * ((size_t)A.m + 1)));
+    return SBLAS_OK;
+}
+
+}  // namespace sblas
+
+using namespace sblas;
+
+extern "C" {
+
+const char *sblas_status_string(int s)
+{
+    switch (s) {
+    case SBLAS_OK: return "ok";
+    case SBLAS_ERR_INVALID: return "invalid argument";
+    case SBLAS_ERR_HIP: return "HIP runtime error";
+    case SBLAS_ERR_NOMEM: return "insufficient device memory";
+    case SBLAS_ERR_NODEV: return "no device";
+    case SBLAS_ERR_UNSUPPORTED: return "unsupported";
+    case SBLAS_ERR_RCCL: return "RCCL error";
+    case SBLAS_ERR_IO: return "I/O error";
+    default: return s == -1 ? "footprint exceeds 0.8 x free device memory" : "unknown";
+    }
+}
+
+int sblas_version(void) { return 100; }
+
+int sblas_device_count(int *count)
+{
+    if (!count) return SBLAS_ERR_INVALID;
+    *count = 0;
+    if (hipGetDeviceCount(count) != hipSuccess) {
+        *count = 0;
+        return SBLAS_ERR_NODEV;
+    }
+    return SBLAS_OK;
+}
+
+int sblas_csr_upload_slice(sblas_csr *out, int device, int n, const long long *rowptr,
+                           const int *col, const double *val, int row_begin, int row_end,
+                           long long idx_begin, long long idx_end, void *stream)
+{
+    if (!out || !rowptr || row_begin < 0 || row_end < row_begin || idx_end < idx_begin || n < 0)
+        return SBLAS_ERR_INVALID;
+    const long long dnnz = idx_end - idx_begin;
+    if (dnnz >= (long long)std::numeric_limits<int>::max()) {
+        set_error("local nnz %lld >= 2^31: partition across more devices", dnnz);
+        return SBLAS_ERR_UNSUPPORTED;
+    }
+    int phys;
+    SBLAS_TRY(resolve_device(device, &phys));
+    DeviceGuard g(phys);
+    hipStream_t s = (hipStream_t)stream;
+    auto *A = new sblas_csr_s();
+    A->device = phys;
+    A->m = row_end - row_begin;
+    A->n = n;
+    A->nnz = dnnz;
+    A->h_rowptr.resize((size_t)A->m + 1);
+    // local int32 rowptr: [0]=0, [m]=dnnz, middle rebased (dspmv_mgpu_v1.cu:125-133)
+    A->h_rowptr[0] = 0;
+    if (A->m > 0) A->h_rowptr[(size_t)A->m] = (int)dnnz;
+    for (int j = 1; j < A->m; ++j) A->h_rowptr[(size_t)j] = (int)(rowptr[row_begin + j] - idx_begin);
+    int st = alloc_padded(*A, dnnz);
+    if (st != SBLAS_OK) {
+        sblas_csr_destroy(A);
+        return st;
+    }
+#define UP_CHECK(expr)                                                         \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error("%s -> %s", #expr, hipGetErrorString(e_));               \
+            sblas_csr_destroy(A);                                              \
+            return SBLAS_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+    UP_CHECK(hipMemcpyAsync(A->rowptr, A->h_rowptr.data(), sizeof(int) * ((size_t)A->m + 1),
+                            hipMemcpyHostToDevice, s));
+    if (dnnz) {
+        UP_CHECK(hipMemcpyAsync(A->col, col + idx_begin, sizeof(int) * dnnz, hipMemcpyHostToDevice, s));
+        UP_CHECK(hipMemcpyAsync(A->val, val + idx_begin, sizeof(double) * dnnz, hipMemcpyHostToDevice, s));
+    }
+    UP_CHECK(hipStreamSynchronize(s));
+#undef UP_CHECK
+    *out = A;
+    return SBLAS_OK;
+}
+
+int sblas_csr_from_device(sblas_csr *out, int device, int m, int n, int nnz, const int *d_rowptr,
+                          const int *d_col, const double *d_val, void *stream)
+{
+    if (!out || m < 0 || n < 0 || nnz < 0 || !d_rowptr) return SBLAS_ERR_INVALID;
+    int phys;
+    SBLAS_TRY(resolve_device(device, &phys));
+    DeviceGuard g(phys);
+    hipStream_t s = (hipStream_t)stream;
+    auto *A = new sblas_csr_s();
+    A->device = phys;
+    A->m = m;
+    A->n = n;
+    A->nnz = nnz;
+    int st = alloc_padded(*A, nnz);
+    if (st == SBLAS_OK) {
+        A->h_rowptr.resize((size_t)m + 1);
+        hipError_t e = hipMemcpyAsync(A->rowptr, d_rowptr, sizeof(int) * ((size_t)m + 1),
+                                      hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && nnz)
+            e = hipMemcpyAsync(A->col, d_col, sizeof(int) * (size_t)nnz, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && nnz)
+            e = hipMemcpyAsync(A->val, d_val, sizeof(double) * (size_t)nnz, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(A->h_rowptr.data(), d_rowptr, sizeof(int) * ((size_t)m + 1),
+                               hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            set_error("sblas_csr_from_device: %s", hipGetErrorString(e));
+            st = SBLAS_ERR_HIP;
+        }
+    }
+    if (st != SBLAS_OK) {
+        sblas_csr_destroy(A);
+        return st;
+    }
+    if (A->h_rowptr[0] != 0 || A->h_rowptr[(size_t)m] != nnz) {
+        sblas_csr_destroy(A);
+        set_error("rowptr must start at 0 and end at nnz");
+        return SBLAS_ERR_INVALID;
+    }
+    *out = A;
+    return SBLAS_OK;
+}
+
+int sblas_csr_destroy(sblas_csr A)
+{
+    if (!A) return SBLAS_OK;
+    {
+        DeviceGuard g(A->device);
+        free_plans(*A);
+        (void)hipFree(A->rowptr);
+        (void)hipFree(A->col);
+        (void)hipFree(A->val);
+    }
+    delete A;
+    return SBLAS_OK;
+}
+
+int sblas_csr_info(sblas_csr A, int *m, int *n, long long *nnz)
+{
+    if (!A) return SBLAS_ERR_INVALID;
+    if (m) *m = A->m;
+    if (n) *n = A->n;
+    if (nnz) *nnz = A->nnz;
+    return SBLAS_OK;
+}
+
+int sblas_csr_analyse(sblas_csr A, int algo, void *stream)
+{
+    if (!A) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    hipStream_t s = (hipStream_t)stream;
+    switch (algo) {
+    case SBLAS_SPMV_ROWSPLIT: return build_rowsplit_plan(*A, s);
+    case SBLAS_SPMV_CSR5:
+    case SBLAS_SPMV_CSR5_ALT: return build_csr5_plan(*A, s);
+    default: return SBLAS_ERR_INVALID;
+    }
+}
+
+int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x, double beta, double *d_y,
+               void *stream)
+{
+    if (!A || (!d_x && A->nnz) || (!d_y && A->m)) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    hipStream_t s = (hipStream_t)stream;
+    switch (algo) {
+    case SBLAS_SPMV_ROWSPLIT:
+        if (!A->rs.ready) SBLAS_TRY(build_rowsplit_plan(*A, s));
+        return launch_spmv_rowsplit(*A, alpha, d_x, beta, d_y, s);
+    case SBLAS_SPMV_CSR5:
+    case SBLAS_SPMV_CSR5_ALT:
+        if (!A->c5.ready) SBLAS_TRY(build_csr5_plan(*A, s));
+        return launch_spmv_csr5(*A, alpha, d_x, beta, d_y, s);
+    default: return SBLAS_ERR_INVALID;
+    }
+}
+
+// Compulsory traffic: each array touched once.
+long long sblas_spmv_algorithmic_bytes(sblas_csr A, int beta_nonzero)
+{
+    if (!A) return 0;
+    return A->nnz * 12LL + ((long long)A->m + 1) * 4LL + (long long)A->n * 8LL +
+           (long long)A->m * 8LL + (beta_nonzero ? (long long)A->m * 8LL : 0LL);
+}
+
+int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb, int b_layout,
+               double beta, double *d_C, int ldc, void *stream)
+{
+    if (!A || n < 0 || (b_layout != 0 && b_layout != 1)) return SBLAS_ERR_INVALID;
+    if (b_layout == 0 && ldb < A->n) return SBLAS_ERR_INVALID;
+    if (b_layout == 1 && ldb < n) return SBLAS_ERR_INVALID;
+    if (ldc < A->m) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    return launch_spmm(*A, n, alpha, d_B, ldb, b_layout, beta, d_C, ldc, (hipStream_t)stream);
+}
+
+int sblas_csr_transpose(sblas_csr A, int *d_colptr, int *d_rowidx, double *d_cval, void *stream)
+{
+    if (!A || !d_colptr) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    return launch_transpose(*A, d_colptr, d_rowidx, d_cval, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// sblas_internal.hpp -- shared internals of libsblas (HIP host + kernels).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/sblas.h"
+
+namespace sblas {
+
+void set_error(const char *fmt, ...);
+
+#define SBLAS_HIP(expr)                                                        \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            ::sblas::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,    \
+                               hipGetErrorString(e_));                         \
+            return SBLAS_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+
+#define SBLAS_TRY(expr)                                                        \
+    do {                                                                       \
+        int s_ = (expr);                                                       \
+        if (s_ != SBLAS_OK) return s_;                                         \
+    } while (0)
+
+// Row-split (CSR-adaptive) tuning. One 256-thread workgroup per row block.
+constexpr int kRsThreads = 256;
+constexpr int kRsBlockNnz = 2048;   // LDS product stream capacity (16 KiB f64)
+constexpr int kRsMaxRows = 1024;    // rows per stream block
+constexpr int kRsLongChunk = 8192;  // nnz per workgroup for long rows
+
+// Row block descriptor (16 B): stream block when a > row (a = end row);
+// long-row chunk when a < 0 (chunk k = -a-1, b = partial slot or -1).
+struct RowBlock {
+    int row;
+    int a;
+    int b;
+    int c;
+};
+
+// CSR5-style tiles: 64 lanes x kC5Sigma nnz per tile (one wave per tile).
+constexpr int kC5Lanes = 64;
+constexpr int kC5Sigma = 16;
+constexpr int kC5Tile = kC5Lanes * kC5Sigma;
+
+struct Csr5Plan {
+    long long ntiles = 0;
+    int *tile_row = nullptr;       // [ntiles+1] row of tile's first element; bit31: tile has empty rows
+    uint32_t *flags = nullptr;     // [ntiles*64] per-lane row-start bits (bit k: element k starts a row)
+    double *tval = nullptr;        // [ntiles*kC5Tile] tile-transposed values
+    int *tcol = nullptr;           // [ntiles*kC5Tile] tile-transposed columns
+    int *seg_off = nullptr;        // [ntiles+1] offset into seg_row for tiles with empty rows
+    int *seg_row = nullptr;        // explicit row of each row start for flagged tiles
+    int *empty_rows = nullptr;     // rows with no entries (y = beta*y)
+    int nempty = 0;
+    double *carry = nullptr;       // [ntiles] tile head partial sums
+    bool ready = false;
+};
+
+struct RsPlan {
+    int nblocks = 0;
+    RowBlock *blocks = nullptr;
+    int nlong = 0;                 // multi-chunk long rows
+    int4 *long_rows = nullptr;     // {row, first_slot, nchunks, 0}
+    double *partial = nullptr;     // [nslots]
+    int nslots = 0;
+    bool ready = false;
+};
+
+}  // namespace sblas
+
+struct sblas_csr_s {
+    int device = 0;
+    int m = 0, n = 0;
+    long long nnz = 0;
+    int *rowptr = nullptr;   // [m+1] int32 local
+    int *col = nullptr;      // [nnz + pad]
+    double *val = nullptr;   // [nnz + pad]
+    sblas::RsPlan rs;
+    sblas::Csr5Plan c5;
+    std::vector<int> h_rowptr;  // host copy (analysis)
+};
+
+namespace sblas {
+
+// Kernel launchers (defined in the .hip files).
+int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
+                         double beta, double *y, hipStream_t s);
+int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s);
+int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
+                     double beta, double *y, hipStream_t s);
+int build_csr5_plan(sblas_csr_s &A, hipStream_t s);
+void free_plans(sblas_csr_s &A);
+
+int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
+                int ldb, int b_layout, double beta, double *C, int ldc,
+                hipStream_t s);
+int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx,
+                     double *cval, hipStream_t s);
+
+// Scoped device switch.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Host helpers shared by capi / refapi (host_utils.cpp).
+int row_of_index(int m, const long long *rowptr, long long idx);
+int resolve_device(int ordinal, int *phys);  // wraps ordinals on few GPUs
+
+}  // namespace sblas

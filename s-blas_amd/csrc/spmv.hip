@@ -1,0 +1,485 @@
+// spmv.hip -- fp64 CSR SpMV kernels for gfx950 (MI355X).
+//
+// Replaces the per-device cusparseDcsrmv / cusparseDcsrmv_mp calls of
+// spmv/src/dspmv_mgpu_baseline.cu:163-167 and dspmv_mgpu_v1.cu:199-210, and
+// the (disabled) CSR5 library spmv/include/detail/cuda/csr5_spmv_cuda.h.
+//
+//  * Row split ("kernel 1"): CSR-adaptive row blocks. One 256-thread
+//    workgroup per block of whole rows holding <= 2048 nnz; val/col are
+//    streamed with 16-byte non-temporal loads (fully coalesced, they are read
+//    once), products val*x[col] land in LDS, then a power-of-two group of
+//    lanes per row (1..64, chosen from the block's row count) reduces each
+//    row from LDS with wave shuffles.  Rows longer than a block are split in
+//    8192-nnz chunks, one workgroup each, combined by a tiny finalize pass.
+//  * CSR5-style segmented sum ("kernel 2/3"): wave64 tiles of 64 lanes x 16
+//    nnz.  Values/columns are stored tile-transposed so every lane issues
+//    16-byte loads and a wave reads 1 KiB contiguous per instruction; a
+//    32-bit row-start mask per lane replaces CSR5's 32-lane bit-flag
+//    descriptor.  Lane-local segmented sums, then a 6-step suffix segmented
+//    scan across the wave joins rows that cross lanes; rows that cross tiles
+//    are completed by a calibration pass (csr5_spmv_cuda.h:313-382 analogue).
+//  * alpha/beta are honoured by both (the reference's CSR5 ignored them, Q4);
+//    beta == 0 never reads y (BLAS/cuSPARSE convention).
+#include <algorithm>
+#include <vector>
+
+#include "sblas_internal.hpp"
+
+namespace sblas {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v4i ld_nt_v4i(const int *p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const v4i *>(p));
+}
+__device__ __forceinline__ v2d ld_nt_v2d(const double *p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
+}
+
+// ---------------------------------------------------------------------------
+// Row split
+// ---------------------------------------------------------------------------
+template <bool kBeta>
+__global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
+    const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    const RowBlock *__restrict__ blocks, double alpha, double beta,
+    double *__restrict__ y, double *__restrict__ partial)
+{
+    __shared__ double prod[kRsBlockNnz + 8];
+    __shared__ double wsum[kRsThreads / 64];
+    const RowBlock blk = blocks[blockIdx.x];
+    const int tid = threadIdx.x;
+
+    if (blk.a >= 0) {
+        // ---- stream block: rows [r0, r1), nnz <= kRsBlockNnz -------------
+        const int r0 = blk.row, r1 = blk.a;
+        const int j0 = rowptr[r0], j1 = rowptr[r1];
+        const int base = j0 & ~3;
+        const int ngroups = (j1 - base + 3) >> 2;
+        for (int g = tid; g < ngroups; g += kRsThreads) {
+            const int e = base + 4 * g;
+            const v4i c = ld_nt_v4i(col + e);
+            const v2d va = ld_nt_v2d(val + e);
+            const v2d vb = ld_nt_v2d(val + e + 2);
+            const double v[4] = {va.x, va.y, vb.x, vb.y};
+            const int cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = e + k;
+                if (idx >= j0 && idx < j1) prod[idx - j0] = v[k] * x[cc[k]];
+            }
+        }
+        __syncthreads();
+        const int nrows = r1 - r0;
+        int tpr = nrows > 0 ? kRsThreads / nrows : 64;
+        tpr = tpr >= 64 ? 64 : tpr >= 32 ? 32 : tpr >= 16 ? 16 : tpr >= 8 ? 8
+            : tpr >= 4 ? 4 : tpr >= 2 ? 2 : 1;
+        const int grp = tid / tpr, lane = tid & (tpr - 1);
+        const int ngrp = kRsThreads / tpr;
+        for (int r = r0 + grp; r < r1; r += ngrp) {
+            const int a = rowptr[r] - j0, b = rowptr[r + 1] - j0;
+            double s = 0.0;
+            for (int k = a + lane; k < b; k += tpr) s += prod[k];
+            for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+            if (lane == 0) y[r] = kBeta ? alpha * s + beta * y[r] : alpha * s;
+        }
+    } else {
+        // ---- long-row chunk ------------------------------------------------
+        const int r = blk.row, k = -blk.a - 1;
+        const int rs = rowptr[r], re = rowptr[r + 1];
+        const int j0 = rs + k * kRsLongChunk;
+        const int j1 = min(re, j0 + kRsLongChunk);
+        const int base = j0 & ~3;
+        const int ngroups = (j1 - base + 3) >> 2;
+        double s = 0.0;
+        for (int g = tid; g < ngroups; g += kRsThreads) {
+            const int e = base + 4 * g;
+            const v4i c = ld_nt_v4i(col + e);
+            const v2d va = ld_nt_v2d(val + e);
+            const v2d vb = ld_nt_v2d(val + e + 2);
+            const double v[4] = {va.x, va.y, vb.x, vb.y};
+            const int cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = e + q;
+                if (idx >= j0 && idx < j1) s += v[q] * x[cc[q]];
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if ((tid & 63) == 0) wsum[tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < kRsThreads / 64; ++w) t += wsum[w];
+            if (blk.b < 0) y[r] = kBeta ? alpha * t + beta * y[r] : alpha * t;
+            else partial[blk.b] = t;
+        }
+    }
+}
+
+template <bool kBeta>
+__global__ void k_spmv_long_finalize(const int4 *__restrict__ long_rows, int nlong,
+                                     const double *__restrict__ partial,
+                                     double alpha, double beta,
+                                     double *__restrict__ y)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlong) return;
+    const int4 L = long_rows[i];
+    double s = 0.0;
+    for (int q = 0; q < L.z; ++q) s += partial[L.y + q];
+    y[L.x] = kBeta ? alpha * s + beta * y[L.x] : alpha * s;
+}
+
+int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.rs.ready) return SBLAS_OK;
+    DeviceGuard g(A.device);
+    const std::vector<int> &rp = A.h_rowptr;
+    std::vector<RowBlock> blocks;
+    std::vector<int4> longs;
+    blocks.reserve(A.nnz / kRsBlockNnz + A.m / kRsMaxRows + 16);
+    int nslots = 0;
+    int r = 0;
+    while (r < A.m) {
+        const int len = rp[r + 1] - rp[r];
+        if (len > kRsBlockNnz) {
+            const int nch = (len + kRsLongChunk - 1) / kRsLongChunk;
+            if (nch == 1) {
+                blocks.push_back({r, -1, -1, 0});
+            } else {
+                longs.push_back(make_int4(r, nslots, nch, 0));
+                for (int k = 0; k < nch; ++k) blocks.push_back({r, -1 - k, nslots + k, 0});
+                nslots += nch;
+            }
+            ++r;
+            continue;
+        }
+        const int start = r;
+        int nz = 0;
+        while (r < A.m && r - start < kRsMaxRows) {
+            const int l = rp[r + 1] - rp[r];
+            if (l > kRsBlockNnz || nz + l > kRsBlockNnz) break;
+            nz += l;
+            ++r;
+        }
+        blocks.push_back({start, r, 0, 0});
+    }
+    A.rs.nblocks = (int)blocks.size();
+    A.rs.nlong = (int)longs.size();
+    A.rs.nslots = nslots;
+    if (A.rs.nblocks) {
+        SBLAS_HIP(hipMalloc(&A.rs.blocks, sizeof(RowBlock) * blocks.size()));
+        SBLAS_HIP(hipMemcpyAsync(A.rs.blocks, blocks.data(), sizeof(RowBlock) * blocks.size(),
+                                 hipMemcpyHostToDevice, s));
+    }
+    if (A.rs.nlong) {
+        SBLAS_HIP(hipMalloc(&A.rs.long_rows, sizeof(int4) * longs.size()));
+        SBLAS_HIP(hipMemcpyAsync(A.rs.long_rows, longs.data(), sizeof(int4) * longs.size(),
+                                 hipMemcpyHostToDevice, s));
+        SBLAS_HIP(hipMalloc(&A.rs.partial, sizeof(double) * nslots));
+    }
+    SBLAS_HIP(hipStreamSynchronize(s));
+    A.rs.ready = true;
+    return SBLAS_OK;
+}
+
+int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
+                         double beta, double *y, hipStream_t s)
+{
+    if (!A.rs.ready) return SBLAS_ERR_INVALID;
+    if (A.rs.nblocks == 0) return SBLAS_OK;
+    if (beta != 0.0) {
+        hipLaunchKernelGGL(k_spmv_rowsplit<true>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+                           A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
+        if (A.rs.nlong)
+            hipLaunchKernelGGL(k_spmv_long_finalize<true>, dim3((A.rs.nlong + 63) / 64), dim3(64),
+                               0, s, A.rs.long_rows, A.rs.nlong, A.rs.partial, alpha, beta, y);
+    } else {
+        hipLaunchKernelGGL(k_spmv_rowsplit<false>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+                           A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
+        if (A.rs.nlong)
+            hipLaunchKernelGGL(k_spmv_long_finalize<false>, dim3((A.rs.nlong + 63) / 64), dim3(64),
+                               0, s, A.rs.long_rows, A.rs.nlong, A.rs.partial, alpha, beta, y);
+    }
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// CSR5-style wave64 tiles
+// ---------------------------------------------------------------------------
+// Storage position of element (lane l, k) of a tile, k in [0, 16):
+//   values : pairs  -> (k/2)*128 + 2l + (k&1)   (16-B loads, 1 KiB per wave)
+//   columns: quads  -> (k/4)*256 + 4l + (k&3)
+__device__ __forceinline__ int c5_vpos(int l, int k) { return (k >> 1) * 128 + 2 * l + (k & 1); }
+__device__ __forceinline__ int c5_cpos(int l, int k) { return (k >> 2) * 256 + 4 * l + (k & 3); }
+
+__global__ void k_c5_transpose(const int *__restrict__ col, const double *__restrict__ val,
+                               long long nnz, long long total, int *__restrict__ tcol,
+                               double *__restrict__ tval)
+{
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const long long t = e / kC5Tile;
+    const int w = (int)(e - t * kC5Tile);
+    const int l = w / kC5Sigma, k = w % kC5Sigma;
+    const bool in = e < nnz;
+    tval[t * kC5Tile + c5_vpos(l, k)] = in ? val[e] : 0.0;
+    tcol[t * kC5Tile + c5_cpos(l, k)] = in ? col[e] : 0;
+}
+
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmv_csr5(
+    const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+    const double *__restrict__ tval, const int *__restrict__ tcol,
+    const int *__restrict__ seg_off, const int *__restrict__ seg_row,
+    const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
+    double beta, double *__restrict__ y, double *__restrict__ carry)
+{
+    const int lane = threadIdx.x & 63;
+    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;  // wave-uniform
+    const double *tv = tval + t * kC5Tile;
+    const int *tc = tcol + t * kC5Tile;
+    const uint32_t f = flags[t * 64 + lane];
+    const int trow = tile_row[t];
+    const bool gap = trow < 0;  // bit31: tile contains empty rows
+    const int r0 = trow & 0x7fffffff;
+
+    double p[kC5Sigma];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        const v4i c = ld_nt_v4i(tc + q * 256 + 4 * lane);
+        const v2d va = ld_nt_v2d(tv + (2 * q) * 128 + 2 * lane);
+        const v2d vb = ld_nt_v2d(tv + (2 * q + 1) * 128 + 2 * lane);
+        p[4 * q + 0] = va.x * x[c.x];
+        p[4 * q + 1] = va.y * x[c.y];
+        p[4 * q + 2] = vb.x * x[c.z];
+        p[4 * q + 3] = vb.y * x[c.w];
+    }
+    if (t == ntiles - 1) {  // zero the padding past nnz (x[0] may be inf/nan)
+        const long long e0 = t * kC5Tile + (long long)lane * kC5Sigma;
+#pragma unroll
+        for (int k = 0; k < kC5Sigma; ++k)
+            if (e0 + k >= nnz) p[k] = 0.0;
+    }
+
+    // Exclusive prefix count of row starts over lanes -> segment index base.
+    const int cnt = __popc(f);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const int segbase = incl - cnt;
+    const uint32_t f0 = __shfl(f, 0, 64);
+    const int first_row = (f0 & 1u) ? r0 : r0 + 1;  // row of segment 0 (no gaps)
+    const int soff = gap ? seg_off[t] : 0;
+
+    double head = 0.0, sum = 0.0;
+    int seg = -1;
+#pragma unroll
+    for (int k = 0; k < kC5Sigma; ++k) {
+        if ((f >> k) & 1u) {
+            if (seg < 0) {
+                head = sum;
+                seg = segbase;
+            } else {
+                const int row = gap ? seg_row[soff + seg] : first_row + seg;
+                y[row] = kBeta ? alpha * sum + beta * y[row] : alpha * sum;
+                ++seg;
+            }
+            sum = 0.0;
+        }
+        sum += p[k];
+    }
+    const bool has = seg >= 0;
+    if (!has) head = sum;
+
+    // Suffix segmented scan: S_l = head_l + (has_l ? 0 : S_{l+1}).
+    double S = head;
+    bool stop = has;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double vS = __shfl_down(S, off, 64);
+        const int vstop = __shfl_down((int)stop, off, 64);
+        if (!stop) {
+            if (lane + off < 64) {
+                S += vS;
+                stop = vstop != 0;
+            } else {
+                stop = true;
+            }
+        }
+    }
+    double Snext = __shfl_down(S, 1, 64);
+    if (lane == 63) Snext = 0.0;
+    if (has) {
+        const int row = gap ? seg_row[soff + seg] : first_row + seg;
+        const double tot = sum + Snext;
+        y[row] = kBeta ? alpha * tot + beta * y[row] : alpha * tot;
+    }
+    if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
+}
+
+// Adds each tile's head (the part of the row that started in an earlier
+// tile) to y, one thread per run of tiles sharing that row: deterministic.
+__global__ void k_csr5_calibrate(const int *__restrict__ tile_row,
+                                 const uint32_t *__restrict__ flags,
+                                 const double *__restrict__ carry, long long ntiles,
+                                 double alpha, double *__restrict__ y)
+{
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    auto has_head = [&](long long u) { return (flags[u * 64] & 1u) == 0u; };
+    if (!has_head(t)) return;
+    const int R = tile_row[t] & 0x7fffffff;
+    if (t > 0 && (tile_row[t - 1] & 0x7fffffff) == R && has_head(t - 1)) return;
+    double s = 0.0;
+    for (long long u = t; u < ntiles && (tile_row[u] & 0x7fffffff) == R && has_head(u); ++u)
+        s += carry[u];
+    y[R] += alpha * s;
+}
+
+template <bool kBeta>
+__global__ void k_empty_rows(const int *__restrict__ rows, int n, double beta,
+                             double *__restrict__ y)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = rows[i];
+    y[r] = kBeta ? beta * y[r] : 0.0;
+}
+
+int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.c5.ready) return SBLAS_OK;
+    DeviceGuard g(A.device);
+    Csr5Plan &P = A.c5;
+    const long long nnz = A.nnz;
+    const std::vector<int> &rp = A.h_rowptr;
+    P.ntiles = (nnz + kC5Tile - 1) / kC5Tile;
+    const long long nt = P.ntiles;
+    std::vector<uint32_t> flags((size_t)nt * 64, 0u);
+    std::vector<int> empty;
+    for (int r = 0; r < A.m; ++r) {
+        const int a = rp[r], b = rp[r + 1];
+        if (a == b) {
+            empty.push_back(r);
+            continue;
+        }
+        const long long t = a / kC5Tile;
+        const int w = (int)(a - t * kC5Tile);
+        flags[(size_t)t * 64 + w / kC5Sigma] |= 1u << (w % kC5Sigma);
+    }
+    // tile_row: row holding the tile's first element (last r with rp[r] <= e)
+    std::vector<int> trow((size_t)nt + 1, A.m);
+    std::vector<int> seg_off((size_t)nt + 1, 0);
+    std::vector<int> seg_row;
+    int r = 0;
+    for (long long t = 0; t < nt; ++t) {
+        const long long e = t * kC5Tile;
+        while (r < A.m && rp[r + 1] <= e) ++r;
+        const int rfirst = r;
+        // last row of tile
+        const long long elast = std::min(nnz, e + kC5Tile) - 1;
+        int rl = r;
+        while (rl < A.m && rp[rl + 1] <= elast) ++rl;
+        int nstarts = 0;
+        for (int l = 0; l < 64; ++l) nstarts += __builtin_popcount(flags[(size_t)t * 64 + l]);
+        const bool start0 = flags[(size_t)t * 64] & 1u;
+        const int expected = rl - rfirst + (start0 ? 1 : 0);
+        trow[t] = rfirst;
+        seg_off[t] = (int)seg_row.size();
+        if (nstarts != expected) {
+            trow[t] = rfirst | (int)0x80000000u;
+            for (int q = (start0 ? rfirst : rfirst + 1); q <= rl; ++q)
+                if (rp[q + 1] > rp[q] && rp[q] >= e && rp[q] <= elast) seg_row.push_back(q);
+        }
+    }
+    seg_off[nt] = (int)seg_row.size();
+    P.nempty = (int)empty.size();
+
+    SBLAS_HIP(hipMalloc(&P.tile_row, sizeof(int) * (nt + 1)));
+    SBLAS_HIP(hipMalloc(&P.flags, sizeof(uint32_t) * std::max<long long>(nt * 64, 1)));
+    SBLAS_HIP(hipMalloc(&P.tval, sizeof(double) * std::max<long long>(nt * kC5Tile, 1)));
+    SBLAS_HIP(hipMalloc(&P.tcol, sizeof(int) * std::max<long long>(nt * kC5Tile, 1)));
+    SBLAS_HIP(hipMalloc(&P.seg_off, sizeof(int) * (nt + 1)));
+    SBLAS_HIP(hipMalloc(&P.seg_row, sizeof(int) * std::max<size_t>(seg_row.size(), 1)));
+    SBLAS_HIP(hipMalloc(&P.empty_rows, sizeof(int) * std::max<size_t>(empty.size(), 1)));
+    SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
+    SBLAS_HIP(hipMemcpyAsync(P.tile_row, trow.data(), sizeof(int) * (nt + 1), hipMemcpyHostToDevice, s));
+    if (nt) SBLAS_HIP(hipMemcpyAsync(P.flags, flags.data(), sizeof(uint32_t) * nt * 64, hipMemcpyHostToDevice, s));
+    SBLAS_HIP(hipMemcpyAsync(P.seg_off, seg_off.data(), sizeof(int) * (nt + 1), hipMemcpyHostToDevice, s));
+    if (!seg_row.empty())
+        SBLAS_HIP(hipMemcpyAsync(P.seg_row, seg_row.data(), sizeof(int) * seg_row.size(), hipMemcpyHostToDevice, s));
+    if (!empty.empty())
+        SBLAS_HIP(hipMemcpyAsync(P.empty_rows, empty.data(), sizeof(int) * empty.size(), hipMemcpyHostToDevice, s));
+    const long long total = nt * kC5Tile;
+    if (total) {
+        hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                           A.col, A.val, nnz, total, P.tcol, P.tval);
+        SBLAS_HIP(hipGetLastError());
+    }
+    SBLAS_HIP(hipStreamSynchronize(s));
+    P.ready = true;
+    return SBLAS_OK;
+}
+
+int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
+                     double beta, double *y, hipStream_t s)
+{
+    const Csr5Plan &P = A.c5;
+    if (!P.ready) return SBLAS_ERR_INVALID;
+    if (P.ntiles) {
+        const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmv_csr5<true>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
+                               P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
+                               beta, y, P.carry);
+        else
+            hipLaunchKernelGGL(k_spmv_csr5<false>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
+                               P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
+                               beta, y, P.carry);
+        hipLaunchKernelGGL(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
+                           0, s, P.tile_row, P.flags, P.carry, P.ntiles, alpha, y);
+    }
+    if (P.nempty) {
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_empty_rows<true>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
+                               P.empty_rows, P.nempty, beta, y);
+        else
+            hipLaunchKernelGGL(k_empty_rows<false>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
+                               P.empty_rows, P.nempty, beta, y);
+    }
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+void free_plans(sblas_csr_s &A)
+{
+    DeviceGuard g(A.device);
+    (void)hipFree(A.rs.blocks);
+    (void)hipFree(A.rs.long_rows);
+    (void)hipFree(A.rs.partial);
+    A.rs = RsPlan{};
+    Csr5Plan &P = A.c5;
+    (void)hipFree(P.tile_row);
+    (void)hipFree(P.flags);
+    (void)hipFree(P.tval);
+    (void)hipFree(P.tcol);
+    (void)hipFree(P.seg_off);
+    (void)hipFree(P.seg_row);
+    (void)hipFree(P.empty_rows);
+    (void)hipFree(P.carry);
+    A.c5 = Csr5Plan{};
+}
+
+}  // namespace sblas

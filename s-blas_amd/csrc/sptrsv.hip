@@ -1,0 +1,318 @@
+// sptrsv.hip -- sync-free sparse triangular solve for gfx950.
+//
+// Replaces sptrsv_syncfree_cuda_analyser / _executor
+// (sptrsv/sptrsv_v1/src/sptrsv_syncfree_cuda.h:10-167).
+//
+// Forward progress on CDNA: there is no independent thread scheduling and
+// dispatch order is not a contract, so a wave must never wait on work that
+// has not been handed to a running wave.  Both executors therefore take
+// their columns/rows from a monotone ticket (one device-scope atomicAdd):
+// everything a waiting wave depends on was ticketed earlier, by a wave that
+// is already resident, and the earliest unfinished item can always proceed.
+// Every spin is bounded (timeout word -> SBLAS_ERR_HIP instead of a hang).
+//
+// Cross-workgroup visibility (MI355X: per-XCD L2s, per-CU L1):
+//   * push (algo 0, the reference's CSC scatter): left_sum updates are
+//     device-scope fp64 atomic adds (performed at the memory side), then
+//     `s_waitcnt vmcnt(0)`, then the in-degree counters are bumped; the
+//     consumer polls its counter with an sc1 (L1-bypassing) load and reads
+//     left_sum with an sc1 load -- no L2 write-back fence per column.
+//   * pull (algo 1, CSR with ready flags): x_i is stored sc1, drained with
+//     `s_waitcnt vmcnt(0)`, then ready[i] is stored sc1; consumers poll the
+//     flag sc1 and load x sc1.  No float atomics: sums are deterministic.
+//     One LANE per row; lanes never block inside an iteration, so rows that
+//     depend on rows of the same wave resolve across iterations.
+#include <algorithm>
+#include <vector>
+
+#include "sblas_internal.hpp"
+
+struct sblas_trsv_s {
+    int device = 0;
+    int n = 0, nnz = 0;
+    int substitution = 0;
+    // CSC (input layout; push executor)
+    int *colptr = nullptr, *rowidx = nullptr;
+    double *val = nullptr;
+    int *in_degree = nullptr;  // per row: entries in the row (incl. diagonal)
+    // CSR (pull executor): built lazily with the device transpose
+    int *rrowptr = nullptr, *rcol = nullptr;
+    double *rval = nullptr;
+    // scratch
+    int *done = nullptr;       // push: arrivals per row; pull: ready flags
+    double *left = nullptr;    // push: left sums
+    unsigned *ctl = nullptr;   // [0] ticket, [1] timeout flag (16-byte block)
+    int nlevels = -1;
+};
+
+namespace sblas {
+
+constexpr unsigned kSpinLimit = 1u << 26;
+
+__device__ __forceinline__ int ld_sc1_i32(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_f64(const double *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_trsv_indegree(const int *__restrict__ rowidx, int nnz, int *__restrict__ deg)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nnz) atomicAdd(&deg[rowidx[e]], 1);
+}
+
+// ---- push: one wave per column, reference dataflow -----------------------
+__global__ __launch_bounds__(256) void k_trsv_push(
+    const int *__restrict__ colptr, const int *__restrict__ rowidx,
+    const double *__restrict__ val, const int *__restrict__ in_degree, int n,
+    int backward, const double *__restrict__ b, double *__restrict__ x, int *done,
+    double *left, unsigned *ctl)
+{
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = (int)atomicAdd(&ctl[0], 1u);
+        t = __shfl(t, 0, 64);
+        if (t >= n) return;
+        const int i = backward ? n - 1 - t : t;
+        const int a = colptr[i], e = colptr[i + 1];
+        const int dpos = backward ? e - 1 : a;
+        const double diag = val[dpos];
+        const int need = in_degree[i] - 1;
+        // wait for all left contributions (one lane polls)
+        if (lane == 0) {
+            unsigned spins = 0;
+            while (ld_sc1_i32(&done[i]) != need) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {
+                    atomicOr(&ctl[1], 1u);
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double xi = 0.0;
+        if (lane == 0) {
+            xi = (b[i] - ld_sc1_f64(&left[i])) / diag;
+            x[i] = xi;
+        }
+        xi = __shfl(xi, 0, 64);
+        const int lo = backward ? a : a + 1, hi = backward ? e - 1 : e;
+        for (int j = lo + lane; j < hi; j += 64)
+            (void)__hip_atomic_fetch_add(&left[rowidx[j]], xi * val[j], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int j = lo + lane; j < hi; j += 64)
+            (void)__hip_atomic_fetch_add(&done[rowidx[j]], 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ---- pull: one lane per row over CSR, ready flags -------------------------
+// Row layout: forward (lower) = off-diagonals ascending, diagonal LAST;
+// backward (upper, rows processed from n-1 down) = diagonal FIRST.
+__global__ __launch_bounds__(256) void k_trsv_pull(
+    const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, int n, int backward, const double *__restrict__ b,
+    double *x, int *ready, unsigned *ctl)
+{
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        int t0 = 0;
+        if (lane == 0) t0 = (int)atomicAdd(&ctl[0], 64u);
+        t0 = __shfl(t0, 0, 64);
+        if (t0 >= n) return;
+        const int t = t0 + lane;
+        const bool live = t < n;
+        const int i = live ? (backward ? n - 1 - t : t) : 0;
+        int j = 0, jend = 0;
+        double diag = 1.0, sum = 0.0;
+        if (live) {
+            const int a = rowptr[i], e = rowptr[i + 1];
+            if (backward) {
+                diag = val[a];
+                j = a + 1;
+                jend = e;
+            } else {
+                diag = val[e - 1];
+                j = a;
+                jend = e - 1;
+            }
+        }
+        bool pending = live;
+        unsigned spins = 0;
+        while (__any(pending)) {
+            if (pending) {
+                // consume every dependency that is already available
+                while (j < jend) {
+                    const int c = col[j];
+                    if (ld_sc1_i32(&ready[c]) == 0) break;
+                    sum += val[j] * ld_sc1_f64(&x[c]);
+                    ++j;
+                }
+                if (j == jend) {
+                    const double xi = (b[i] - sum) / diag;
+                    __hip_atomic_store(&x[i], xi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&ready[i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pending = false;
+                }
+            }
+            if (__any(pending)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kSpinLimit) {
+                    if (lane == 0) atomicOr(&ctl[1], 1u);
+                    break;
+                }
+            }
+        }
+    }
+}
+
+static int grid_for(int dev)
+{
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 1024;
+    return p.multiProcessorCount * 4;  // resident 256-thread workgroups, margin kept
+}
+
+}  // namespace sblas
+
+using namespace sblas;
+
+extern "C" {
+
+int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz, const int *d_colptr,
+                      const int *d_rowidx, const double *d_val, int substitution, void *stream)
+{
+    if (!out || n < 0 || nnz < n || (substitution != 0 && substitution != 1)) return SBLAS_ERR_INVALID;
+    int phys;
+    SBLAS_TRY(resolve_device(device, &phys));
+    DeviceGuard g(phys);
+    hipStream_t s = (hipStream_t)stream;
+    auto *T = new sblas_trsv_s();
+    T->device = phys;
+    T->n = n;
+    T->nnz = nnz;
+    T->substitution = substitution;
+    auto fail = [&](hipError_t e) {
+        set_error("sblas_trsv_create: %s", hipGetErrorString(e));
+        sblas_trsv_destroy(T);
+        return SBLAS_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&T->colptr, sizeof(int) * ((size_t)n + 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->rowidx, sizeof(int) * std::max(nnz, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->val, sizeof(double) * std::max(nnz, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->in_degree, sizeof(int) * std::max(n, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->done, sizeof(int) * std::max(n, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->left, sizeof(double) * std::max(n, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->ctl, 16)) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(T->colptr, d_colptr, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(e);
+    if (nnz) {
+        if ((e = hipMemcpyAsync(T->rowidx, d_rowidx, sizeof(int) * nnz, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(e);
+        if ((e = hipMemcpyAsync(T->val, d_val, sizeof(double) * nnz, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(e);
+    }
+    if ((e = hipMemsetAsync(T->in_degree, 0, sizeof(int) * std::max(n, 1), s)) != hipSuccess) return fail(e);
+    if (nnz) hipLaunchKernelGGL(k_trsv_indegree, dim3((nnz + 255) / 256), dim3(256), 0, s, T->rowidx, nnz, T->in_degree);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    // CSR copy for the pull executor: transpose of the CSC (= CSC of L^T).
+    sblas_csr_s csc;
+    csc.device = phys;
+    csc.m = n;  // "rows" of the CSC-as-CSR are L's columns
+    csc.n = n;
+    csc.nnz = nnz;
+    csc.rowptr = T->colptr;
+    csc.col = T->rowidx;
+    csc.val = T->val;
+    if ((e = hipMalloc(&T->rrowptr, sizeof(int) * ((size_t)n + 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->rcol, sizeof(int) * std::max(nnz, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->rval, sizeof(double) * std::max(nnz, 1))) != hipSuccess) return fail(e);
+    int st = launch_transpose(csc, T->rrowptr, T->rcol, T->rval, s);
+    csc.rowptr = nullptr;
+    csc.col = nullptr;
+    csc.val = nullptr;
+    if (st != SBLAS_OK) {
+        sblas_trsv_destroy(T);
+        return st;
+    }
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
+    *out = T;
+    return SBLAS_OK;
+}
+
+int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, void *stream)
+{
+    if (!T || !d_b || !d_x || (algo != 0 && algo != 1)) return SBLAS_ERR_INVALID;
+    if (T->n == 0) return SBLAS_OK;
+    DeviceGuard g(T->device);
+    hipStream_t s = (hipStream_t)stream;
+    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, 16, s));
+    SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
+    const int grid = grid_for(T->device);
+    if (algo == 0) {
+        SBLAS_HIP(hipMemsetAsync(T->left, 0, sizeof(double) * T->n, s));
+        hipLaunchKernelGGL(k_trsv_push, dim3(grid), dim3(256), 0, s, T->colptr, T->rowidx, T->val,
+                           T->in_degree, T->n, T->substitution, d_b, d_x, T->done, T->left, T->ctl);
+    } else {
+        hipLaunchKernelGGL(k_trsv_pull, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
+                           T->n, T->substitution, d_b, d_x, T->done, T->ctl);
+    }
+    SBLAS_HIP(hipGetLastError());
+    unsigned h[4] = {0, 0, 0, 0};
+    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, 16, hipMemcpyDeviceToHost, s));
+    SBLAS_HIP(hipStreamSynchronize(s));
+    if (h[1]) {
+        set_error("sptrsv: spin limit exceeded (matrix not triangular or missing diagonal?)");
+        return SBLAS_ERR_HIP;
+    }
+    return SBLAS_OK;
+}
+
+int sblas_trsv_levels(sblas_trsv T, int *nlevel)
+{
+    if (!T || !nlevel) return SBLAS_ERR_INVALID;
+    if (T->nlevels < 0) {
+        DeviceGuard g(T->device);
+        std::vector<int> cp((size_t)T->n + 1), ri((size_t)T->nnz);
+        SBLAS_HIP(hipMemcpy(cp.data(), T->colptr, sizeof(int) * cp.size(), hipMemcpyDeviceToHost));
+        if (T->nnz) SBLAS_HIP(hipMemcpy(ri.data(), T->rowidx, sizeof(int) * ri.size(), hipMemcpyDeviceToHost));
+        std::vector<int> lev((size_t)T->n, 0);
+        int nl = 0;
+        for (int k = 0; k < T->n; ++k) {
+            const int i = T->substitution ? T->n - 1 - k : k;
+            const int li = lev[(size_t)i];
+            nl = std::max(nl, li + 1);
+            for (int j = cp[(size_t)i]; j < cp[(size_t)i + 1]; ++j)
+                if (ri[(size_t)j] != i) lev[(size_t)ri[(size_t)j]] = std::max(lev[(size_t)ri[(size_t)j]], li + 1);
+        }
+        T->nlevels = nl;
+    }
+    *nlevel = T->nlevels;
+    return SBLAS_OK;
+}
+
+int sblas_trsv_destroy(sblas_trsv T)
+{
+    if (!T) return SBLAS_OK;
+    {
+        DeviceGuard g(T->device);
+        (void)hipFree(T->colptr);
+        (void)hipFree(T->rowidx);
+        (void)hipFree(T->val);
+        (void)hipFree(T->in_degree);
+        (void)hipFree(T->rrowptr);
+        (void)hipFree(T->rcol);
+        (void)hipFree(T->rval);
+        (void)hipFree(T->done);
+        (void)hipFree(T->left);
+        (void)hipFree(T->ctl);
+    }
+    delete T;
+    return SBLAS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,275 @@
+// transpose.hip -- device CSR -> CSC transpose with bit-exact indices.
+//
+// Semantics of sptrsv/sptrsv_v1/src/tranpose.h:6-43 (matrix_transposition):
+// column histogram, exclusive scan, then a STABLE scatter in row order, so
+// row indices ascend inside every column and equal-(row,col) duplicates keep
+// their CSR order.  GPU form:
+//   1. histogram of columns (int atomics) into colptr[c+1];
+//   2. in-place inclusive scan (multi-block, recursive) -> colptr;
+//   3. scatter the CSR element index e of every nonzero to an atomic slot of
+//      its column (order inside a column is arbitrary here);
+//   4. segmented sort of each column's element indices (e ascending == CSR
+//      order == the reference's stable order): per-thread insertion sort for
+//      short columns, LDS bitonic sort per workgroup up to 4096, a
+//      global-memory merge sort per workgroup beyond;
+//   5. gather: rowidx = row of e (binary search of rowptr), cval = val[e].
+#include <algorithm>
+#include <climits>
+
+#include "sblas_internal.hpp"
+
+namespace sblas {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ int wave_incl_scan(int v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// Inclusive scan of each 2048-element tile; tile totals to bsum.
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(int *__restrict__ a, long long len,
+                                                             int *__restrict__ bsum)
+{
+    __shared__ int wtot[kScanThreads / 64];
+    const long long base = (long long)blockIdx.x * kScanTile + (long long)threadIdx.x * kScanItems;
+    int v[kScanItems];
+    int run = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const long long i = base + k;
+        run += (i < len) ? a[i] : 0;
+        v[k] = run;
+    }
+    const int incl = wave_incl_scan(run);
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) wtot[wid] = incl;
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wid; ++w) woff += wtot[w];
+    const int off = woff + incl - run;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const long long i = base + k;
+        if (i < len) a[i] = v[k] + off;
+    }
+    if (threadIdx.x == kScanThreads - 1) bsum[blockIdx.x] = woff + incl;
+}
+
+__global__ void k_scan_add(int *__restrict__ a, long long len, const int *__restrict__ bsum)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long tile = i / kScanTile;
+    if (i < len && tile > 0) a[i] += bsum[tile - 1];
+}
+
+// In-place inclusive scan; scratch must hold >= sum over levels of tiles.
+static int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s)
+{
+    if (len <= 0) return SBLAS_OK;
+    const long long tiles = (len + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, len, scratch);
+    if (tiles > 1) {
+        SBLAS_TRY(scan_inclusive(scratch, tiles, scratch + tiles, s));
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, a, len,
+                           scratch);
+    }
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+__global__ void k_col_hist(const int *__restrict__ col, long long nnz, int *__restrict__ cnt1)
+{
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nnz) atomicAdd(&cnt1[col[e] + 1], 1);
+}
+
+__global__ void k_col_scatter(const int *__restrict__ col, long long nnz, int *__restrict__ next,
+                              int *__restrict__ perm)
+{
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nnz) perm[atomicAdd(&next[col[e]], 1)] = (int)e;
+}
+
+// Short columns sorted in place by their own thread; others queued.
+__global__ void k_sort_short(const int *__restrict__ colptr, int n, int *__restrict__ perm,
+                             int *__restrict__ qcount, int *__restrict__ qmed,
+                             int *__restrict__ qbig)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const int a = colptr[c], b = colptr[c + 1];
+    const int len = b - a;
+    if (len <= 32) {
+        for (int i = a + 1; i < b; ++i) {
+            const int key = perm[i];
+            int j = i - 1;
+            while (j >= a && perm[j] > key) {
+                perm[j + 1] = perm[j];
+                --j;
+            }
+            perm[j + 1] = key;
+        }
+    } else if (len <= 4096) {
+        qmed[atomicAdd(&qcount[0], 1)] = c;
+    } else {
+        qbig[atomicAdd(&qcount[1], 1)] = c;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sort_medium(const int *__restrict__ colptr,
+                                                     int *__restrict__ perm,
+                                                     const int *__restrict__ qcount,
+                                                     const int *__restrict__ qmed)
+{
+    __shared__ int sk[4096];
+    const int nq = qcount[0];
+    for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int c = qmed[q];
+        const int a = colptr[c], len = colptr[c + 1] - a;
+        int P = 64;
+        while (P < len) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += 256) sk[i] = i < len ? perm[a + i] : INT_MAX;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = threadIdx.x; i < P; i += 256) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const bool up = (i & k) == 0;
+                        const int x = sk[i], y = sk[ixj];
+                        if (up ? x > y : x < y) {
+                            sk[i] = y;
+                            sk[ixj] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = threadIdx.x; i < len; i += 256) perm[a + i] = sk[i];
+        __syncthreads();
+    }
+}
+
+// Bottom-up merge sort of one long column per workgroup in global memory
+// (ping-pong with tmp, same offsets).  Keys are unique.
+__global__ __launch_bounds__(256) void k_sort_big(const int *__restrict__ colptr,
+                                                  int *__restrict__ perm, int *__restrict__ tmp,
+                                                  const int *__restrict__ qcount,
+                                                  const int *__restrict__ qbig)
+{
+    const int nq = qcount[1];
+    for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int c = qbig[q];
+        const int a = colptr[c], len = colptr[c + 1] - a;
+        int *src = perm + a, *dst = tmp + a;
+        for (int w = 1; w < len; w <<= 1) {
+            for (int i = threadIdx.x; i < len; i += 256) {
+                const int run = i / (2 * w);
+                const int s0 = run * 2 * w;
+                const int m0 = min(s0 + w, len), e0 = min(s0 + 2 * w, len);
+                const int key = src[i];
+                int pos;
+                if (i < m0) {  // left run: count right-run keys < key
+                    int lo = m0, hi = e0;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (src[mid] < key) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    pos = s0 + (i - s0) + (lo - m0);
+                } else {  // right run: count left-run keys < key
+                    int lo = s0, hi = m0;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (src[mid] < key) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    pos = s0 + (i - m0) + (lo - s0);
+                }
+                dst[pos] = key;
+            }
+            __syncthreads();
+            int *t = src;
+            src = dst;
+            dst = t;
+        }
+        if (src != perm + a)
+            for (int i = threadIdx.x; i < len; i += 256) perm[a + i] = src[i];
+        __syncthreads();
+    }
+}
+
+__global__ void k_gather_csc(const int *__restrict__ rowptr, int m, const double *__restrict__ val,
+                             const int *__restrict__ perm, long long nnz, int *__restrict__ rowidx,
+                             double *__restrict__ cval)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nnz) return;
+    const int e = perm[p];
+    int lo = 0, hi = m - 1;  // row r: rowptr[r] <= e < rowptr[r+1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rowptr[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    if (rowidx) rowidx[p] = lo;
+    if (cval) cval[p] = val[e];
+}
+
+struct TransposeScratch {
+    int *buf = nullptr;
+    size_t ints = 0;
+};
+static thread_local TransposeScratch g_tscratch[64];
+
+int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cval, hipStream_t s)
+{
+    const long long nnz = A.nnz;
+    const int n = A.n;
+    SBLAS_HIP(hipMemsetAsync(colptr, 0, sizeof(int) * ((size_t)n + 1), s));
+    if (nnz == 0) return SBLAS_OK;
+    // scratch: next[n+1] | perm[nnz] | tmp[nnz] | q[2] | qmed[n] | qbig[n] | scan
+    const size_t scan_ints = (size_t)((n + 1) / kScanTile + 64) * 2;
+    const size_t need = (size_t)(n + 1) + 2 * (size_t)nnz + 4 + 2 * (size_t)n + scan_ints;
+    TransposeScratch &S = g_tscratch[A.device & 63];
+    if (S.ints < need) {
+        (void)hipFree(S.buf);
+        S.buf = nullptr;
+        S.ints = 0;
+        SBLAS_HIP(hipMalloc(&S.buf, need * sizeof(int)));
+        S.ints = need;
+    }
+    int *next = S.buf;
+    int *perm = next + (n + 1);
+    int *tmp = perm + nnz;
+    int *qc = tmp + nnz;
+    int *qmed = qc + 4;
+    int *qbig = qmed + n;
+    int *scan = qbig + n;
+    const unsigned gb = (unsigned)((nnz + 255) / 256);
+    hipLaunchKernelGGL(k_col_hist, dim3(gb), dim3(256), 0, s, A.col, nnz, colptr);
+    SBLAS_TRY(scan_inclusive(colptr, (long long)n + 1, scan, s));
+    SBLAS_HIP(hipMemcpyAsync(next, colptr, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_col_scatter, dim3(gb), dim3(256), 0, s, A.col, nnz, next, perm);
+    SBLAS_HIP(hipMemsetAsync(qc, 0, sizeof(int) * 4, s));
+    hipLaunchKernelGGL(k_sort_short, dim3((n + 255) / 256), dim3(256), 0, s, colptr, n, perm, qc,
+                       qmed, qbig);
+    hipLaunchKernelGGL(k_sort_medium, dim3(1024), dim3(256), 0, s, colptr, perm, qc, qmed);
+    hipLaunchKernelGGL(k_sort_big, dim3(256), dim3(256), 0, s, colptr, perm, tmp, qc, qbig);
+    hipLaunchKernelGGL(k_gather_csc, dim3(gb), dim3(256), 0, s, A.rowptr, A.m, A.val, perm, nnz,
+                       rowidx, cval);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+}  // namespace sblas

@@ -1,0 +1,273 @@
+"""sblas -- Python view of libsblas.so (the MI355X-native sparse-BLAS hot path).
+
+Thin ctypes binding of include/sblas.h.  This is the host-side mirror the
+tests and bench.py drive; all compute happens in libsblas.so's HIP kernels.
+Importing fails loudly when the library has not been built -- there is no
+CPU fallback anywhere on the product path.
+
+Device arrays are passed as raw pointers: torch tensors (``t.data_ptr()``)
+serve as device memory and ``torch.cuda.Stream.cuda_stream`` as the stream
+handle, so torch is only plumbing (allocation, streams, torch.distributed).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsblas.so")
+
+ROWSPLIT = 1  # test_spmv kernel 1 (csrmv)
+CSR5 = 2      # test_spmv kernel 2/3 (csrmv_mp / CSR5)
+
+_STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error",
+           3: "insufficient device memory", 4: "no device", 5: "unsupported",
+           6: "RCCL error", 7: "I/O error", -1: "footprint > 0.8 x free memory"}
+
+
+class SblasError(RuntimeError):
+    pass
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise SblasError(
+            f"{LIB_PATH} missing: build it with `make -C s-blas_amd` "
+            "(or __graft_entry__.build()); there is no fallback path")
+    return C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+
+
+lib = _load()
+
+_p = C.c_void_p
+_i = C.c_int
+_ll = C.c_longlong
+_d = C.c_double
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("sblas_status_string", C.c_char_p, _i)
+_sig("sblas_last_error", C.c_char_p)
+_sig("sblas_version", _i)
+_sig("sblas_device_count", _i, _p)
+_sig("sblas_spMV_mgpu_baseline", _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _i)
+_sig("sblas_spMV_mgpu_v1", _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _i, _i)
+_sig("sblas_spMV_mgpu_v2", _i, _i, _i, _ll, _p, _p, _p, _p, _p, _p, _p, _i, _i, _ll, _i)
+_sig("sblas_get_row_from_index", _i, _i, _p, _ll)
+_sig("sblas_get_time", _d)
+_sig("sblas_get_gpu_availble_mem", _d, _i)
+_sig("sblas_csrmm_mgpu", _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _i)
+_sig("sblas_sptrsv_syncfree", _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i)
+_sig("sblas_csr_upload_slice", _i, _p, _i, _i, _p, _p, _p, _i, _i, _ll, _ll, _p)
+_sig("sblas_csr_from_device", _i, _p, _i, _i, _i, _i, _p, _p, _p, _p)
+_sig("sblas_csr_destroy", _i, _p)
+_sig("sblas_csr_info", _i, _p, _p, _p, _p)
+_sig("sblas_csr_analyse", _i, _p, _i, _p)
+_sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
+_sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
+_sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
+_sig("sblas_csr_transpose", _i, _p, _p, _p, _p, _p)
+_sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
+_sig("sblas_trsv_solve", _i, _p, _i, _p, _p, _p)
+_sig("sblas_trsv_levels", _i, _p, _p)
+_sig("sblas_trsv_destroy", _i, _p)
+_sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _p)
+_sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
+_sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
+_sig("sblas_partition_rowblock", _i, _i, _i, _p)
+_sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
+_sig("sblas_gen_synth_rows", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _i, _i, _p, _p)
+_sig("sblas_gen_vector", _i, _i, C.c_ulonglong, _p)
+
+
+def check(st: int, what: str = "") -> None:
+    if st != 0:
+        msg = _STATUS.get(st, str(st))
+        detail = lib.sblas_last_error().decode(errors="replace")
+        raise SblasError(f"{what}: {msg} ({detail})")
+
+
+def ptr(a) -> Optional[int]:
+    """Raw address of a numpy array or torch tensor (None passes NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    lib.sblas_device_count(C.byref(c))
+    return c.value
+
+
+# --------------------------------------------------------------------------
+# host utilities
+# --------------------------------------------------------------------------
+def mm_read(path: str, mode: int = 0):
+    """Matrix-Market -> (m, n, rowptr int64, col int32, val f64).
+    mode 0 = mmio_data semantics, 1 = test_spmv 'f', 2 = test_spmv 'b'."""
+    m, n, nnz = C.c_int(), C.c_int(), C.c_longlong()
+    check(lib.sblas_mm_read(path.encode(), mode, C.byref(m), C.byref(n), C.byref(nnz),
+                            None, None, None), f"mm_read {path}")
+    rp = np.zeros(m.value + 1, np.int64)
+    ci = np.zeros(max(nnz.value, 1), np.int32)
+    v = np.zeros(max(nnz.value, 1), np.float64)
+    check(lib.sblas_mm_read(path.encode(), mode, C.byref(m), C.byref(n), C.byref(nnz),
+                            ptr(rp), ptr(ci), ptr(v)), f"mm_read {path}")
+    return m.value, n.value, rp, ci[:nnz.value], v[:nnz.value]
+
+
+def partition_nnz(rowptr: np.ndarray, g: int):
+    m = len(rowptr) - 1
+    nnz = int(rowptr[-1])
+    si = np.zeros(g, np.int64); ei = np.zeros(g, np.int64)
+    sr = np.zeros(g, np.int32); er = np.zeros(g, np.int32); sf = np.zeros(g, np.int32)
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    check(lib.sblas_partition_nnz(m, nnz, ptr(rp), g, ptr(si), ptr(ei), ptr(sr), ptr(er), ptr(sf)),
+          "partition_nnz")
+    return si, ei, sr, er, sf
+
+
+def partition_rowblock(m: int, g: int) -> np.ndarray:
+    rs = np.zeros(g + 1, np.int32)
+    check(lib.sblas_partition_rowblock(m, g, ptr(rs)), "partition_rowblock")
+    return rs
+
+
+def gen_synth_rowptr(n: int, heavy: int = 96, light: int = 9) -> np.ndarray:
+    rp = np.zeros(n + 1, np.int64)
+    check(lib.sblas_gen_synth_rowptr(n, heavy, light, ptr(rp)), "gen_synth_rowptr")
+    return rp
+
+
+def gen_synth_rows(n: int, rowptr: np.ndarray, r0: int, r1: int, heavy: int = 96,
+                   light: int = 9, prefix: bool = False, seed: int = 42):
+    cnt = int(rowptr[r1] - rowptr[r0])
+    col = np.zeros(max(cnt, 1), np.int32)
+    val = np.zeros(max(cnt, 1), np.float64)
+    check(lib.sblas_gen_synth_rows(n, heavy, light, int(prefix), seed, ptr(rowptr), r0, r1,
+                                   ptr(col), ptr(val)), "gen_synth_rows")
+    return col[:cnt], val[:cnt]
+
+
+def gen_vector(n: int, seed: int) -> np.ndarray:
+    v = np.zeros(max(n, 1), np.float64)
+    check(lib.sblas_gen_vector(n, seed, ptr(v)), "gen_vector")
+    return v[:n]
+
+
+# --------------------------------------------------------------------------
+# reference operator API (host arrays)
+# --------------------------------------------------------------------------
+def spmv_mgpu(version: str, m, n, rowptr, col, val, x, y, alpha, beta, ngpu=1, kernel=1,
+              nb=None, q=1) -> int:
+    """version in {'baseline','v1','v2'}; y updated in place (numpy)."""
+    a = np.array([alpha], np.float64)
+    b = np.array([beta], np.float64)
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    nnz = int(rp[-1])
+    args = (m, n, nnz, ptr(a), ptr(val), ptr(rp), ptr(col), ptr(x), ptr(b), ptr(y), ngpu)
+    if version == "baseline":
+        return lib.sblas_spMV_mgpu_baseline(*args)
+    if version == "v1":
+        return lib.sblas_spMV_mgpu_v1(*args, kernel)
+    if version == "v2":
+        return lib.sblas_spMV_mgpu_v2(*args, kernel, nb if nb else max(nnz, 1), q)
+    raise ValueError(version)
+
+
+# --------------------------------------------------------------------------
+# persistent device objects
+# --------------------------------------------------------------------------
+class DeviceCSR:
+    """A CSR slice resident on one GPU (sblas_csr handle)."""
+
+    def __init__(self, handle: int):
+        self.h = C.c_void_p(handle)
+
+    @classmethod
+    def upload_slice(cls, device: int, n: int, rowptr: np.ndarray, col: np.ndarray,
+                     val: np.ndarray, r0: int, r1: int, i0: int, i1: int, stream=None):
+        h = C.c_void_p()
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        check(lib.sblas_csr_upload_slice(C.byref(h), device, n, ptr(rp), ptr(col), ptr(val),
+                                         r0, r1, i0, i1, stream), "csr_upload_slice")
+        return cls(h.value)
+
+    @classmethod
+    def upload(cls, device: int, n: int, rowptr, col, val, stream=None):
+        m = len(rowptr) - 1
+        return cls.upload_slice(device, n, rowptr, col, val, 0, m, 0, int(rowptr[-1]), stream)
+
+    def info(self) -> Tuple[int, int, int]:
+        m, n, nnz = C.c_int(), C.c_int(), C.c_longlong()
+        check(lib.sblas_csr_info(self.h, C.byref(m), C.byref(n), C.byref(nnz)), "csr_info")
+        return m.value, n.value, nnz.value
+
+    def analyse(self, algo: int, stream=None) -> None:
+        check(lib.sblas_csr_analyse(self.h, algo, stream), "csr_analyse")
+
+    def spmv(self, algo: int, alpha: float, x_ptr: int, beta: float, y_ptr: int,
+             stream=None) -> None:
+        check(lib.sblas_spmv(self.h, algo, alpha, x_ptr, beta, y_ptr, stream), "spmv")
+
+    def spmm(self, ncols: int, alpha: float, b_ptr: int, ldb: int, b_layout: int, beta: float,
+             c_ptr: int, ldc: int, stream=None) -> None:
+        check(lib.sblas_spmm(self.h, ncols, alpha, b_ptr, ldb, b_layout, beta, c_ptr, ldc,
+                             stream), "spmm")
+
+    def transpose(self, colptr_ptr: int, rowidx_ptr: int, cval_ptr: int, stream=None) -> None:
+        check(lib.sblas_csr_transpose(self.h, colptr_ptr, rowidx_ptr, cval_ptr, stream),
+              "csr_transpose")
+
+    def algorithmic_bytes(self, beta_nonzero: bool) -> int:
+        return int(lib.sblas_spmv_algorithmic_bytes(self.h, int(beta_nonzero)))
+
+    def close(self) -> None:
+        if self.h:
+            lib.sblas_csr_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceTRSV:
+    def __init__(self, device, n, nnz, colptr_ptr, rowidx_ptr, val_ptr, substitution=0,
+                 stream=None):
+        self.h = C.c_void_p()
+        check(lib.sblas_trsv_create(C.byref(self.h), device, n, nnz, colptr_ptr, rowidx_ptr,
+                                    val_ptr, substitution, stream), "trsv_create")
+
+    def solve(self, algo: int, b_ptr: int, x_ptr: int, stream=None) -> None:
+        check(lib.sblas_trsv_solve(self.h, algo, b_ptr, x_ptr, stream), "trsv_solve")
+
+    def levels(self) -> int:
+        n = C.c_int()
+        check(lib.sblas_trsv_levels(self.h, C.byref(n)), "trsv_levels")
+        return n.value
+
+    def close(self) -> None:
+        if self.h:
+            lib.sblas_trsv_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,115 @@
+"""Host-side product code (libsblas, no GPU needed) vs the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.mark.parametrize("name", ["qh768", "ash85"])
+def test_mm_read_mmio_mode(sb, orc, name):
+    path = os.path.join(GOLDEN, f"{name}.mtx")
+    m, n, rp, col, val = sb.mm_read(path, 0)
+    m2, n2, rp2, col2, val2, _ = orc.load_mmio(path)
+    assert (m, n) == (m2, n2)
+    assert np.array_equal(rp, rp2.astype(np.int64))
+    assert np.array_equal(col, col2) and np.array_equal(val, val2)
+
+
+@pytest.mark.parametrize("mode,dt,name", [(1, "f", "qh768"), (2, "b", "ash85")])
+def test_mm_read_testspmv_modes(sb, orc, mode, dt, name):
+    path = os.path.join(GOLDEN, f"{name}.mtx")
+    m, n, rp, col, val = sb.mm_read(path, mode)
+    m2, n2, rp2, col2, val2 = orc.load_testspmv(path, dt)
+    assert np.array_equal(rp, rp2) and np.array_equal(col, col2) and np.array_equal(val, val2)
+
+
+def test_mm_read_errors(sb, tmp_path):
+    bad = tmp_path / "bad.mtx"
+    bad.write_text("not a matrix\n")
+    with pytest.raises(sb.SblasError):
+        sb.mm_read(str(bad))
+    with pytest.raises(sb.SblasError):
+        sb.mm_read(str(tmp_path / "missing.mtx"))
+    oob = tmp_path / "oob.mtx"
+    oob.write_text("%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1.0\n")
+    with pytest.raises(sb.SblasError):
+        sb.mm_read(str(oob))
+
+
+def test_mm_read_integer_complex(sb, orc, tmp_path):
+    p = tmp_path / "ic.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate integer symmetric\n% c\n3 3 3\n1 1 4\n3 1 -2\n3 2 7\n")
+    m, n, rp, col, val = sb.mm_read(str(p), 0)
+    m2, n2, rp2, col2, val2, _ = orc.load_mmio(str(p))
+    assert np.array_equal(rp, rp2) and np.array_equal(col, col2) and np.array_equal(val, val2)
+    p2 = tmp_path / "cx.mtx"
+    p2.write_text("%%MatrixMarket matrix coordinate complex general\n2 2 2\n1 2 1.5 9\n2 1 -3 1\n")
+    m, n, rp, col, val = sb.mm_read(str(p2), 0)
+    assert list(val) == [1.5, -3.0]
+
+
+def _rand_rowptr(rng, m, maxlen, empty_frac):
+    lens = rng.integers(0, maxlen, m)
+    lens[rng.random(m) < empty_frac] = 0
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_partition_nnz_matches_oracle(sb, orc, seed):
+    rng = np.random.default_rng(seed)
+    m = int(rng.integers(1, 500))
+    rp = _rand_rowptr(rng, m, int(rng.integers(1, 50)), [0.0, 0.3, 0.9][seed % 3])
+    if seed == 5:
+        rp[1:] += 5000  # a single giant first row spanning partitions
+    for g in (1, 2, 3, 5, 8, 13):
+        a = sb.partition_nnz(rp, g)
+        b = orc.partition_nnz(rp, g)
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+        si, ei, sr, er, sf = a
+        # every row covered, in order; continuation only when the row is split
+        covered = []
+        for d in range(g):
+            rows = list(range(sr[d], er[d] + 1))
+            if sf[d]:
+                assert covered and covered[-1] == sr[d]
+                rows = rows[1:]
+            covered += rows
+        assert covered == list(range(m))
+
+
+def test_partition_rowblock(sb, orc):
+    for m, g in [(10, 3), (2000000, 8), (5, 8), (0, 2)]:
+        rs = sb.partition_rowblock(m, g)
+        assert rs[0] == 0 and rs[-1] == m and np.all(np.diff(rs) >= 0)
+
+
+@pytest.mark.parametrize("prefix", [False, True])
+def test_generator_bit_exact(sb, orc, prefix):
+    n = 6000
+    rp = sb.gen_synth_rowptr(n)
+    rp2, col2, val2 = orc.gen_synth(n, prefix=prefix)
+    assert np.array_equal(rp, rp2)
+    col, val = sb.gen_synth_rows(n, rp, 0, n, prefix=prefix)
+    assert np.array_equal(col, col2) and np.array_equal(val, val2)
+    # slices generate the same rows
+    c1, v1 = sb.gen_synth_rows(n, rp, 700, 3100, prefix=prefix)
+    assert np.array_equal(c1, col2[rp[700]:rp[3100]]) and np.array_equal(v1, val2[rp[700]:rp[3100]])
+    if not prefix:
+        for r in (0, 5, n // 8 - 1, n // 8, n - 1):
+            seg = col[rp[r]:rp[r + 1]]
+            assert np.all(np.diff(seg) > 0) and seg.min() >= 0 and seg.max() < n
+
+
+def test_config2_shape(sb):
+    rp = sb.gen_synth_rowptr(2_000_000)
+    assert int(rp[-1]) == 39_750_000
+    assert np.array_equal(sb.gen_vector(1000, 43), __import__("orc").gen_vector(1000, 43))
+
+
+def test_get_row_from_index_fixed(sb):
+    rp = np.array([0, 2, 2, 2, 5, 7], np.int64)
+    assert sb.lib.sblas_get_row_from_index(5, sb.ptr(rp), 2) == 3
+    assert sb.lib.sblas_get_row_from_index(5, sb.ptr(rp), 6) == 4

@@ -1,0 +1,153 @@
+"""SpMV parity on the GPU: HIP kernels (via libsblas C-ABI) vs the oracle.
+
+Tolerance (DESIGN.md "Parity"): per row
+  |y_gpu - y_ref| <= 4*gamma_k*sum_j |alpha*a_ij*x_j| + 4u*|beta*y0|,
+gamma_k = k*u/(1-k*u), u = 2^-53, k = row length.  The reference's own abs
+1e-3 check (spmv/test/dspmv_test.cu:390-401) is asserted as well.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+ALGOS = [1, 2]
+
+
+def random_csr(rng, m, n, density_rows, long_rows=(), empty_frac=0.1):
+    lens = rng.integers(0, density_rows, size=m)
+    lens[rng.random(m) < empty_frac] = 0
+    for r, L in long_rows:
+        lens[r] = L
+    lens = np.minimum(lens, n)
+    rp = np.zeros(m + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    col = np.concatenate([np.sort(rng.choice(n, size=L, replace=False)) for L in lens]
+                         ).astype(np.int32) if rp[-1] else np.zeros(0, np.int32)
+    val = rng.standard_normal(int(rp[-1]))
+    return rp, col, val
+
+
+def run_gpu(torch, sb, algo, n, rp, col, val, x, alpha, beta, y0):
+    A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    xd = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    yd = torch.from_numpy(np.ascontiguousarray(y0)).cuda()
+    A.analyse(algo)
+    A.spmv(algo, alpha, xd.data_ptr(), beta, yd.data_ptr())
+    torch.cuda.synchronize()
+    out = yd.cpu().numpy()
+    A.close()
+    return out
+
+
+def check(orc, rp, col, val, x, alpha, beta, y0, got):
+    want = orc.csr_spmv(rp, col, val, x, alpha, beta, y0)
+    bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y0)
+    err = np.abs(got - want)
+    assert np.all(err <= bound), f"max excess {np.max(err - bound)} at {np.argmax(err - bound)}"
+    assert np.all(np.abs(got - want) <= 1e-3 * np.maximum(1.0, np.abs(want)))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_qh768(torch_cuda, sb, orc, algo, mode):
+    path = os.path.join(GOLDEN, "qh768.mtx")
+    m, n, rp, col, val = sb.mm_read(path, mode)
+    alpha, beta = orc.alpha_beta()
+    x = np.ones(n)
+    y0 = np.zeros(m)
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, alpha, beta, y0)
+    check(orc, rp, col, val, x, alpha, beta, y0, got)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("prefix", [False, True])
+def test_synthetic(torch_cuda, sb, orc, algo, prefix):
+    n = 20000
+    rp, col, val = orc.gen_synth(n, prefix=prefix)
+    x = orc.gen_vector(n, 43)
+    alpha, beta = orc.alpha_beta()
+    y0 = orc.gen_vector(n, 44)
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, alpha, beta, y0)
+    check(orc, rp, col, val, x, alpha, beta, y0, got)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("beta", [0.0, 0.75])
+def test_ragged_long_empty(torch_cuda, sb, orc, algo, beta):
+    rng = np.random.default_rng(7)
+    m, n = 3000, 40000
+    rp, col, val = random_csr(rng, m, n, 60, long_rows=[(5, 2049), (17, 8192), (900, 30000),
+                                                          (2999, 9000), (1500, 20000)])
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    if beta == 0.0:
+        y0[::7] = np.nan  # beta == 0 must not read y
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, 1.25, beta, y0)
+    y0c = np.where(np.isnan(y0), 0.0, y0)
+    check(orc, rp, col, val, x, 1.25, beta, y0c, got)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_edge_shapes(torch_cuda, sb, orc, algo):
+    rng = np.random.default_rng(3)
+    # all rows empty
+    m, n = 100, 50
+    rp = np.zeros(m + 1, np.int64)
+    got = run_gpu(torch_cuda, sb, algo, n, rp, np.zeros(0, np.int32), np.zeros(0), np.ones(n),
+                  2.0, 0.5, np.ones(m))
+    assert np.array_equal(got, np.full(m, 0.5))
+    # one dense row; many leading empty rows
+    for m, n in [(1, 1000), (5000, 1000)]:
+        rp = np.zeros(m + 1, np.int64)
+        rp[-1] = n
+        col = np.arange(n, dtype=np.int32)
+        val = rng.standard_normal(n)
+        x = rng.standard_normal(n)
+        y0 = rng.standard_normal(m)
+        got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, 0.5, -1.0, y0)
+        check(orc, rp, col, val, x, 0.5, -1.0, y0, got)
+    # rows of length 1 (tile boundaries everywhere), nnz not a multiple of 4
+    m = n = 4099
+    rp = np.arange(m + 1, dtype=np.int64)
+    col = rng.integers(0, n, size=m).astype(np.int32)
+    val = rng.standard_normal(m)
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, 1.0, 1.0, y0)
+    check(orc, rp, col, val, x, 1.0, 1.0, y0, got)
+
+
+def test_repeat_deterministic(torch_cuda, sb, orc):
+    n = 5000
+    rp, col, val = orc.gen_synth(n)
+    x = orc.gen_vector(n, 43)
+    outs = [run_gpu(torch_cuda, sb, a, n, rp, col, val, x, 1.0, 0.0, np.zeros(n))
+            for a in (1, 1, 2, 2)]
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[2], outs[3])
+
+
+@pytest.mark.parametrize("version", ["baseline", "v1", "v2"])
+@pytest.mark.parametrize("ngpu", [1, 2, 3, 8])
+def test_reference_api(torch_cuda, sb, orc, version, ngpu):
+    """spMV_mgpu_* drop-in (host pointers); ordinals wrap onto the box's GPU."""
+    rng = np.random.default_rng(11)
+    m, n = 2500, 3000
+    rp, col, val = random_csr(rng, m, n, 40, long_rows=[(10, 2500)])
+    x = rng.standard_normal(n)
+    alpha, beta = orc.alpha_beta()
+    y0 = rng.standard_normal(m)
+    for kernel in ([1] if version == "baseline" else [1, 2, 3]):
+        y = y0.copy()
+        nb = max(int(rp[-1]) // 5, 1) if version == "v2" else None
+        rc = sb.spmv_mgpu(version, m, n, rp, col, val, x, y, alpha, beta, ngpu=ngpu,
+                          kernel=kernel, nb=nb, q=2)
+        assert rc == 0
+        check(orc, rp, col, val, x, alpha, beta, y0, y)
+        if version != "v2":
+            y_ref_flow = orc.spmv_mgpu(version, m, n, rp, col, val, x, alpha, beta, y0, ngpu)
+            assert np.all(np.abs(y - y_ref_flow) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
