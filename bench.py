@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""bench.py -- fp64 CSR SpMV on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[1]): synthetic non-uniform
+n = 2e6 CSR, rows < n/8 hold 96 nnz and the rest 9 (nnz = 39,750,000),
+distinct uniform-random sorted columns (seed 42), values U[0,1), x U[0,1)
+(seed 43), y0 = 0, alpha/beta = the test_spmv constants (glibc rand(),
+0.8401877172 / 0.3943829268).  One step = one y = alpha*A*x + beta*y over
+the whole matrix with every input already resident in HBM; at N > 1 the
+matrix is split by nnz over the ranks (x replicated) and a step also
+includes the RCCL allgather of the y slices plus their device-side merge
+(strong scaling: the same matrix at every N).
+
+  python bench.py [--gpus N --steps K --warmup W] [--algo rowsplit|csr5]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
+launch (12*nnz + 4*(m+1) + 8*n + 8*m + 8*m[beta!=0]) / average
+duration of the SpMV kernel measured with HIP events on the launch stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "s-blas_amd"))
+
+METRIC = "fp64 CSR SpMV GFLOP/s + achieved HBM GB/s (% roofline) at 1/2/4/8 MI355X"
+ALPHA = 0.8401877171547095  # dspmv_test.cu:281 (glibc rand(), unseeded)
+BETA = 0.39438292681909304  # dspmv_test.cu:282
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
+    """Oracle restatement (oracle/liboracle.so) timed on this host's cores.
+    Only this leg of bench.py touches oracle/ (DESIGN.md)."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    f = lib.orc_csr_spmv_omp
+    f.restype = None
+    f.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                  C.c_double, C.c_void_p, C.c_int]
+    g = lib.orc_csr_spmv
+    g.restype = None
+    g.argtypes = f.argtypes[:-1]
+    y = np.zeros(m)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    args = (m, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data, x.ctypes.data, ALPHA, BETA,
+            y.ctypes.data)
+
+    def timeit(fn, extra, share):
+        fn(*args, *extra)  # warm-up
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn(*args, *extra)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > share or reps >= 200:
+                return reps, el / reps
+
+    r_mt, t_mt = timeit(f, (threads,), budget_s * 0.5)
+    r_st, t_st = timeit(g, (), budget_s * 0.5)
+    return {
+        "value": round(2.0 * nnz / t_mt / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
+        "kind": "port",
+        "sample": (f"full config-2 matrix, orc_csr_spmv_omp (OpenMP, schedule dynamic) x{r_mt} "
+                   f"reps, {t_mt * 1e3:.1f} ms/SpMV; single-core scalar port orc_csr_spmv "
+                   f"x{r_st}: {t_st * 1e3:.1f} ms/SpMV = {2.0 * nnz / t_st / 1e9:.3f} GFLOP/s"),
+        "single_core_value": round(2.0 * nnz / t_st / 1e9, 3),
+    }
+
+
+def pmc_traffic(algo_name: str):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary
+    (profiles/pmc_<algo>.json, written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{algo_name}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as fh:
+            return float(json.load(fh)["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--algo", choices=["rowsplit", "csr5"], default="rowsplit")
+    ap.add_argument("--n", type=int, default=2_000_000)
+    ap.add_argument("--heavy", type=int, default=96)
+    ap.add_argument("--light", type=int, default=9)
+    ap.add_argument("--cols", choices=["random", "prefix"], default="random")
+    ap.add_argument("--exchange", choices=["allgather", "allreduce"], default="allgather")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import sblas
+    import sblas_dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
+              file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    algo = sblas.ROWSPLIT if args.algo == "rowsplit" else sblas.CSR5
+    n = args.n
+    rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
+    nnz = int(rowptr[-1])
+    plan = sblas_dist.make_plan(rowptr, n, world)
+    r0, r1, i0, i1, _ = plan.local(rank)
+    t_gen = time.perf_counter()
+    col_rows, val_rows = sblas.gen_synth_rows(n, rowptr, r0, r1, args.heavy, args.light,
+                                              prefix=args.cols == "prefix", seed=42)
+    off = i0 - int(rowptr[r0])
+    col = np.ascontiguousarray(col_rows[off:off + (i1 - i0)])
+    val = np.ascontiguousarray(val_rows[off:off + (i1 - i0)])
+    t_gen = time.perf_counter() - t_gen
+    x_h = sblas.gen_vector(n, 43)
+    x = torch.from_numpy(x_h).to(dev)
+
+    stream = torch.cuda.Stream(device=dev)
+    sp = stream.cuda_stream
+    op = sblas_dist.DistSpMV(plan, rank, local_rank, rowptr, col, val, algo, torch, dist,
+                             args.exchange)
+    local_bytes = op.A.algorithmic_bytes(BETA != 0.0)
+    local_flops = 2.0 * (i1 - i0)
+    torch.cuda.synchronize()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        op.kernel(ALPHA, x, BETA, sp)
+        if ev is not None:
+            ev[1].record(stream)
+        op.exchange(sp)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    stats = torch.tensor([el, kern_ms, local_bytes, local_flops], dtype=torch.float64, device=dev)
+    if dist is not None:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el, kern_ms_max = float(mx[0]), float(mx[1])
+        tot_bytes = float(sm[2])
+    else:
+        kern_ms_max, tot_bytes = kern_ms, float(local_bytes)
+    ms_step = el / args.steps * 1e3
+    total_flops = 2.0 * nnz
+
+    if rank == 0:
+        achieved = local_bytes / (kern_ms * 1e-3) / 1e9  # rank 0's kernel
+        traffic = pmc_traffic(args.algo) if world == 1 else None
+        out = {
+            "metric": METRIC,
+            "value": round(total_flops / (ms_step * 1e-3) / 1e9, 3),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (deterministic generator, DESIGN.md)",
+            "config": {
+                "workload": (f"synthetic non-uniform n={n} CSR fp64 SpMV, rows<n/8: {args.heavy} "
+                             f"nnz else {args.light}, {args.cols} sorted cols (seed 42), "
+                             f"y=alpha*A*x+beta*y, {args.algo} kernel"),
+                "n": n, "nnz": nnz, "algo": args.algo,
+                "partition": "nnz-balanced (spMV_mgpu_v1)" if world > 1 else "single GPU",
+                "exchange": args.exchange if world > 1 else "none",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+            },
+            "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
+            "kernel_only_gflops": round(total_flops / (kern_ms_max * 1e-3) / 1e9, 3),
+            "algorithmic_bytes_per_launch": int(local_bytes),
+            "algorithmic_bytes_all_ranks": int(tot_bytes),
+            "host_gen_s": round(t_gen, 2),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rp_all = rowptr
+            out["cpu_baseline"] = cpu_baseline(rp_all, col, val, x_h, plan.m, nnz, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    op.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -142,9 +142,13 @@ int sblas_trsv_destroy(sblas_trsv T);
 /* Multi-partition y assembly after an allgather of padded slices: partition
  * r's slice starts at d_gathered + r*stride; d_meta (DEVICE, 3*g ints) holds
  * {row0, nrows, cont} per partition; cont = first row continues partition
- * r-1 (its entry is added, in partition order). */
+ * r-1 (its entry is added, in partition order).  If d_y_local != NULL it
+ * is partition `self`'s slice and is prepared as the next call's y input
+ * (continuation entry zeroed, last entry refreshed when the next partition
+ * continues that row). */
 int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
-                          const int *d_meta, double *d_y, void *stream);
+                          const int *d_meta, double *d_y, int self,
+                          double *d_y_local, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Host utilities (no GPU needed). */

@@ -23,12 +23,24 @@ __global__ void k_assemble_copy(const double *__restrict__ gathered, int g, long
     y[row0 + k] = gathered[i];
 }
 
+// Carries in partition order (deterministic), then -- if this rank's local
+// slice is given -- prepare it as the next call's y input: its continuation
+// entry is zeroed (partial = alpha*p only) and its last entry takes the
+// assembled value when the next partition continues that row.
 __global__ void k_assemble_carry(const double *__restrict__ gathered, int g, long long stride,
-                                 const int *__restrict__ meta, double *__restrict__ y)
+                                 const int *__restrict__ meta, double *__restrict__ y, int self,
+                                 double *__restrict__ y_local)
 {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    for (int r = 0; r < g; ++r)  // partition order: deterministic
+    for (int r = 0; r < g; ++r)
         if (meta[3 * r + 2] && meta[3 * r + 1] > 0) y[meta[3 * r]] += gathered[(long long)r * stride];
+    if (y_local && self >= 0 && self < g) {
+        const int row0 = meta[3 * self], nrows = meta[3 * self + 1];
+        if (nrows > 0) {
+            if (self + 1 < g && meta[3 * (self + 1) + 2]) y_local[nrows - 1] = y[row0 + nrows - 1];
+            if (meta[3 * self + 2]) y_local[0] = 0.0;
+        }
+    }
 }
 
 }  // namespace sblas
@@ -36,7 +48,8 @@ __global__ void k_assemble_carry(const double *__restrict__ gathered, int g, lon
 using namespace sblas;
 
 extern "C" int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
-                                     const int *d_meta, double *d_y, void *stream)
+                                     const int *d_meta, double *d_y, int self,
+                                     double *d_y_local, void *stream)
 {
     if (g <= 0 || stride < 0 || !d_meta || !d_y) return SBLAS_ERR_INVALID;
     hipStream_t s = (hipStream_t)stream;
@@ -44,7 +57,8 @@ extern "C" int sblas_assemble_slices(const double *d_gathered, int g, long long 
     if (total > 0)
         hipLaunchKernelGGL(k_assemble_copy, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                            d_gathered, g, stride, d_meta, d_y);
-    hipLaunchKernelGGL(k_assemble_carry, dim3(1), dim3(64), 0, s, d_gathered, g, stride, d_meta, d_y);
+    hipLaunchKernelGGL(k_assemble_carry, dim3(1), dim3(64), 0, s, d_gathered, g, stride, d_meta, d_y,
+                       self, d_y_local);
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;
 }

@@ -80,7 +80,7 @@ _sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
 _sig("sblas_trsv_solve", _i, _p, _i, _p, _p, _p)
 _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
-_sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _p)
+_sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
 _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)

@@ -1,0 +1,125 @@
+"""Multi-GPU SpMV over torch.distributed (one process per GPU, RCCL over xGMI).
+
+SURVEY §8 G1: the matrix is split by nnz (dspmv_mgpu_v1.cu:60-94, with the
+Q5 fix), each rank keeps its slice resident, x is replicated, and after the
+local kernel the y slices are exchanged with ONE collective:
+
+* ``allgather`` (default): every rank contributes its slice padded to the
+  largest slice (all_gather_into_tensor == ncclAllGather); the rank-order
+  merge of split rows then runs on the device (sblas_assemble_slices), so
+  every rank ends with the full y, bit-identical across ranks;
+* ``allreduce`` (BASELINE config 3's literal form): each rank places its
+  slice into a zero vector of length m and the vectors are summed.
+
+Torch is plumbing here (device buffers, the process group); the kernels are
+libsblas's.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import sblas
+
+
+@dataclass
+class Plan:
+    world: int
+    m: int
+    n: int
+    nnz: int
+    start_idx: np.ndarray
+    end_idx: np.ndarray
+    start_row: np.ndarray
+    end_row: np.ndarray
+    start_flag: np.ndarray
+
+    @property
+    def nrows(self) -> np.ndarray:
+        return (self.end_row - self.start_row + 1).astype(np.int64)
+
+    @property
+    def stride(self) -> int:
+        return int(max(1, self.nrows.max()))
+
+    def meta(self) -> np.ndarray:
+        """{row0, nrows, cont} per rank, int32, as sblas_assemble_slices wants."""
+        return np.stack([self.start_row, self.nrows.astype(np.int32),
+                         self.start_flag]).T.astype(np.int32).ravel()
+
+    def local(self, rank: int):
+        """(row_begin, row_end_exclusive, idx_begin, idx_end_exclusive, cont)."""
+        return (int(self.start_row[rank]), int(self.end_row[rank]) + 1,
+                int(self.start_idx[rank]), int(self.end_idx[rank]) + 1,
+                bool(self.start_flag[rank]))
+
+
+def make_plan(rowptr: np.ndarray, n: int, world: int) -> Plan:
+    si, ei, sr, er, sf = sblas.partition_nnz(rowptr, world)
+    return Plan(world, len(rowptr) - 1, n, int(rowptr[-1]), si, ei, sr, er, sf)
+
+
+class DistSpMV:
+    """One rank's share of a multi-GPU y = alpha*A*x + beta*y."""
+
+    def __init__(self, plan: Plan, rank: int, device: int, rowptr, col_slice, val_slice,
+                 algo: int, torch, dist=None, exchange: str = "allgather"):
+        self.plan, self.rank, self.algo = plan, rank, algo
+        self.torch, self.dist, self.exchange_mode = torch, dist, exchange
+        r0, r1, i0, i1, cont = plan.local(rank)
+        self.r0, self.r1, self.cont = r0, r1, cont
+        dev = torch.device("cuda", device)
+        # upload_slice indexes col/val by GLOBAL element index: shift the bases.
+        col_base = col_slice.ctypes.data - i0 * 4
+        val_base = val_slice.ctypes.data - i0 * 8
+        h = sblas.C.c_void_p()
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        sblas.check(sblas.lib.sblas_csr_upload_slice(sblas.C.byref(h), device, plan.n, rp.ctypes.data,
+                                                     col_base, val_base, r0, r1, i0, i1, None),
+                    "csr_upload_slice")
+        self.A = sblas.DeviceCSR(h.value)
+        self.A.analyse(algo)
+        self.dm = r1 - r0
+        stride = plan.stride
+        f64 = torch.float64
+        self.y_local = torch.zeros(stride, dtype=f64, device=dev)  # padded slice
+        self.y_full = torch.zeros(plan.m, dtype=f64, device=dev)
+        self.gathered = torch.zeros(plan.world * stride, dtype=f64, device=dev)
+        self.meta = torch.from_numpy(plan.meta()).to(dev)
+
+    def load_y(self, y_full) -> None:
+        """Set y (full vector, device tensor) as the next call's input."""
+        self.y_full.copy_(y_full)
+        self.y_local[: self.dm].copy_(self.y_full[self.r0:self.r1])
+        if self.cont and self.dm > 0:
+            self.y_local[0] = 0.0
+
+    def kernel(self, alpha: float, x, beta: float, stream=None) -> None:
+        self.A.spmv(self.algo, alpha, x.data_ptr(), beta, self.y_local.data_ptr(), stream)
+
+    def exchange(self, stream=None) -> None:
+        if self.plan.world == 1:
+            return
+        if self.exchange_mode == "allgather":
+            self.dist.all_gather_into_tensor(self.gathered, self.y_local)
+            sblas.check(sblas.lib.sblas_assemble_slices(
+                self.gathered.data_ptr(), self.plan.world, self.plan.stride, self.meta.data_ptr(),
+                self.y_full.data_ptr(), self.rank, self.y_local.data_ptr(), stream),
+                "assemble_slices")
+        else:  # literal allreduce of y (config 3)
+            self.y_full.zero_()
+            self.y_full[self.r0:self.r1].copy_(self.y_local[: self.dm])
+            self.dist.all_reduce(self.y_full)
+            self.y_local[: self.dm].copy_(self.y_full[self.r0:self.r1])
+            if self.cont and self.dm > 0:
+                self.y_local[0] = 0.0
+
+    def result(self):
+        """Full y after exchange (world 1: the local slice is the whole y)."""
+        if self.plan.world == 1:
+            return self.y_local[: self.plan.m]
+        return self.y_full
+
+    def close(self):
+        self.A.close()

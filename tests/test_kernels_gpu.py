@@ -1,0 +1,194 @@
+"""SpMM, CSR->CSC transpose, SpTRSV and y-assembly kernels vs the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_csr(rng, m, n, maxlen, empty_frac=0.1, long_rows=()):
+    lens = rng.integers(0, maxlen, m)
+    lens[rng.random(m) < empty_frac] = 0
+    for r, L in long_rows:
+        lens[r] = L
+    lens = np.minimum(lens, n)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = (np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+           if rp[-1] else np.zeros(0, np.int32))
+    return rp, col, rng.standard_normal(int(rp[-1]))
+
+
+# ---------------------------------------------------------------- SpMM ----
+def spmm_bound(rp, col, val, B, alpha, beta, C0):
+    u = 2.0 ** -53
+    m = len(rp) - 1
+    k = np.diff(rp).astype(np.float64)
+    gam = (k * u / (1 - k * u))[:, None]
+    rows = np.repeat(np.arange(m), np.diff(rp))
+    S = np.zeros((m, B.shape[1]))
+    np.add.at(S, rows, np.abs(alpha * val[:, None] * B[col, :]))
+    return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
+
+
+@pytest.mark.parametrize("ncols", [1, 16, 64, 100])
+@pytest.mark.parametrize("layout", [0, 1])
+def test_spmm(torch_cuda, sb, orc, ncols, layout):
+    torch = torch_cuda
+    rng = np.random.default_rng(ncols + 10 * layout)
+    m, k = 700, 5000
+    rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
+    B = rng.standard_normal((k, ncols))
+    C0 = rng.standard_normal((m, ncols))
+    alpha, beta = -0.7, 0.8  # dspmm_baseline_test.cu:518-519
+    want = orc.spmm(m, ncols, k, alpha, rp, col, val, B, beta, C0)
+    A = sb.DeviceCSR.upload(0, k, rp, col, val)
+    if layout == 0:  # column-major B (ld = k)
+        Bd = torch.from_numpy(np.asfortranarray(B).ravel(order="F")).cuda()
+        ldb = k
+    else:            # row-major B (ld = ncols)
+        Bd = torch.from_numpy(np.ascontiguousarray(B).ravel()).cuda()
+        ldb = ncols
+    Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
+    A.spmm(ncols, alpha, Bd.data_ptr(), ldb, layout, beta, Cd.data_ptr(), m)
+    torch.cuda.synchronize()
+    got = Cd.cpu().numpy().reshape((ncols, m)).T
+    assert np.all(np.abs(got - want) <= spmm_bound(rp, col, val, B, alpha, beta, C0))
+    A.close()
+
+
+@pytest.mark.parametrize("ngpu", [1, 2, 3])
+def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu):
+    """cusparse_mgpu_csrmm drop-in on qh768 x 128 (run_test.py's spmm case)."""
+    path = os.path.join(GOLDEN, "qh768.mtx")
+    m, k, rp, col, val = sb.mm_read(path, 0)
+    ncols = 128
+    rng = np.random.default_rng(1)
+    B = rng.random((k, ncols))
+    C0 = rng.random((m, ncols))
+    Cf = np.asfortranarray(C0).copy()
+    Bf = np.asfortranarray(B)
+    rp32 = rp.astype(np.int32)
+    a = np.array([-0.7]); b = np.array([0.8])
+    rc = sb.lib.sblas_csrmm_mgpu(m, ncols, k, sb.ptr(a), int(rp[-1]), sb.ptr(rp32), sb.ptr(col),
+                                 sb.ptr(val), sb.ptr(b), Bf.ctypes.data, Cf.ctypes.data, ngpu)
+    assert rc == 0
+    want = orc.spmm(m, ncols, k, -0.7, rp32, col, val, B, 0.8, C0)
+    assert np.all(np.abs(Cf - want) <= spmm_bound(rp, col, val, B, -0.7, 0.8, C0))
+    assert np.all(np.abs(Cf - want) < 1e-3)  # the reference's own check (:544-549)
+
+
+# ----------------------------------------------------------- transpose ----
+@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols"])
+def test_transpose_bit_exact(torch_cuda, sb, orc, case):
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    if case in ("qh768", "ash85"):
+        m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
+    elif case == "random":
+        m, n = 3000, 2500
+        rp, col, val = rand_csr(rng, m, n, 30)
+    else:  # columns longer than 32 / 4096 (medium and big sort paths)
+        m, n = 9000, 40
+        rp, col, val = rand_csr(rng, m, n, 40, empty_frac=0.2)
+    nnz = int(rp[-1])
+    cp, ri, cv = orc.transpose(m, n, rp, col, val)
+    A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    dcp = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    dri = torch.zeros(max(nnz, 1), dtype=torch.int32, device="cuda")
+    dcv = torch.zeros(max(nnz, 1), dtype=torch.float64, device="cuda")
+    A.transpose(dcp.data_ptr(), dri.data_ptr(), dcv.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(dcp.cpu().numpy(), cp)
+    assert np.array_equal(dri.cpu().numpy()[:nnz], ri)
+    assert np.array_equal(dcv.cpu().numpy()[:nnz], cv)
+    A.close()
+
+
+# -------------------------------------------------------------- SpTRSV ----
+@pytest.mark.parametrize("name", ["qh768", "ash85"])
+@pytest.mark.parametrize("sub", ["fwd", "bwd"])
+@pytest.mark.parametrize("algo", [0, 1])
+def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
+    torch = torch_cuda
+    g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
+    cp, ri, cv, b = g["colptr"], g["rowidx"], g["val"], g["b"]
+    n, nnz = len(cp) - 1, len(ri)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    T = sb.DeviceTRSV(0, n, nnz, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                      0 if sub == "fwd" else 1)
+    for _ in range(3):
+        xd.zero_()
+        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xd.cpu().numpy(), g["x_ref"])  # exact KAT
+    if sub == "fwd":
+        assert T.levels() == orc.levels_lower(cp, ri)
+    T.close()
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
+    """Random lower-triangular with long chains and a long column/row."""
+    torch = torch_cuda
+    rng = np.random.default_rng(9)
+    n = 20000
+    rp, col, _ = rand_csr(rng, n, n, 8, empty_frac=0.0)
+    (trp, tc, tv), (cp, ri, cv), xref, b = orc.build_tri(rp.astype(np.int32), col, 0, seed=3)
+    # scale to keep the solve well conditioned
+    lens = np.diff(cp)
+    rows = ri
+    cv = cv.copy()
+    off = np.ones(len(cv), bool)
+    off[cp[:-1]] = False
+    rl = np.bincount(ri, minlength=n)
+    cv[off] = cv[off] / (2.0 * rl[rows[off]])
+    b = np.zeros(n)
+    for c in range(n):
+        b[ri[cp[c]:cp[c + 1]]] += cv[cp[c]:cp[c + 1]] * xref[c]
+    want = orc.sptrsv_serial(cp, ri, cv, b, 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 0)
+    T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+    torch.cuda.synchronize()
+    x = xd.cpu().numpy()
+    rel = np.abs(x - want).sum() / np.abs(want).sum()
+    assert rel <= 1e-12, rel
+    T.close()
+
+
+def test_sptrsv_reference_api(torch_cuda, sb, capfd):
+    g = np.load(os.path.join(GOLDEN, "trsv_qh768_fwd.npz"))
+    cp, ri, cv, b, xref = g["colptr"], g["rowidx"], g["val"], g["b"], g["x_ref"]
+    n = len(cp) - 1
+    x = np.zeros(n)
+    gf = np.zeros(1)
+    for opt in (1, 3):
+        rc = sb.lib.sblas_sptrsv_syncfree(sb.ptr(cp), sb.ptr(ri), sb.ptr(cv), n, n, len(ri), 0, 1,
+                                          opt, sb.ptr(x), sb.ptr(b), sb.ptr(xref), sb.ptr(gf), 1)
+        assert rc == 0 and np.array_equal(x, xref)
+    out = capfd.readouterr().out
+    assert "cuda syncfree SpTRSV solve used" in out and "executor passed!" in out
+
+
+# ------------------------------------------------------------ assembly ----
+def test_assemble_slices(torch_cuda, sb):
+    torch = torch_cuda
+    # 4 partitions; rank 2 and 3 continue a row of the previous one
+    meta = np.array([0, 3, 0, 3, 2, 0, 4, 2, 1, 5, 1, 1], np.int32)  # rows 0-2 | 3-4 | 4-5 | 5
+    stride = 3
+    gathered = np.array([1, 2, 3, 4, 5, 0, 6, 7, 0, 8, 0, 0], np.float64)
+    want = np.array([1, 2, 3, 4, 5 + 6, 7 + 8])
+    gd = torch.from_numpy(gathered).cuda()
+    md = torch.from_numpy(meta).cuda()
+    y = torch.full((6,), -1.0, dtype=torch.float64, device="cuda")
+    yl = torch.from_numpy(np.array([6.0, 7.0, 0.0])).cuda()  # rank 2's slice
+    sb.check(sb.lib.sblas_assemble_slices(gd.data_ptr(), 4, stride, md.data_ptr(), y.data_ptr(),
+                                          2, yl.data_ptr(), None), "assemble")
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), want)
+    assert np.array_equal(yl.cpu().numpy(), [0.0, 15.0, 0.0])
