@@ -68,7 +68,7 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu):
     rng = np.random.default_rng(1)
     B = rng.random((k, ncols))
     C0 = rng.random((m, ncols))
-    Cf = np.asfortranarray(C0).copy()
+    Cf = np.array(C0, order="F", copy=True)
     Bf = np.asfortranarray(B)
     rp32 = rp.astype(np.int32)
     a = np.array([-0.7]); b = np.array([0.8])
