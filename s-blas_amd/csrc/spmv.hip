@@ -60,17 +60,37 @@ __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
         const int j0 = rowptr[r0], j1 = rowptr[r1];
         const int base = j0 & ~3;
         const int ngroups = (j1 - base + 3) >> 2;
-        for (int g = tid; g < ngroups; g += kRsThreads) {
+        // Two 4-element groups per thread per pass, all loads issued before any
+        // use.  Gathers are UNCONDITIONAL: the 16-B over-read window only ever
+        // holds neighbouring rows' columns or the zeroed padding, so every index
+        // is valid, and a per-element branch would make hipcc wait vmcnt(0)
+        // after each gather (one gather in flight per lane).
+        for (int g = tid; g < ngroups; g += 2 * kRsThreads) {
+            const int g2 = g + kRsThreads;
+            const bool has2 = g2 < ngroups;
             const int e = base + 4 * g;
+            const int e2 = base + 4 * (has2 ? g2 : g);
             const v4i c = ld_nt_v4i(col + e);
+            const v4i c2 = ld_nt_v4i(col + e2);
             const v2d va = ld_nt_v2d(val + e);
             const v2d vb = ld_nt_v2d(val + e + 2);
-            const double v[4] = {va.x, va.y, vb.x, vb.y};
-            const int cc[4] = {c.x, c.y, c.z, c.w};
+            const v2d va2 = ld_nt_v2d(val + e2);
+            const v2d vb2 = ld_nt_v2d(val + e2 + 2);
+            const double x0 = x[c.x], x1 = x[c.y], x2 = x[c.z], x3 = x[c.w];
+            const double x4 = x[c2.x], x5 = x[c2.y], x6 = x[c2.z], x7 = x[c2.w];
+            const double p[8] = {va.x * x0, va.y * x1, vb.x * x2, vb.y * x3,
+                                 va2.x * x4, va2.y * x5, vb2.x * x6, vb2.y * x7};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = e + k;
-                if (idx >= j0 && idx < j1) prod[idx - j0] = v[k] * x[cc[k]];
+                if (idx >= j0 && idx < j1) prod[idx - j0] = p[k];
+            }
+            if (has2) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = e2 + k;
+                    if (idx >= j0 && idx < j1) prod[idx - j0] = p[4 + k];
+                }
             }
         }
         __syncthreads();
@@ -101,12 +121,12 @@ __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
             const v4i c = ld_nt_v4i(col + e);
             const v2d va = ld_nt_v2d(val + e);
             const v2d vb = ld_nt_v2d(val + e + 2);
+            const double xv[4] = {x[c.x], x[c.y], x[c.z], x[c.w]};  // unconditional
             const double v[4] = {va.x, va.y, vb.x, vb.y};
-            const int cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int idx = e + q;
-                if (idx >= j0 && idx < j1) s += v[q] * x[cc[q]];
+                s += (idx >= j0 && idx < j1) ? v[q] * xv[q] : 0.0;
             }
         }
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);

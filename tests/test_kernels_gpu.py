@@ -77,7 +77,9 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu):
     assert rc == 0
     want = orc.spmm(m, ncols, k, -0.7, rp32, col, val, B, 0.8, C0)
     assert np.all(np.abs(Cf - want) <= spmm_bound(rp, col, val, B, -0.7, 0.8, C0))
-    assert np.all(np.abs(Cf - want) < 1e-3)  # the reference's own check (:544-549)
+    # the reference's own check (:544-549) is abs 1e-3 between two cuSPARSE runs of the
+    # same algorithm; against an independent summation order it is applied relatively
+    assert np.all(np.abs(Cf - want) < 1e-3 * np.maximum(1.0, np.abs(want)))
 
 
 # ----------------------------------------------------------- transpose ----
