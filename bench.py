@@ -11,7 +11,12 @@ matrix is split by nnz over the ranks (x replicated) and a step also
 includes the RCCL allgather of the y slices plus their device-side merge
 (strong scaling: the same matrix at every N).
 
-  python bench.py [--gpus N --steps K --warmup W] [--algo rowsplit|csr5]
+  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5]
+
+Default kernel: `panel` = the row-split kernel run over XCD-affine column
+panels (x slice ~4 MiB per panel, panel p's row blocks on workgroups with
+blockIdx % P == p) plus a partial-y reduce; with a single non-empty panel it
+is exactly the plain row-split kernel.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
@@ -94,7 +99,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--algo", choices=["rowsplit", "csr5"], default="rowsplit")
+    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel"], default="panel")
     ap.add_argument("--n", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
@@ -121,7 +126,7 @@ def main() -> int:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    algo = sblas.ROWSPLIT if args.algo == "rowsplit" else sblas.CSR5
+    algo = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL}[args.algo]
     n = args.n
     rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
     nnz = int(rowptr[-1])

@@ -64,6 +64,38 @@ struct Csr5Plan {
     bool ready = false;
 };
 
+// XCD-panel plan: A split into P column panels (x panel ~2 MiB), each a CSR
+// with its own rowptr; one launch interleaves the panels' row blocks so that
+// blockIdx % P selects the panel (P = 8 = #XCDs: each XCD's L2 then serves
+// one x panel).  Panels write alpha-scaled partial y; a reduce adds them.
+struct PanelDesc {
+    const int *rowptr;
+    const int *col;
+    const double *val;
+    const RowBlock *blocks;
+    double *out;      // ypart + p*m
+    double *partial;  // long-row chunk partials
+    int nblocks;
+    int pad;
+};
+
+struct PanelPlan {
+    int P = 0;
+    long long W = 0;
+    int maxblocks = 0;
+    int *rowptr = nullptr;      // [P][m+1] panel-local
+    int *col = nullptr;         // panel-major, padded
+    double *val = nullptr;
+    RowBlock *blocks = nullptr; // [P][maxblocks]
+    PanelDesc *desc = nullptr;  // device [P]
+    double *ypart = nullptr;    // [P][m]
+    double *partial = nullptr;  // long-row slots, all panels
+    int4 *long_rows = nullptr;  // {row, slot, nchunks, panel}
+    int nlong = 0;
+    bool degenerate = false;    // <= 1 non-empty panel: plain row split
+    bool ready = false;
+};
+
 struct RsPlan {
     int nblocks = 0;
     RowBlock *blocks = nullptr;
@@ -85,6 +117,7 @@ struct sblas_csr_s {
     double *val = nullptr;   // [nnz + pad]
     sblas::RsPlan rs;
     sblas::Csr5Plan c5;
+    sblas::PanelPlan pn;
     std::vector<int> h_rowptr;  // host copy (analysis)
 };
 
@@ -98,6 +131,11 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
                      double beta, double *y, hipStream_t s);
 int build_csr5_plan(sblas_csr_s &A, hipStream_t s);
 void free_plans(sblas_csr_s &A);
+
+int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x,
+                      double beta, double *y, hipStream_t s);
+int build_panel_plan(sblas_csr_s &A, hipStream_t s);
+int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s);
 
 int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
                 int ldb, int b_layout, double beta, double *C, int ldc,

@@ -21,6 +21,7 @@
 //  * alpha/beta are honoured by both (the reference's CSR5 ignored them, Q4);
 //    beta == 0 never reads y (BLAS/cuSPARSE convention).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -42,16 +43,22 @@ __device__ __forceinline__ v2d ld_nt_v2d(const double *p)
 // ---------------------------------------------------------------------------
 // Row split
 // ---------------------------------------------------------------------------
-template <bool kBeta>
-__global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
-    const int *__restrict__ rowptr, const int *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ x,
-    const RowBlock *__restrict__ blocks, double alpha, double beta,
-    double *__restrict__ y, double *__restrict__ partial)
+// One row block (stream or long-row chunk) of a CSR: shared by the plain
+// row-split kernel and the XCD-panel kernel (which runs it on column panels).
+template <bool kBeta, bool kSc1 = false>
+__device__ __forceinline__ void store_y(double *p, double v)
 {
-    __shared__ double prod[kRsBlockNnz + 8];
-    __shared__ double wsum[kRsThreads / 64];
-    const RowBlock blk = blocks[blockIdx.x];
+    if (kSc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <bool kBeta, bool kSc1 = false>
+__device__ __forceinline__ void rowsplit_block(
+    const RowBlock blk, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x, double alpha, double beta,
+    double *__restrict__ y, double *__restrict__ partial, double *__restrict__ prod,
+    double *__restrict__ wsum)
+{
     const int tid = threadIdx.x;
 
     if (blk.a >= 0) {
@@ -105,7 +112,7 @@ __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
             double s = 0.0;
             for (int k = a + lane; k < b; k += tpr) s += prod[k];
             for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-            if (lane == 0) y[r] = kBeta ? alpha * s + beta * y[r] : alpha * s;
+            if (lane == 0) store_y<kBeta, kSc1>(&y[r], kBeta ? alpha * s + beta * y[r] : alpha * s);
         }
     } else {
         // ---- long-row chunk ------------------------------------------------
@@ -136,10 +143,23 @@ __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
             double t = 0.0;
 #pragma unroll
             for (int w = 0; w < kRsThreads / 64; ++w) t += wsum[w];
-            if (blk.b < 0) y[r] = kBeta ? alpha * t + beta * y[r] : alpha * t;
+            if (blk.b < 0) store_y<kBeta, kSc1>(&y[r], kBeta ? alpha * t + beta * y[r] : alpha * t);
             else partial[blk.b] = t;
         }
     }
+}
+
+template <bool kBeta>
+__global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
+    const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    const RowBlock *__restrict__ blocks, double alpha, double beta,
+    double *__restrict__ y, double *__restrict__ partial)
+{
+    __shared__ double prod[kRsBlockNnz + 8];
+    __shared__ double wsum[kRsThreads / 64];
+    rowsplit_block<kBeta>(blocks[blockIdx.x], rowptr, col, val, x, alpha, beta, y, partial, prod,
+                          wsum);
 }
 
 template <bool kBeta>
@@ -156,17 +176,14 @@ __global__ void k_spmv_long_finalize(const int4 *__restrict__ long_rows, int nlo
     y[L.x] = kBeta ? alpha * s + beta * y[L.x] : alpha * s;
 }
 
-int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
+// Greedy CSR-adaptive blocking of rows [0, m): whole rows up to kRsBlockNnz
+// nnz / kRsMaxRows rows per block; longer rows in kRsLongChunk chunks (slot
+// numbers continue from `nslots`).
+void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
+                     std::vector<int4> &longs, int &nslots)
 {
-    if (A.rs.ready) return SBLAS_OK;
-    DeviceGuard g(A.device);
-    const std::vector<int> &rp = A.h_rowptr;
-    std::vector<RowBlock> blocks;
-    std::vector<int4> longs;
-    blocks.reserve(A.nnz / kRsBlockNnz + A.m / kRsMaxRows + 16);
-    int nslots = 0;
     int r = 0;
-    while (r < A.m) {
+    while (r < m) {
         const int len = rp[r + 1] - rp[r];
         if (len > kRsBlockNnz) {
             const int nch = (len + kRsLongChunk - 1) / kRsLongChunk;
@@ -182,7 +199,7 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
         }
         const int start = r;
         int nz = 0;
-        while (r < A.m && r - start < kRsMaxRows) {
+        while (r < m && r - start < kRsMaxRows) {
             const int l = rp[r + 1] - rp[r];
             if (l > kRsBlockNnz || nz + l > kRsBlockNnz) break;
             nz += l;
@@ -190,6 +207,17 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
         }
         blocks.push_back({start, r, 0, 0});
     }
+}
+
+int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.rs.ready) return SBLAS_OK;
+    DeviceGuard g(A.device);
+    std::vector<RowBlock> blocks;
+    std::vector<int4> longs;
+    blocks.reserve(A.nnz / kRsBlockNnz + A.m / kRsMaxRows + 16);
+    int nslots = 0;
+    make_row_blocks(A.h_rowptr.data(), A.m, blocks, longs, nslots);
     A.rs.nblocks = (int)blocks.size();
     A.rs.nlong = (int)longs.size();
     A.rs.nslots = nslots;
@@ -483,6 +511,232 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     return SBLAS_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// XCD-affine column panels (algo 4)
+// ---------------------------------------------------------------------------
+// Config 2's columns are uniform over n: with one launch over all of A every
+// XCD gathers from all of x (16 MB, 4x its 4 MB L2) and ~55% of gathers miss
+// to the Infinity Cache at 64-B line granularity.  Splitting A into P = 8
+// column panels and dealing panel p's row blocks to workgroups with
+// blockIdx % 8 == p keeps each XCD on one ~2 MB slice of x (round-robin
+// dispatch; a different placement is only slower, never wrong).
+template <bool kSc1>
+__global__ __launch_bounds__(kRsThreads) void k_spmv_panel(const PanelDesc *__restrict__ desc,
+                                                           int P, const double *__restrict__ x,
+                                                           double alpha)
+{
+    __shared__ double prod[kRsBlockNnz + 8];
+    __shared__ double wsum[kRsThreads / 64];
+    const int p = blockIdx.x % P;
+    const int lb = blockIdx.x / P;
+    const PanelDesc d = desc[p];
+    if (lb >= d.nblocks) return;
+    rowsplit_block<false, kSc1>(d.blocks[lb], d.rowptr, d.col, d.val, x, alpha, 0.0, d.out,
+                                d.partial, prod, wsum);
+}
+
+__global__ void k_panel_long_finalize(const int4 *__restrict__ long_rows, int nlong,
+                                      const double *__restrict__ partial, double alpha,
+                                      double *__restrict__ ypart, long long m)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlong) return;
+    const int4 L = long_rows[i];
+    double s = 0.0;
+    for (int q = 0; q < L.z; ++q) s += partial[L.y + q];
+    ypart[(long long)L.w * m + L.x] = alpha * s;
+}
+
+template <bool kBeta>
+__global__ void k_panel_reduce(const double *__restrict__ ypart, int P, long long m, double beta,
+                               double *__restrict__ y)
+{
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    double s = 0.0;
+    for (int p = 0; p < P; ++p) s += __builtin_nontemporal_load(ypart + (long long)p * m + r);
+    y[r] = kBeta ? s + beta * y[r] : s;
+}
+
+// thread per row: counts of the row's entries per panel -> rowptr[p][r+1]
+__global__ void k_panel_count(const int *__restrict__ rowptr, const int *__restrict__ col, int m,
+                              long long W, int P, int *__restrict__ prp)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+        const int p = (int)(col[j] / W);
+        prp[(long long)p * (m + 1) + r + 1]++;
+    }
+}
+
+// thread per row: stable scatter of the row's entries into the panels
+__global__ void k_panel_scatter(const int *__restrict__ rowptr, const int *__restrict__ col,
+                                const double *__restrict__ val, int m, long long W, int P,
+                                const int *__restrict__ prp, const long long *__restrict__ base,
+                                int *__restrict__ pcol, double *__restrict__ pval)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const int a = rowptr[r], b = rowptr[r + 1];
+    for (int p = 0; p < P; ++p) {
+        long long o = base[p] + prp[(long long)p * (m + 1) + r];
+        for (int j = a; j < b; ++j) {
+            const int c = col[j];
+            if ((int)(c / W) == p) {
+                pcol[o] = c;
+                pval[o] = val[j];
+                ++o;
+            }
+        }
+    }
+}
+
+int build_panel_plan(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.pn.ready) return SBLAS_OK;
+    DeviceGuard g(A.device);
+    PanelPlan &Q = A.pn;
+    // ~4 MiB of x per panel (one XCD's L2), at most one panel per XCD; measured
+    // on config 2: P = 4 beats 8 (fewer partial-y bytes), DESIGN.md.
+    int P = (int)std::min<long long>(8, std::max<long long>(1, ((long long)A.n * 8 + (4 << 20) - 1) >> 22));
+    if (const char *e = getenv("SBLAS_PANELS")) P = std::max(1, std::min(64, atoi(e)));
+    if (A.n < P) P = std::max(1, A.n);
+    Q.P = P;
+    Q.W = ((long long)A.n + P - 1) / P;
+    const long long m = A.m;
+    SBLAS_HIP(hipMalloc(&Q.rowptr, sizeof(int) * P * (m + 1)));
+    SBLAS_HIP(hipMemsetAsync(Q.rowptr, 0, sizeof(int) * P * (m + 1), s));
+    const long long cap = ((A.nnz + 3) & ~3LL) + 4 * P + 4;
+    SBLAS_HIP(hipMalloc(&Q.col, sizeof(int) * cap));
+    SBLAS_HIP(hipMalloc(&Q.val, sizeof(double) * cap));
+    SBLAS_HIP(hipMemsetAsync(Q.col, 0, sizeof(int) * cap, s));
+    SBLAS_HIP(hipMemsetAsync(Q.val, 0, sizeof(double) * cap, s));
+    SBLAS_HIP(hipMalloc(&Q.ypart, sizeof(double) * std::max<long long>(P * m, 1)));
+    if (m > 0) {
+        hipLaunchKernelGGL(k_panel_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                           A.rowptr, A.col, (int)m, Q.W, P, Q.rowptr);
+        int *scratch = nullptr;
+        SBLAS_HIP(hipMalloc(&scratch, sizeof(int) * ((m + 1) / 1024 + 256)));
+        for (int p = 0; p < P; ++p) SBLAS_TRY(scan_inclusive(Q.rowptr + p * (m + 1), m + 1, scratch, s));
+        SBLAS_HIP(hipStreamSynchronize(s));
+        (void)hipFree(scratch);
+    }
+    std::vector<int> hrp((size_t)P * (m + 1));
+    SBLAS_HIP(hipMemcpy(hrp.data(), Q.rowptr, sizeof(int) * hrp.size(), hipMemcpyDeviceToHost));
+    // panel bases, 4-element aligned so each panel starts 16-B aligned
+    std::vector<long long> base(P);
+    long long acc = 0;
+    for (int p = 0; p < P; ++p) {
+        base[p] = acc;
+        acc += hrp[(size_t)p * (m + 1) + m];
+        acc = (acc + 3) & ~3LL;
+    }
+    long long *dbase = nullptr;
+    SBLAS_HIP(hipMalloc(&dbase, sizeof(long long) * P));
+    SBLAS_HIP(hipMemcpy(dbase, base.data(), sizeof(long long) * P, hipMemcpyHostToDevice));
+    if (m > 0)
+        hipLaunchKernelGGL(k_panel_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                           A.rowptr, A.col, A.val, (int)m, Q.W, P, Q.rowptr, dbase, Q.col, Q.val);
+    SBLAS_HIP(hipStreamSynchronize(s));
+    (void)hipFree(dbase);
+    // Only non-empty panels take part.  One non-empty panel (all columns in
+    // one x slice, e.g. the prefix layout) is plain row split: use it.
+    std::vector<int> live;
+    for (int p = 0; p < P; ++p)
+        if (hrp[(size_t)p * (m + 1) + m] > 0) live.push_back(p);
+    if (live.size() <= 1) {
+        (void)hipFree(Q.rowptr);
+        (void)hipFree(Q.col);
+        (void)hipFree(Q.val);
+        (void)hipFree(Q.ypart);
+        Q.rowptr = nullptr;
+        Q.col = nullptr;
+        Q.val = nullptr;
+        Q.ypart = nullptr;
+        Q.P = 1;
+        Q.degenerate = true;
+        SBLAS_TRY(build_rowsplit_plan(A, s));
+        Q.ready = true;
+        return SBLAS_OK;
+    }
+    const int PL = (int)live.size();
+    // per-panel row blocks, padded to a common count for the interleaved grid
+    std::vector<std::vector<RowBlock>> pb(PL);
+    std::vector<int4> longs;
+    int nslots = 0;
+    for (int q = 0; q < PL; ++q) {
+        std::vector<int4> pl;
+        make_row_blocks(hrp.data() + (size_t)live[q] * (m + 1), (int)m, pb[q], pl, nslots);
+        for (auto &L : pl) longs.push_back(make_int4(L.x, L.y, L.z, q));
+        Q.maxblocks = std::max<int>(Q.maxblocks, (int)pb[q].size());
+    }
+    std::vector<RowBlock> all((size_t)PL * Q.maxblocks, RowBlock{0, 0, 0, 0});
+    for (int q = 0; q < PL; ++q)
+        std::copy(pb[q].begin(), pb[q].end(), all.begin() + (size_t)q * Q.maxblocks);
+    SBLAS_HIP(hipMalloc(&Q.blocks, sizeof(RowBlock) * std::max<size_t>(all.size(), 1)));
+    if (!all.empty())
+        SBLAS_HIP(hipMemcpy(Q.blocks, all.data(), sizeof(RowBlock) * all.size(), hipMemcpyHostToDevice));
+    Q.nlong = (int)longs.size();
+    SBLAS_HIP(hipMalloc(&Q.partial, sizeof(double) * std::max(nslots, 1)));
+    if (Q.nlong) {
+        SBLAS_HIP(hipMalloc(&Q.long_rows, sizeof(int4) * longs.size()));
+        SBLAS_HIP(hipMemcpy(Q.long_rows, longs.data(), sizeof(int4) * longs.size(), hipMemcpyHostToDevice));
+    }
+    std::vector<PanelDesc> hd(PL);
+    for (int q = 0; q < PL; ++q) {
+        const int p = live[q];
+        hd[q].rowptr = Q.rowptr + (size_t)p * (m + 1);
+        hd[q].col = Q.col + base[p];
+        hd[q].val = Q.val + base[p];
+        hd[q].blocks = Q.blocks + (size_t)q * Q.maxblocks;
+        hd[q].out = Q.ypart + (size_t)q * m;
+        hd[q].partial = Q.partial;
+        hd[q].nblocks = (int)pb[q].size();
+        hd[q].pad = 0;
+    }
+    Q.P = PL;
+    SBLAS_HIP(hipMalloc(&Q.desc, sizeof(PanelDesc) * PL));
+    SBLAS_HIP(hipMemcpy(Q.desc, hd.data(), sizeof(PanelDesc) * PL, hipMemcpyHostToDevice));
+    Q.ready = true;
+    return SBLAS_OK;
+}
+
+int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x, double beta,
+                      double *y, hipStream_t s)
+{
+    const PanelPlan &Q = A.pn;
+    if (!Q.ready) return SBLAS_ERR_INVALID;
+    if (Q.degenerate) return launch_spmv_rowsplit(A, alpha, x, beta, y, s);
+    if (A.m == 0) return SBLAS_OK;
+    const long long grid = (long long)Q.maxblocks * Q.P;
+    static const bool sc1 = [] {
+        const char *e = getenv("SBLAS_PANEL_SC1");
+        return e && atoi(e) != 0;
+    }();
+    if (grid > 0) {
+        if (sc1)
+            hipLaunchKernelGGL(k_spmv_panel<true>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
+                               Q.desc, Q.P, x, alpha);
+        else
+            hipLaunchKernelGGL(k_spmv_panel<false>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
+                               Q.desc, Q.P, x, alpha);
+    }
+    if (Q.nlong)
+        hipLaunchKernelGGL(k_panel_long_finalize, dim3((Q.nlong + 63) / 64), dim3(64), 0, s,
+                           Q.long_rows, Q.nlong, Q.partial, alpha, Q.ypart, (long long)A.m);
+    const unsigned rb = (unsigned)((A.m + 255) / 256);
+    if (beta != 0.0)
+        hipLaunchKernelGGL(k_panel_reduce<true>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
+                           (long long)A.m, beta, y);
+    else
+        hipLaunchKernelGGL(k_panel_reduce<false>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
+                           (long long)A.m, beta, y);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
 void free_plans(sblas_csr_s &A)
 {
     DeviceGuard g(A.device);
@@ -500,6 +754,16 @@ void free_plans(sblas_csr_s &A)
     (void)hipFree(P.empty_rows);
     (void)hipFree(P.carry);
     A.c5 = Csr5Plan{};
+    PanelPlan &Q = A.pn;
+    (void)hipFree(Q.rowptr);
+    (void)hipFree(Q.col);
+    (void)hipFree(Q.val);
+    (void)hipFree(Q.blocks);
+    (void)hipFree(Q.desc);
+    (void)hipFree(Q.ypart);
+    (void)hipFree(Q.partial);
+    (void)hipFree(Q.long_rows);
+    A.pn = PanelPlan{};
 }
 
 }  // namespace sblas

@@ -72,7 +72,7 @@ __global__ void k_scan_add(int *__restrict__ a, long long len, const int *__rest
 }
 
 // In-place inclusive scan; scratch must hold >= sum over levels of tiles.
-static int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s)
+int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s)
 {
     if (len <= 0) return SBLAS_OK;
     const long long tiles = (len + kScanTile - 1) / kScanTile;

@@ -25,7 +25,7 @@ if [[ $STEP == all || $STEP == cli ]]; then
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
   run bench
-  for a in rowsplit csr5; do for c in random prefix; do
+  for a in panel rowsplit csr5; do for c in random prefix; do
     timeout -k 10 300 python bench.py --algo $a --cols $c --no-cpu-baseline > $O/bench_${a}_${c}.log 2>&1 || exit 1
   done; done
   timeout -k 10 400 python bench.py > $O/bench_default.log 2>&1 || exit 1
@@ -33,12 +33,16 @@ if [[ $STEP == all || $STEP == bench ]]; then
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
   run prof
-  for a in rowsplit csr5; do
+  for a in panel rowsplit csr5; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run --output-format csv -- python bench.py --algo $a --no-cpu-baseline > $O/prof_$a.log 2>&1 || exit 1
     timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$a -o run --output-format csv -- python bench.py --algo $a --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_fetch_$a.log 2>&1 || exit 1
     timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$a -o run --output-format csv -- python bench.py --algo $a --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_write_$a.log 2>&1 || exit 1
     timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $O/pmc_l2_$a -o run --output-format csv -- python bench.py --algo $a --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc_l2_$a.log 2>&1 || exit 1
   done
-  find $O/prof_rowsplit $O/pmc_fetch_rowsplit -name "*.csv" | head
+  for a in panel rowsplit csr5; do
+    case $a in panel) k=k_spmv_panel,k_panel_reduce;; rowsplit) k=k_spmv_rowsplit;; csr5) k=k_spmv_csr5,k_csr5_calibrate;; esac
+    python3 s-blas_amd/tools/pmc_traffic.py --kernel $k --fetch $O/pmc_fetch_$a --write $O/pmc_write_$a --l2 $O/pmc_l2_$a --algorithmic 533000004 --out $O/pmc_$a.json > /dev/null || exit 1
+  done
+  ls $O/pmc_*.json
 fi
 echo "[$(date +%T)] session done"

@@ -25,13 +25,21 @@ import statistics
 
 
 def counter_values(d, kernel, name):
-    vals = []
-    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(path) as fh:
-            for row in csv.DictReader(fh):
-                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == name:
-                    vals.append(float(row["Counter_Value"]))
-    return vals
+    """Per-launch values; `kernel` may list several comma-separated kernels
+    that make up one operation (e.g. panel SpMV + its reduce): their medians
+    are summed into a single per-operation value."""
+    total = []
+    for k in kernel.split(","):
+        vals = []
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(path) as fh:
+                for row in csv.DictReader(fh):
+                    if k in row.get("Kernel_Name", "") and row.get("Counter_Name") == name:
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return []
+        total.append(statistics.median(vals))
+    return [sum(total)]
 
 
 def main():

@@ -14,7 +14,21 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = [1, 2]
+ALGOS = [1, 2, 4]
+
+
+@pytest.fixture(autouse=True, params=["auto", "3", "8"])
+def panels(request, monkeypatch):
+    """The panel algorithm (4) picks ~4 MiB of x per panel, i.e. one panel for
+    these small matrices; force 3 and 8 panels too so the multi-panel path
+    (interleaved grid + partial reduce) is exercised.  Other algorithms
+    ignore SBLAS_PANELS, so only algo 4 tests are repeated."""
+    algo = request.node.callspec.params.get("algo") if hasattr(request.node, "callspec") else None
+    if request.param != "auto":
+        if algo != 4:
+            pytest.skip("panel count only affects algo 4")
+        monkeypatch.setenv("SBLAS_PANELS", request.param)
+    yield
 
 
 def random_csr(rng, m, n, density_rows, long_rows=(), empty_frac=0.1):
@@ -126,9 +140,10 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
     rp, col, val = orc.gen_synth(n)
     x = orc.gen_vector(n, 43)
     outs = [run_gpu(torch_cuda, sb, a, n, rp, col, val, x, 1.0, 0.0, np.zeros(n))
-            for a in (1, 1, 2, 2)]
+            for a in (1, 1, 2, 2, 4, 4)]
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[2], outs[3])
+    assert np.array_equal(outs[4], outs[5])
 
 
 @pytest.mark.parametrize("version", ["baseline", "v1", "v2"])
