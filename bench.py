@@ -100,11 +100,17 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel"], default="panel")
-    ap.add_argument("--n", type=int, default=2_000_000)
+    ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
     ap.add_argument("--cols", choices=["random", "prefix"], default="random")
     ap.add_argument("--exchange", choices=["allgather", "allreduce"], default="allgather")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the "
+                         "multi-rank path with several ranks on one GPU")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, verify the assembled y of one fresh step against the "
+                         "oracle (rank 0; small n only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -119,15 +125,20 @@ def main() -> int:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
               file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev_idx = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     algo = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL}[args.algo]
-    n = args.n
+    n = args.nrows
     rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
     nnz = int(rowptr[-1])
     plan = sblas_dist.make_plan(rowptr, n, world)
@@ -144,7 +155,7 @@ def main() -> int:
 
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
-    op = sblas_dist.DistSpMV(plan, rank, local_rank, rowptr, col, val, algo, torch, dist,
+    op = sblas_dist.DistSpMV(plan, rank, dev_idx, rowptr, col, val, algo, torch, dist,
                              args.exchange)
     local_bytes = op.A.algorithmic_bytes(BETA != 0.0)
     local_flops = 2.0 * (i1 - i0)
@@ -176,7 +187,26 @@ def main() -> int:
         el = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    stats = torch.tensor([el, kern_ms, local_bytes, local_flops], dtype=torch.float64, device=dev)
+    check = None
+    if args.check:
+        # one fresh step from y0 = 0, then compare the assembled y (every rank
+        # holds it) with the oracle on rank 0 -- verification only
+        with torch.cuda.stream(stream):
+            op.load_y(torch.zeros(plan.m, dtype=torch.float64, device=dev))
+            step()
+        torch.cuda.synchronize()
+        y_dev = op.result().cpu().numpy()
+        if rank == 0:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import orc  # oracle: checker only
+            col_all, val_all = sblas.gen_synth_rows(n, rowptr, 0, n, args.heavy, args.light,
+                                                    prefix=args.cols == "prefix", seed=42)
+            want = orc.csr_spmv(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
+            bound = orc.spmv_bound(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
+            check = bool(np.all(np.abs(y_dev - want) <= bound))
+    stats_dev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
+    stats = torch.tensor([el, kern_ms, local_bytes, local_flops], dtype=torch.float64,
+                         device=stats_dev)
     if dist is not None:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -191,7 +221,10 @@ def main() -> int:
 
     if rank == 0:
         achieved = local_bytes / (kern_ms * 1e-3) / 1e9  # rank 0's kernel
-        traffic = pmc_traffic(args.algo) if world == 1 else None
+        # the committed PMC summary was collected on the default workload only
+        profiled = world == 1 and args.cols == "random" and n == 2_000_000 and \
+            (args.heavy, args.light) == (96, 9)
+        traffic = pmc_traffic(args.algo) if profiled else None
         out = {
             "metric": METRIC,
             "value": round(total_flops / (ms_step * 1e-3) / 1e9, 3),
@@ -228,6 +261,10 @@ def main() -> int:
             "algorithmic_bytes_all_ranks": int(tot_bytes),
             "host_gen_s": round(t_gen, 2),
         }
+        if world > 1 and args.dist_backend != "nccl":
+            out["note"] = f"rehearsal: {world} ranks on {ndev} GPU(s) over {args.dist_backend}"
+        if check is not None:
+            out["check_vs_oracle"] = check
         if world == 1 and not args.no_cpu_baseline:
             rp_all = rowptr
             out["cpu_baseline"] = cpu_baseline(rp_all, col, val, x_h, plan.m, nnz, args.cpu_budget)

@@ -102,7 +102,12 @@ class DistSpMV:
         if self.plan.world == 1:
             return
         if self.exchange_mode == "allgather":
-            self.dist.all_gather_into_tensor(self.gathered, self.y_local)
+            if self.dist.get_backend() == "nccl":
+                self.dist.all_gather_into_tensor(self.gathered, self.y_local)
+            else:  # gloo rehearsal path (CPU staging)
+                chunks = [c.cpu() for c in self.gathered.chunk(self.plan.world)]
+                self.dist.all_gather(chunks, self.y_local.cpu())
+                self.gathered.copy_(self.torch.cat(chunks).to(self.gathered.device))
             sblas.check(sblas.lib.sblas_assemble_slices(
                 self.gathered.data_ptr(), self.plan.world, self.plan.stride, self.meta.data_ptr(),
                 self.y_full.data_ptr(), self.rank, self.y_local.data_ptr(), stream),
@@ -110,7 +115,12 @@ class DistSpMV:
         else:  # literal allreduce of y (config 3)
             self.y_full.zero_()
             self.y_full[self.r0:self.r1].copy_(self.y_local[: self.dm])
-            self.dist.all_reduce(self.y_full)
+            if self.dist.get_backend() == "nccl":
+                self.dist.all_reduce(self.y_full)
+            else:
+                h = self.y_full.cpu()
+                self.dist.all_reduce(h)
+                self.y_full.copy_(h.to(self.y_full.device))
             self.y_local[: self.dm].copy_(self.y_full[self.r0:self.r1])
             if self.cont and self.dm > 0:
                 self.y_local[0] = 0.0

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Rehearse bench.py's multi-rank path on a 1-GPU box: several ranks share the
+# GPU and talk over gloo (RCCL refuses two ranks on one GPU).  Each run checks
+# the assembled y against the oracle (--check).  Outputs under gpurun_out/.
+set -o pipefail
+O=gpurun_out; mkdir -p $O
+port=29611
+for np in 2 3 4; do for ex in allgather allreduce; do for algo in panel rowsplit csr5; do
+  port=$((port+1))
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
+    --master-addr 127.0.0.1 --master-port $port bench.py --gpus $np --dist-backend gloo \
+    --nrows 200000 --steps 3 --warmup 1 --check --exchange $ex --algo $algo \
+    > $O/rehearsal_${np}_${ex}_${algo}.log 2>&1 || { echo "FAIL np=$np $ex $algo"; tail -20 $O/rehearsal_${np}_${ex}_${algo}.log; exit 1; }
+  grep -h '^{' $O/rehearsal_${np}_${ex}_${algo}.log | python3 -c "
+import sys,json
+d=json.loads(sys.stdin.read()); print('np=$np $ex $algo check=', d.get('check_vs_oracle'), d['value'])"
+done; done; done
+# torchrun with one rank over RCCL (the driver's N=1 launch shape)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port $((port+1)) bench.py --gpus 1 --no-cpu-baseline --check --nrows 200000 > $O/rehearsal_1_nccl.log 2>&1 || exit 1
+grep -h '^{' $O/rehearsal_1_nccl.log | cut -c1-200
