@@ -176,6 +176,11 @@ int sblas_gen_synth_rows(int n, int heavy, int light, int prefix_cols,
                          unsigned long long seed, const long long *rowptr,
                          int row_begin, int row_end, int *col, double *val);
 int sblas_gen_vector(int n, unsigned long long seed, double *v);
+/* Unit-lower-triangular CSC (diagonal first) for SpTRSV benchmarks:
+ * `offd` distinct rows per column within (j, j+band], values
+ * (1 + r%10)/(20*row_len).  rowidx == NULL: colptr only. */
+int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed,
+                           int *colptr, int *rowidx, double *val);
 
 #ifdef __cplusplus
 }

@@ -353,6 +353,61 @@ int sblas_gen_synth_rows(int n, int heavy, int light, int prefix_cols,
     return SBLAS_OK;
 }
 
+// Unit-lower-triangular CSC stand-in for circuit5M-class SpTRSV (SURVEY
+// M1-cfg5): column j holds its unit diagonal first, then `offd` distinct rows
+// drawn uniformly from (j, min(n-1, j+band)] (fewer near the end), sorted.
+// Off-diagonal value = (1 + r%10) / (20 * row_len(i)), r from the column's
+// SplitMix64 stream, so every row's off-diagonal sum stays <= 0.5 and the
+// forward solve is well conditioned.  Two calls: colptr only (rowidx NULL),
+// then the full arrays.
+int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed, int *colptr,
+                           int *rowidx, double *val)
+{
+    if (n < 0 || offd < 0 || band < 1 || !colptr) return SBLAS_ERR_INVALID;
+    colptr[0] = 0;
+    for (int j = 0; j < n; ++j) {
+        const long long room = std::min<long long>((long long)n - 1 - j, band);
+        colptr[j + 1] = colptr[j] + 1 + (int)std::min<long long>(offd, room);
+    }
+    if (!rowidx) return SBLAS_OK;
+    std::vector<int> rowlen((size_t)n, 1);
+    std::vector<unsigned char> draw((size_t)colptr[n]);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int j = 0; j < n; ++j) {
+        unsigned long long st = seed ^ ((unsigned long long)(j + 1) * 0x9E3779B97F4A7C15ULL);
+        const int a = colptr[j], b = colptr[j + 1];
+        rowidx[a] = j;
+        const long long room = std::min<long long>((long long)n - 1 - j, band);
+        for (int k = a + 1; k < b; ++k) {
+            for (;;) {
+                const unsigned long long r = splitmix(st);
+                const int v = j + 1 + (int)(((unsigned __int128)r * (unsigned long long)room) >> 64);
+                bool dup = false;
+                for (int t = a + 1; t < k; ++t)
+                    if (rowidx[t] == v) {
+                        dup = true;
+                        break;
+                    }
+                if (!dup) {
+                    rowidx[k] = v;
+                    break;
+                }
+            }
+        }
+        std::sort(rowidx + a + 1, rowidx + b);
+        for (int k = a + 1; k < b; ++k) draw[(size_t)k] = (unsigned char)(splitmix(st) % 10);
+    }
+    for (int j = 0; j < n; ++j)
+        for (int k = colptr[j] + 1; k < colptr[j + 1]; ++k) rowlen[(size_t)rowidx[k]]++;
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < n; ++j) {
+        val[colptr[j]] = 1.0;
+        for (int k = colptr[j] + 1; k < colptr[j + 1]; ++k)
+            val[k] = (1.0 + draw[(size_t)k]) / (20.0 * rowlen[(size_t)rowidx[k]]);
+    }
+    return SBLAS_OK;
+}
+
 int sblas_gen_vector(int n, unsigned long long seed, double *v)
 {
     if (n < 0 || !v) return SBLAS_ERR_INVALID;

@@ -88,6 +88,7 @@ _sig("sblas_partition_rowblock", _i, _i, _i, _p)
 _sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
 _sig("sblas_gen_synth_rows", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _i, _i, _p, _p)
 _sig("sblas_gen_vector", _i, _i, C.c_ulonglong, _p)
+_sig("sblas_gen_lower_banded", _i, _i, _i, _i, C.c_ulonglong, _p, _p, _p)
 
 
 def check(st: int, what: str = "") -> None:
@@ -160,6 +161,18 @@ def gen_synth_rows(n: int, rowptr: np.ndarray, r0: int, r1: int, heavy: int = 96
     check(lib.sblas_gen_synth_rows(n, heavy, light, int(prefix), seed, ptr(rowptr), r0, r1,
                                    ptr(col), ptr(val)), "gen_synth_rows")
     return col[:cnt], val[:cnt]
+
+
+def gen_lower_banded(n: int, offd: int, band: int, seed: int = 47):
+    """Unit-lower CSC (colptr, rowidx, val), diagonal first per column."""
+    cp = np.zeros(n + 1, np.int32)
+    check(lib.sblas_gen_lower_banded(n, offd, band, seed, ptr(cp), None, None), "gen_lower_banded")
+    nnz = int(cp[-1])
+    ri = np.zeros(max(nnz, 1), np.int32)
+    v = np.zeros(max(nnz, 1), np.float64)
+    check(lib.sblas_gen_lower_banded(n, offd, band, seed, ptr(cp), ptr(ri), ptr(v)),
+          "gen_lower_banded")
+    return cp, ri[:nnz], v[:nnz]
 
 
 def gen_vector(n: int, seed: int) -> np.ndarray:

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""SpTRSV benchmark (BASELINE configs[4]), one GPU.
+
+circuit5M-class stand-in (circuit5M itself is not in the container): n =
+5,558,326 unit-lower CSC, 5 off-diagonal rows per column drawn from a band of
+80,000 below the diagonal (~985 level sets, nnz 33.35M incl. diagonal), values
+(1 + r%10)/(20*row_len) (sblas_gen_lower_banded), x_ref in {1..10}, b = L x_ref.
+
+Reports both executors (0 = CSC push / reference algorithm, 1 = CSR pull) with
+HIP-event timing around sblas_trsv_solve, GFLOP/s = 2*nnz/t
+(sptrsv_syncfree_cuda.h:604), algorithmic bytes 12*nnz + 4*(n+1) + 16*n, and
+the reference's own serial executor (oracle/_ref, sptrsv_syncfree_serialref.h)
+timed on one host core as the CPU baseline.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nrows", type=int, default=5_558_326)
+    ap.add_argument("--offd", type=int, default=5)
+    ap.add_argument("--band", type=int, default=80_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import sblas
+
+    n = args.nrows
+    cp, ri, v = sblas.gen_lower_banded(n, args.offd, args.band, 47)
+    nnz = len(ri)
+    xref = np.floor(sblas.gen_vector(n, 48) * 10.0) + 1.0
+    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
+    b = np.bincount(ri, weights=v * xref[cols], minlength=n)
+    dev = torch.device("cuda", 0)
+    dcp, dri, dv, db = (torch.from_numpy(a).to(dev) for a in (cp, ri, v, b))
+    dx = torch.zeros(n, dtype=torch.float64, device=dev)
+    t0 = time.perf_counter()
+    T = sblas.DeviceTRSV(0, n, nnz, dcp.data_ptr(), dri.data_ptr(), dv.data_ptr(), 0)
+    setup_s = time.perf_counter() - t0
+    levels = T.levels()
+    abytes = 12 * nnz + 4 * (n + 1) + 16 * n
+    res = {}
+    s = torch.cuda.Stream(device=dev)
+    for algo, name in ((1, "pull_csr"), (0, "push_csc")):
+        with torch.cuda.stream(s):
+            T.solve(algo, db.data_ptr(), dx.data_ptr(), s.cuda_stream)  # warm-up
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(args.steps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                T.solve(algo, db.data_ptr(), dx.data_ptr(), s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                ms.append(e0.elapsed_time(e1))
+        x = dx.cpu().numpy()
+        rel = float(np.abs(x - xref).sum() / np.abs(xref).sum())
+        t = float(np.median(ms))
+        res[name] = {"ms": round(t, 4), "gflops": round(2.0 * nnz / t / 1e6, 3),
+                     "gbps_algorithmic": round(abytes / t / 1e6, 1),
+                     "rel_l1_vs_xref": rel}
+    T.close()
+    out = {
+        "metric": "fp64 sync-free SpTRSV GFLOP/s (2*nnz/t), 1 MI355X",
+        "value": max(r["gflops"] for r in res.values()),
+        "unit": "GFLOP/s", "n_gpus": 1, "steps": args.steps, "higher_is_better": True,
+        "dtype": "f64", "data": "synthetic circuit5M-class lower triangle (DESIGN.md)",
+        "config": {"workload": "sptrsv forward, unit-lower CSC", "n": n, "nnz": nnz,
+                   "offd_per_col": args.offd, "band": args.band, "levels": levels},
+        "executors": res, "algorithmic_bytes": abytes, "setup_s": round(setup_s, 3),
+        "roofline": {"bound": "hbm (latency: level chain)", "peak": 8000.0, "unit": "GB/s"},
+    }
+    if not args.no_cpu_baseline:
+        ref = os.path.join(ROOT, "oracle", "_ref", "libsblas_ref.so")
+        if os.path.exists(ref):
+            lib = C.CDLL(ref)
+            f = lib.ref_sptrsv_serial
+            f.restype = C.c_int
+            f.argtypes = [C.c_void_p] * 3 + [C.c_int] * 4 + [C.c_void_p] * 2
+            xs = np.zeros(n)
+            t0 = time.perf_counter()
+            f(cp.ctypes.data, ri.ctypes.data, v.ctypes.data, n, nnz, 0, 1, b.ctypes.data, xs.ctypes.data)
+            ts = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": round(2.0 * nnz / ts / 1e9, 3), "unit": "GFLOP/s",
+                                   "cores": 1, "kind": "reference",
+                                   "sample": f"reference sptrsv_syncfree_analyser+_executor "
+                                             f"(oracle/_ref) on the full matrix: {ts * 1e3:.1f} ms",
+                                   "rel_l1_vs_xref": float(np.abs(xs - xref).sum() / np.abs(xref).sum())}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
