@@ -17,12 +17,14 @@
 //     `s_waitcnt vmcnt(0)`, then the in-degree counters are bumped; the
 //     consumer polls its counter with an sc1 (L1-bypassing) load and reads
 //     left_sum with an sc1 load -- no L2 write-back fence per column.
-//   * pull (algo 1, CSR with ready flags): x_i is stored sc1, drained with
-//     `s_waitcnt vmcnt(0)`, then ready[i] is stored sc1; consumers poll the
-//     flag sc1 and load x sc1.  No float atomics: sums are deterministic.
-//     One LANE per row; lanes never block inside an iteration, so rows that
-//     depend on rows of the same wave resolve across iterations.
+//   * pull (algo 1, CSR): x itself is the ready flag -- x is pre-filled with
+//     a signalling-NaN pattern no arithmetic can produce, x_i is published by
+//     one 8-byte sc1 store and consumed by one sc1 load.  No float atomics:
+//     sums are deterministic.  One LANE per row; lanes never block inside an
+//     iteration, so rows that depend on rows of the same wave resolve across
+//     iterations.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -111,14 +113,33 @@ __global__ __launch_bounds__(256) void k_trsv_push(
     }
 }
 
-// ---- pull: one lane per row over CSR, ready flags -------------------------
+// ---- pull: one lane per row over CSR, x itself is the ready flag -----------
+// x is pre-filled with a signalling-NaN bit pattern that no arithmetic result
+// can equal (IEEE operations return quiet NaNs), so one 8-byte sc1 store
+// publishes x_i and one sc1 load both tests and fetches it.  Each lane loads
+// up to 8 of its row's dependencies at once and consumes the ready prefix in
+// column order (fixed summation order -> deterministic).
 // Row layout: forward (lower) = off-diagonals ascending, diagonal LAST;
 // backward (upper, rows processed from n-1 down) = diagonal FIRST.
+constexpr unsigned long long kXPending = 0x7FF4DEADBEEF5A5AULL;
+
+__global__ void k_fill_pending(unsigned long long *__restrict__ x, int n)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = kXPending;
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void k_trsv_pull(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, int n, int backward, const double *__restrict__ b,
-    double *x, int *ready, unsigned *ctl)
+    unsigned long long *xbits, unsigned *ctl)
 {
+    constexpr int kBatch = 8;
     const int lane = threadIdx.x & 63;
     for (;;) {
         int t0 = 0;
@@ -144,22 +165,51 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
         }
         bool pending = live;
         unsigned spins = 0;
+        // current dependency cached in registers: a spin costs ONE sc1 load
+        int cj = (live && j < jend) ? col[j] : 0;
+        double vj = (live && j < jend) ? val[j] : 0.0;
         while (__any(pending)) {
-            if (pending) {
-                // consume every dependency that is already available
-                while (j < jend) {
-                    const int c = col[j];
-                    if (ld_sc1_i32(&ready[c]) == 0) break;
-                    sum += val[j] * ld_sc1_f64(&x[c]);
+            if (pending && j < jend) {
+                const unsigned long long x0 = ld_sc1_u64(xbits + cj);
+                if (x0 != kXPending) {
+                    sum += vj * __longlong_as_double((long long)x0);
                     ++j;
+                    if (j < jend) {  // ready: batch the next dependencies
+                        int cc[kBatch - 1];
+                        double vv[kBatch - 1];
+                        unsigned long long xb[kBatch - 1];
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) {  // clamped, unconditional
+                            const int jj = min(j + k, jend - 1);
+                            cc[k] = col[jj];
+                            vv[k] = val[jj];
+                        }
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) xb[k] = ld_sc1_u64(xbits + cc[k]);
+                        bool open = true;
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) {
+                            if (open && j < jend) {
+                                if (xb[k] == kXPending) {
+                                    open = false;
+                                } else {
+                                    sum += vv[k] * __longlong_as_double((long long)xb[k]);
+                                    ++j;
+                                }
+                            }
+                        }
+                        if (j < jend) {
+                            cj = col[j];
+                            vj = val[j];
+                        }
+                    }
                 }
-                if (j == jend) {
-                    const double xi = (b[i] - sum) / diag;
-                    __hip_atomic_store(&x[i], xi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(&ready[i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pending = false;
-                }
+            }
+            if (pending && j == jend) {
+                const double xi = (b[i] - sum) / diag;
+                __hip_atomic_store(xbits + i, (unsigned long long)__double_as_longlong(xi),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pending = false;
             }
             if (__any(pending)) {
                 __builtin_amdgcn_s_sleep(1);
@@ -176,7 +226,9 @@ static int grid_for(int dev)
 {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 1024;
-    return p.multiProcessorCount * 4;  // resident 256-thread workgroups, margin kept
+    int per_cu = 4;  // 256-thread workgroups per CU; waves beyond residency just queue
+    if (const char *e = getenv("SBLAS_TRSV_WG_PER_CU")) per_cu = std::max(1, std::min(16, atoi(e)));
+    return p.multiProcessorCount * per_cu;
 }
 
 }  // namespace sblas
@@ -251,15 +303,17 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     DeviceGuard g(T->device);
     hipStream_t s = (hipStream_t)stream;
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, 16, s));
-    SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
     const int grid = grid_for(T->device);
     if (algo == 0) {
+        SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
         SBLAS_HIP(hipMemsetAsync(T->left, 0, sizeof(double) * T->n, s));
         hipLaunchKernelGGL(k_trsv_push, dim3(grid), dim3(256), 0, s, T->colptr, T->rowidx, T->val,
                            T->in_degree, T->n, T->substitution, d_b, d_x, T->done, T->left, T->ctl);
     } else {
+        hipLaunchKernelGGL(k_fill_pending, dim3((T->n + 255) / 256), dim3(256), 0, s,
+                           (unsigned long long *)d_x, T->n);
         hipLaunchKernelGGL(k_trsv_pull, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
-                           T->n, T->substitution, d_b, d_x, T->done, T->ctl);
+                           T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl);
     }
     SBLAS_HIP(hipGetLastError());
     unsigned h[4] = {0, 0, 0, 0};
