@@ -43,13 +43,17 @@ struct sblas_trsv_s {
     // scratch
     int *done = nullptr;       // push: arrivals per row; pull: ready flags
     double *left = nullptr;    // push: left sums
-    unsigned *ctl = nullptr;   // [0] ticket, [1] timeout flag (16-byte block)
+    unsigned *ctl = nullptr;   // [0] ticket, [kAbort] timeout flag (kCtlBytes block)
     int nlevels = -1;
 };
 
 namespace sblas {
 
-constexpr unsigned kSpinLimit = 1u << 26;
+constexpr unsigned kSpinLimit = 1u << 25;  // ~1 s of polling per wave
+// control block: ticket counter at word 0, abort/timeout word on its own
+// 128-B line (word 32) -- polling it next to the hot ticket atomics is slow
+constexpr int kAbort = 32;
+constexpr int kCtlBytes = 256;
 
 __device__ __forceinline__ int ld_sc1_i32(const int *p)
 {
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(256) void k_trsv_push(
     const int lane = threadIdx.x & 63;
     for (;;) {
         int t = 0;
-        if (lane == 0) t = (int)atomicAdd(&ctl[0], 1u);
+        if (lane == 0) t = ld_sc1_i32((const int *)&ctl[kAbort]) ? n : (int)atomicAdd(&ctl[0], 1u);
         t = __shfl(t, 0, 64);
         if (t >= n) return;
         const int i = backward ? n - 1 - t : t;
@@ -85,16 +89,21 @@ __global__ __launch_bounds__(256) void k_trsv_push(
         const double diag = val[dpos];
         const int need = in_degree[i] - 1;
         // wait for all left contributions (one lane polls)
+        int bail = 0;
         if (lane == 0) {
             unsigned spins = 0;
             while (ld_sc1_i32(&done[i]) != need) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > kSpinLimit) {
-                    atomicOr(&ctl[1], 1u);
-                    break;
+                if ((++spins & 1023u) == 0) {
+                    if (spins > kSpinLimit) atomicOr(&ctl[kAbort], 1u);
+                    if (ld_sc1_i32((const int *)&ctl[kAbort])) {
+                        bail = 1;
+                        break;
+                    }
                 }
             }
         }
+        if (__shfl(bail, 0, 64)) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double xi = 0.0;
         if (lane == 0) {
@@ -143,9 +152,9 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
     const int lane = threadIdx.x & 63;
     for (;;) {
         int t0 = 0;
-        if (lane == 0) t0 = (int)atomicAdd(&ctl[0], 64u);
+        if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? n : (int)atomicAdd(&ctl[0], 64u);
         t0 = __shfl(t0, 0, 64);
-        if (t0 >= n) return;
+        if (t0 >= n) return;  // done, or another wave timed out: the solve is void
         const int t = t0 + lane;
         const bool live = t < n;
         const int i = live ? (backward ? n - 1 - t : t) : 0;
@@ -212,10 +221,14 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
                 pending = false;
             }
             if (__any(pending)) {
+                // a timeout voids the whole solve (every wave exits)
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > kSpinLimit) {
-                    if (lane == 0) atomicOr(&ctl[1], 1u);
-                    break;
+                if ((++spins & 1023u) == 0) {
+                    if (spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(&ctl[kAbort], 1u);
+                        return;
+                    }
+                    if (ld_sc1_i32((const int *)&ctl[kAbort])) return;
                 }
             }
         }
@@ -226,8 +239,11 @@ static int grid_for(int dev)
 {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 1024;
-    int per_cu = 4;  // 256-thread workgroups per CU; waves beyond residency just queue
-    if (const char *e = getenv("SBLAS_TRSV_WG_PER_CU")) per_cu = std::max(1, std::min(16, atoi(e)));
+    // 256-thread workgroups per CU.  More spinning waves is slower: every
+    // polling lane costs an L2 request the producers need (config 5, pull:
+    // 1/CU 2.44 ms, 2/CU 2.99 ms, 4/CU 4.92 ms; 8/CU starves the chain).
+    int per_cu = 1;
+    if (const char *e = getenv("SBLAS_TRSV_WG_PER_CU")) per_cu = std::max(1, std::min(4, atoi(e)));
     return p.multiProcessorCount * per_cu;
 }
 
@@ -262,7 +278,7 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz, const int *d_
     if ((e = hipMalloc(&T->in_degree, sizeof(int) * std::max(n, 1))) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&T->done, sizeof(int) * std::max(n, 1))) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&T->left, sizeof(double) * std::max(n, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&T->ctl, 16)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&T->ctl, kCtlBytes)) != hipSuccess) return fail(e);
     if ((e = hipMemcpyAsync(T->colptr, d_colptr, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(e);
     if (nnz) {
         if ((e = hipMemcpyAsync(T->rowidx, d_rowidx, sizeof(int) * nnz, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(e);
@@ -302,7 +318,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     if (T->n == 0) return SBLAS_OK;
     DeviceGuard g(T->device);
     hipStream_t s = (hipStream_t)stream;
-    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, 16, s));
+    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     const int grid = grid_for(T->device);
     if (algo == 0) {
         SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
@@ -316,10 +332,10 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
                            T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl);
     }
     SBLAS_HIP(hipGetLastError());
-    unsigned h[4] = {0, 0, 0, 0};
-    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, 16, hipMemcpyDeviceToHost, s));
+    unsigned h[kCtlBytes / 4] = {0};
+    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, kCtlBytes, hipMemcpyDeviceToHost, s));
     SBLAS_HIP(hipStreamSynchronize(s));
-    if (h[1]) {
+    if (h[kAbort]) {
         set_error("sptrsv: spin limit exceeded (matrix not triangular or missing diagonal?)");
         return SBLAS_ERR_HIP;
     }
