@@ -96,6 +96,21 @@ struct PanelPlan {
     bool ready = false;
 };
 
+// SpMM plan: 16-row blocks whose column union is dense enough run on MFMA
+// (v_mfma_f64_16x16x4f64 over a dense 16 x |U| A tile); other rows take the
+// row-wave FMA kernel.
+struct SpmmPlan {
+    int nmfma = 0;             // MFMA blocks
+    int *mblock = nullptr;     // [nmfma] 16-row block index
+    int *mchunk = nullptr;     // [nmfma+1] offsets in 4-column chunks
+    int *ucol = nullptr;       // [4*chunks] union columns (padded)
+    double *atile = nullptr;   // [chunks*64] A fragments, lane-major
+    int nsparse = 0;           // rows handled by the row-wave kernel
+    int *srows = nullptr;
+    double fill_thresh = 0.25;
+    bool ready = false;
+};
+
 struct RsPlan {
     int nblocks = 0;
     RowBlock *blocks = nullptr;
@@ -118,6 +133,7 @@ struct sblas_csr_s {
     sblas::RsPlan rs;
     sblas::Csr5Plan c5;
     sblas::PanelPlan pn;
+    sblas::SpmmPlan mm;
     std::vector<int> h_rowptr;  // host copy (analysis)
 };
 
@@ -137,6 +153,8 @@ int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x,
 int build_panel_plan(sblas_csr_s &A, hipStream_t s);
 int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s);
 
+int build_spmm_plan(sblas_csr_s &A, hipStream_t s);
+void free_spmm_plan(sblas_csr_s &A);
 int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
                 int ldb, int b_layout, double beta, double *C, int ldc,
                 hipStream_t s);

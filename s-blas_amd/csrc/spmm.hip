@@ -9,11 +9,23 @@
 // host layout) is transposed once into a row-major panel owned by the
 // handle (k_transpose_B, LDS-tiled 64x64).
 //
-// Kernel: one wave per (row of A, 64-column slab of C).  The wave loads 64
-// (col, val) pairs of the row with one coalesced load each, then broadcasts
-// them lane-to-lane (__shfl) while every lane FMAs its column of B; eight
-// independent B-row loads are kept in flight.  Accumulation order per C entry
-// is the row's storage order (same as the oracle).
+// Kernels:
+//  * row-wave: one wave per (row of A, 64-column slab of C).  The wave loads
+//    64 (col, val) pairs of the row with one coalesced load each, then
+//    broadcasts them lane-to-lane (__shfl) while every lane FMAs its column
+//    of B; eight independent B-row loads are kept in flight.  Accumulation
+//    order per C entry is the row's storage order (same as the oracle).
+//  * MFMA B-panel tile: for a 16-row block whose column union U
+//    is dense (nnz / (16|U|) >= fill threshold), A is stored as a dense
+//    16 x |U| tile and C(16 x 64) += A_tile * B[U, :] runs as
+//    v_mfma_f64_16x16x4f64 over 4-column k-chunks -- each B row is read once
+//    per 16 rows instead of once per nonzero.  This is a real contraction
+//    only when rows share columns (banded / FEM-block matrices); a random
+//    matrix like rail4284 has no dense blocks and stays on the row-wave
+//    kernel.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -25,12 +37,12 @@ __global__ __launch_bounds__(256) void k_spmm_rowwave(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ B, long long ldb,
     int m, int n, int nslab, double alpha, double beta, double *__restrict__ C,
-    long long ldc)
+    long long ldc, const int *__restrict__ rows)
 {
     const int lane = threadIdx.x & 63;
     const long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= (long long)m * nslab) return;
-    const int r = (int)(w / nslab);
+    const int r = rows ? rows[w / nslab] : (int)(w / nslab);
     const int c = (int)(w % nslab) * 64 + lane;
     const bool live = c < n;
     const int cc = live ? c : 0;
@@ -62,6 +74,128 @@ __global__ __launch_bounds__(256) void k_spmm_rowwave(
         double *o = C + (long long)c * ldc + r;
         *o = kBeta ? alpha * acc + beta * *o : alpha * acc;
     }
+}
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// One wave per (MFMA block, 64-column group of C): 4 accumulators of
+// 16 x 16.  f64 MFMA lane maps (cdna_hip_programming.md §3): A[i=l&15][k=l>>4],
+// B[k=l>>4][j=l&15], D col = l&15, row = (l>>4) + 4*reg.
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmm_mfma(
+    const int *__restrict__ mblock, const int *__restrict__ mchunk, const int *__restrict__ ucol,
+    const double *__restrict__ atile, int nmfma, const double *__restrict__ B, long long ldb,
+    int m, int n, int ngrp, double alpha, double beta, double *__restrict__ C, long long ldc)
+{
+    const int lane = threadIdx.x & 63;
+    const long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (long long)nmfma * ngrp) return;
+    const int q = (int)(w / ngrp), g = (int)(w % ngrp);
+    const int r0 = mblock[q] * 16;
+    const int kq = lane >> 4, jq = lane & 15;
+    v4d acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    int cj[4];
+    bool live[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        cj[t] = g * 64 + t * 16 + jq;
+        live[t] = cj[t] < n;
+        if (!live[t]) cj[t] = 0;
+    }
+    for (int c = mchunk[q]; c < mchunk[q + 1]; ++c) {
+        const double a = atile[(long long)c * 64 + lane];
+        const long long brow = (long long)ucol[c * 4 + kq] * ldb;
+        double b[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = live[t] ? B[brow + cj[t]] : 0.0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[t], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (!live[t]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = r0 + kq + 4 * r;
+            if (row < m) {
+                double *o = C + (long long)cj[t] * ldc + row;
+                *o = kBeta ? alpha * acc[t][r] + beta * *o : alpha * acc[t][r];
+            }
+        }
+    }
+}
+
+int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.mm.ready) return SBLAS_OK;
+    SpmmPlan &P = A.mm;
+    if (const char *e = getenv("SBLAS_SPMM_MFMA_FILL")) P.fill_thresh = atof(e);
+    const int m = A.m;
+    const std::vector<int> &rp = A.h_rowptr;
+    std::vector<int> hcol((size_t)A.nnz);
+    std::vector<double> hval((size_t)A.nnz);
+    if (A.nnz) {
+        SBLAS_HIP(hipMemcpy(hcol.data(), A.col, sizeof(int) * A.nnz, hipMemcpyDeviceToHost));
+        SBLAS_HIP(hipMemcpy(hval.data(), A.val, sizeof(double) * A.nnz, hipMemcpyDeviceToHost));
+    }
+    std::vector<int> mblock, mchunk{0}, ucol, srows;
+    std::vector<double> atile;
+    std::vector<int> U;
+    const int nblk = (m + 15) / 16;
+    for (int b = 0; b < nblk; ++b) {
+        const int r0 = b * 16, r1 = std::min(m, r0 + 16);
+        U.assign(hcol.begin() + rp[r0], hcol.begin() + rp[r1]);
+        std::sort(U.begin(), U.end());
+        U.erase(std::unique(U.begin(), U.end()), U.end());
+        const long long nz = rp[r1] - rp[r0];
+        const bool dense = P.fill_thresh <= 1.0 && !U.empty() &&
+                           (double)nz >= P.fill_thresh * 16.0 * (double)U.size();
+        if (!dense) {
+            for (int r = r0; r < r1; ++r) srows.push_back(r);
+            continue;
+        }
+        const int nch = ((int)U.size() + 3) / 4;
+        const size_t t0 = atile.size();
+        atile.resize(t0 + (size_t)nch * 64, 0.0);
+        for (int c = 0; c < nch * 4; ++c) ucol.push_back(c < (int)U.size() ? U[c] : U[0]);
+        for (int r = r0; r < r1; ++r)
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                const int k = (int)(std::lower_bound(U.begin(), U.end(), hcol[j]) - U.begin());
+                // lane l of chunk k/4 holds A[l & 15][4*(k/4) + (l >> 4)]
+                atile[t0 + (size_t)(k / 4) * 64 + (size_t)((k % 4) * 16 + (r - r0))] += hval[j];
+            }
+        mblock.push_back(b);
+        mchunk.push_back(mchunk.back() + nch);
+    }
+    P.nmfma = (int)mblock.size();
+    P.nsparse = (int)srows.size();
+    auto up = [&](auto **dst, const auto &v) -> int {
+        using T = typename std::decay_t<decltype(v)>::value_type;
+        SBLAS_HIP(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
+        if (!v.empty()) SBLAS_HIP(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+        return SBLAS_OK;
+    };
+    SBLAS_TRY(up(&P.mblock, mblock));
+    SBLAS_TRY(up(&P.mchunk, mchunk));
+    SBLAS_TRY(up(&P.ucol, ucol));
+    SBLAS_TRY(up(&P.atile, atile));
+    SBLAS_TRY(up(&P.srows, srows));
+    (void)s;
+    P.ready = true;
+    return SBLAS_OK;
+}
+
+void free_spmm_plan(sblas_csr_s &A)
+{
+    SpmmPlan &P = A.mm;
+    (void)hipFree(P.mblock);
+    (void)hipFree(P.mchunk);
+    (void)hipFree(P.ucol);
+    (void)hipFree(P.atile);
+    (void)hipFree(P.srows);
+    A.mm = SpmmPlan{};
 }
 
 // col-major B (k x n, ld=ldb) -> row-major panel Bt (k x n, ld=n)
@@ -111,15 +245,33 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         Brow = S.bt;
         ldr = n;
     }
+    const SpmmPlan &P = A.mm;
     const int nslab = (n + 63) / 64;
-    const long long waves = (long long)A.m * nslab;
-    const unsigned nb = (unsigned)((waves + 3) / 4);
-    if (beta != 0.0)
-        hipLaunchKernelGGL(k_spmm_rowwave<true>, dim3(nb), dim3(256), 0, s, A.rowptr, A.col, A.val,
-                           Brow, ldr, A.m, n, nslab, alpha, beta, C, (long long)ldc);
-    else
-        hipLaunchKernelGGL(k_spmm_rowwave<false>, dim3(nb), dim3(256), 0, s, A.rowptr, A.col, A.val,
-                           Brow, ldr, A.m, n, nslab, alpha, beta, C, (long long)ldc);
+    // rows of sparse blocks (all rows when no plan / no dense block)
+    const int nrows = P.ready ? P.nsparse : A.m;
+    const int *rows = P.ready ? P.srows : nullptr;
+    if (nrows > 0) {
+        const long long waves = (long long)nrows * nslab;
+        const unsigned nb = (unsigned)((waves + 3) / 4);
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmm_rowwave<true>, dim3(nb), dim3(256), 0, s, A.rowptr, A.col, A.val,
+                               Brow, ldr, nrows, n, nslab, alpha, beta, C, (long long)ldc, rows);
+        else
+            hipLaunchKernelGGL(k_spmm_rowwave<false>, dim3(nb), dim3(256), 0, s, A.rowptr, A.col, A.val,
+                               Brow, ldr, nrows, n, nslab, alpha, beta, C, (long long)ldc, rows);
+    }
+    if (P.ready && P.nmfma > 0) {
+        const long long waves = (long long)P.nmfma * nslab;
+        const unsigned nb = (unsigned)((waves + 3) / 4);
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmm_mfma<true>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
+                               P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
+                               (long long)ldc);
+        else
+            hipLaunchKernelGGL(k_spmm_mfma<false>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
+                               P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
+                               (long long)ldc);
+    }
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;
 }

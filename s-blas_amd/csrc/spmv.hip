@@ -764,6 +764,7 @@ void free_plans(sblas_csr_s &A)
     (void)hipFree(Q.partial);
     (void)hipFree(Q.long_rows);
     A.pn = PanelPlan{};
+    free_spmm_plan(A);
 }
 
 }  // namespace sblas

@@ -31,19 +31,34 @@ def main():
     ap.add_argument("--ncols", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--layout", choices=["row", "col"], default="row")
+    ap.add_argument("--blocky", type=int, default=0,
+                    help="instead of the rail4284 shape: 16-row blocks each dense (~90%%) over "
+                         "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
     args = ap.parse_args()
     import torch
     import sblas
 
     m, k, n = args.m, args.k, args.ncols
-    base, extra = divmod(args.nnz, m)
-    lens = np.full(m, base, np.int64)
-    lens[:extra] += 1
-    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     rng = np.random.default_rng(44)
-    col = np.empty(args.nnz, np.int32)
-    for r in range(m):  # distinct sorted columns per row
-        col[rp[r]:rp[r + 1]] = np.sort(rng.choice(k, size=int(lens[r]), replace=False))
+    if args.blocky:
+        rows = []
+        for _ in range(m // 16):
+            cols = np.sort(rng.choice(k, args.blocky, replace=False))
+            for _ in range(16):
+                rows.append(cols[rng.random(args.blocky) < 0.9])
+        m = len(rows)
+        lens = np.array([len(r) for r in rows], np.int64)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate(rows).astype(np.int32)
+        args.nnz = int(rp[-1])
+    else:
+        base, extra = divmod(args.nnz, m)
+        lens = np.full(m, base, np.int64)
+        lens[:extra] += 1
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.empty(args.nnz, np.int32)
+        for r in range(m):  # distinct sorted columns per row
+            col[rp[r]:rp[r + 1]] = np.sort(rng.choice(k, size=int(lens[r]), replace=False))
     val = np.random.default_rng(45).random(args.nnz)
     dev = torch.device("cuda", 0)
     B = torch.rand((k, n), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(45))
@@ -86,7 +101,9 @@ def main():
         "steps": args.steps, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "dtype": "f64", "data": "synthetic rail4284-shaped (DESIGN.md)",
         "config": {"workload": "C = -0.7*A*B + 0.8*C", "m": m, "k": k, "nnz": args.nnz, "ncols": n,
-                   "b_layout": args.layout},
+                   "b_layout": args.layout, "structure": f"blocky{args.blocky}" if args.blocky
+                   else "rail4284-shaped uniform random",
+                   "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.25")},
         "roofline": {"bound": "hbm", "achieved": round(abytes / ms / 1e6, 1), "peak": 8000.0,
                      "unit": "GB/s", "frac": round(abytes / ms / 1e6 / 8000.0, 4)},
         "gbps_l2_brow_traffic": round(args.nnz * n * 8 / ms / 1e6, 1),

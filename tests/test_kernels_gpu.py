@@ -194,3 +194,46 @@ def test_assemble_slices(torch_cuda, sb):
     torch.cuda.synchronize()
     assert np.array_equal(y.cpu().numpy(), want)
     assert np.array_equal(yl.cpu().numpy(), [0.0, 15.0, 0.0])
+
+
+# ------------------------------------------------------- SpMM MFMA tiles ----
+def block_dense_csr(rng, nblk, width, k, sparse_tail=0):
+    """16-row blocks, each dense over `width` random columns (MFMA path), plus
+    `sparse_tail` random sparse rows (row-wave path)."""
+    rows = []
+    for _ in range(nblk):
+        cols = np.sort(rng.choice(k, width, replace=False))
+        for _ in range(16):
+            keep = cols[rng.random(width) < 0.9]  # ~90% fill
+            rows.append(keep)
+    for _ in range(sparse_tail):
+        rows.append(np.sort(rng.choice(k, 20, replace=False)))
+    lens = np.array([len(r) for r in rows])
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate(rows).astype(np.int32)
+    return rp, col, rng.standard_normal(int(rp[-1]))
+
+
+@pytest.mark.parametrize("fill", ["default", "0", "2"])
+@pytest.mark.parametrize("ncols", [64, 40, 130])
+def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols):
+    torch = torch_cuda
+    if fill != "default":
+        monkeypatch.setenv("SBLAS_SPMM_MFMA_FILL", fill)
+    rng = np.random.default_rng(ncols)
+    k = 3000
+    rp, col, val = block_dense_csr(rng, 12, 37, k, sparse_tail=21)  # m = 213: partial last block
+    m = len(rp) - 1
+    B = rng.standard_normal((k, ncols))
+    C0 = rng.standard_normal((m, ncols))
+    want = orc.spmm(m, ncols, k, 0.75, rp, col, val, B, -0.5, C0)
+    A = sb.DeviceCSR.upload(0, k, rp, col, val)
+    Bd = torch.from_numpy(np.ascontiguousarray(B).ravel()).cuda()
+    Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
+    A.spmm(ncols, 0.75, Bd.data_ptr(), ncols, 1, -0.5, Cd.data_ptr(), m)
+    torch.cuda.synchronize()
+    got = Cd.cpu().numpy().reshape((ncols, m)).T
+    # MFMA sums the dense tile in union-column order (the rows' own order here,
+    # columns are sorted) with exact zeros for the holes: same bound applies
+    assert np.all(np.abs(got - want) <= spmm_bound(rp, col, val, B, 0.75, -0.5, C0))
+    A.close()
