@@ -254,22 +254,11 @@ int sblas_csrmm_mgpu(int m, int n, int k, const double *alpha, int nnz_A, int *c
     return SBLAS_OK;
 }
 
-// sptrsv_syncfree_cuda (sptrsv_v1/src/sptrsv_syncfree_cuda.h:287-670).
-// Prints the reference's timing / validation lines.  opt selects the
-// executor: OPT_WARP_NNZ (1) -> CSC push (reference algorithm), otherwise
-// the CSR pull executor.  Multi-device SpTRSV is not partitioned in this
-// release: ngpu > 1 solves on device 0.
-int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int m,
-                          int n, int nnz, int substitution, int rhs, int opt, double *x,
-                          const double *b, const double *x_ref, double *gflops, int ngpu)
+// Single-device solve for sblas_sptrsv_syncfree: upload, analyse, one warm-up
+// and one timed solve (the reference times exactly one executor run).
+static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int n,
+                             int nnz, int substitution, int opt, double *x, const double *b, double *ms)
 {
-    if (m != n) {
-        printf("This is not a square matrix, return.\n");
-        return -1;
-    }
-    if (rhs != 1 || n < 0 || nnz < 0 || ngpu <= 0 || !cscColPtr || !x || !b) return SBLAS_ERR_INVALID;
-    int count;
-    if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
     DeviceGuard g(0);
     DevBuf dcp, dri, dv, db, dx;
     dcp.dev = dri.dev = dv.dev = db.dev = dx.dev = 0;
@@ -291,10 +280,38 @@ int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const doub
     int st = sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr);  // warm-up
     const double t0 = sblas_get_time();
     if (st == SBLAS_OK) st = sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr);
-    const double ms = (sblas_get_time() - t0) * 1e3;
+    *ms = (sblas_get_time() - t0) * 1e3;
     sblas_trsv_destroy(T);
     if (st != SBLAS_OK) return st;
     SBLAS_HIP(hipMemcpy(x, dx.p, sizeof(double) * n, hipMemcpyDeviceToHost));
+    return SBLAS_OK;
+}
+
+// sptrsv_syncfree_cuda (sptrsv_v1/src/sptrsv_syncfree_cuda.h:287-670).
+// Prints the reference's timing / validation lines.  opt selects the
+// executor: OPT_WARP_NNZ (1) -> CSC push (reference algorithm), otherwise
+// the CSR pull executor.  ngpu > 1 runs the multi-device pull executor
+// (sblas_trsv_mgpu_solve: nnz-balanced blocks of the solve order, x pushed to
+// later blocks over xGMI), which is what sptrsv_v2/v3 distribute.
+int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int m,
+                          int n, int nnz, int substitution, int rhs, int opt, double *x,
+                          const double *b, const double *x_ref, double *gflops, int ngpu)
+{
+    if (m != n) {
+        printf("This is not a square matrix, return.\n");
+        return -1;
+    }
+    if (rhs != 1 || n < 0 || nnz < 0 || ngpu <= 0 || !cscColPtr || !x || !b) return SBLAS_ERR_INVALID;
+    int count;
+    if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
+    double ms = 0.0;
+    if (ngpu > 1) {
+        double warm = 0.0;
+        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, b, x, ngpu, &warm));
+        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, b, x, ngpu, &ms));
+    } else {
+        SBLAS_TRY(sptrsv_one_device(cscColPtr, cscRowIdx, cscVal, n, nnz, substitution, opt, x, b, &ms));
+    }
     const double flop = 2.0 * rhs * (double)nnz;
     printf("cuda syncfree SpTRSV solve used %4.2f ms, throughput is %4.2f gflops\n", ms,
            flop / (1e6 * ms));

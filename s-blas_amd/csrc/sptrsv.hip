@@ -27,6 +27,8 @@
 #include <cstdlib>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "sblas_internal.hpp"
 
 struct sblas_trsv_s {
@@ -235,6 +237,117 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
     }
 }
 
+// ---- multi-device pull (replaces sptrsv_v3's NVSHMEM gets) ----
+// Rows are split into g blocks of the solve order (o = i forward, n-1-i
+// backward).  Device d solves its block and keeps a FULL-length x in
+// fine-grained memory; dependencies always have a smaller order index, so
+// they come from blocks <= d.  A producer publishes x_i with one system-scope
+// store into its own x and into the x of every LATER block (xGMI peer writes
+// when the blocks sit on other GPUs); consumers poll only local memory.
+struct TrsvPart {
+    const int *rowptr;   // local CSR of the block's rows (solve order)
+    const int *col;      // global column indices
+    const double *val;
+    const double *b;     // local b (solve order)
+    unsigned long long *const *xs;  // [g] x arrays (peer pointers); xs[d] = own
+    int g, d, o0, nloc, n, backward;
+};
+
+__device__ __forceinline__ unsigned long long ld_sys_u64(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void k_trsv_pull_part(const TrsvPart P, unsigned *ctl)
+{
+    constexpr int kBatch = 8;
+    const int lane = threadIdx.x & 63;
+    unsigned long long *xl = P.xs[P.d];
+    for (;;) {
+        int t0 = 0;
+        if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? P.nloc : (int)atomicAdd(&ctl[0], 64u);
+        t0 = __shfl(t0, 0, 64);
+        if (t0 >= P.nloc) return;
+        const int t = t0 + lane;
+        const bool live = t < P.nloc;
+        const int o = P.o0 + (live ? t : 0);
+        const int i = P.backward ? P.n - 1 - o : o;
+        int j = 0, jend = 0;
+        double diag = 1.0, sum = 0.0;
+        if (live) {
+            const int a = P.rowptr[t], e = P.rowptr[t + 1];
+            if (P.backward) {
+                diag = P.val[a];
+                j = a + 1;
+                jend = e;
+            } else {
+                diag = P.val[e - 1];
+                j = a;
+                jend = e - 1;
+            }
+        }
+        bool pending = live;
+        unsigned spins = 0;
+        int cj = (live && j < jend) ? P.col[j] : 0;
+        double vj = (live && j < jend) ? P.val[j] : 0.0;
+        while (__any(pending)) {
+            if (pending && j < jend) {
+                const unsigned long long x0 = ld_sys_u64(xl + cj);
+                if (x0 != kXPending) {
+                    sum += vj * __longlong_as_double((long long)x0);
+                    ++j;
+                    if (j < jend) {
+                        int cc[kBatch - 1];
+                        double vv[kBatch - 1];
+                        unsigned long long xb[kBatch - 1];
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) {
+                            const int jj = min(j + k, jend - 1);
+                            cc[k] = P.col[jj];
+                            vv[k] = P.val[jj];
+                        }
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) xb[k] = ld_sys_u64(xl + cc[k]);
+                        bool open = true;
+#pragma unroll
+                        for (int k = 0; k < kBatch - 1; ++k) {
+                            if (open && j < jend) {
+                                if (xb[k] == kXPending) {
+                                    open = false;
+                                } else {
+                                    sum += vv[k] * __longlong_as_double((long long)xb[k]);
+                                    ++j;
+                                }
+                            }
+                        }
+                        if (j < jend) {
+                            cj = P.col[j];
+                            vj = P.val[j];
+                        }
+                    }
+                }
+            }
+            if (pending && j == jend) {
+                const double xi = (P.b[t] - sum) / diag;
+                const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
+                for (int q = P.d; q < P.g; ++q)  // own copy, then every later block's
+                    __hip_atomic_store(P.xs[q] + i, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                pending = false;
+            }
+            if (__any(pending)) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 1023u) == 0) {
+                    if (spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(&ctl[kAbort], 1u);
+                        return;
+                    }
+                    if (ld_sc1_i32((const int *)&ctl[kAbort])) return;
+                }
+            }
+        }
+    }
+}
+
 static int grid_for(int dev)
 {
     hipDeviceProp_t p;
@@ -385,4 +498,178 @@ int sblas_trsv_destroy(sblas_trsv T)
     return SBLAS_OK;
 }
 
+
+// Multi-device solve from HOST CSC (diagonal first / last per column as in the
+// reference).  Returns x on the host.  Partition d's rows run on ordinal
+// d % count; partitions sharing a GPU run in order on that GPU's stream,
+// different GPUs run concurrently (peer access + fine-grained x).
+int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val, int n,
+                          int substitution, const double *b, double *x, int ngpu, double *solve_ms)
+{
+    if (n < 0 || ngpu <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
+    const int nnz = colptr[n];
+    const bool bwd = substitution == 1;
+    // CSC of L == CSR of L^T; stable transpose gives CSR of L with columns
+    // ascending (diagonal last for lower, first for upper)
+    std::vector<int> rp((size_t)n + 1, 0), cl((size_t)std::max(nnz, 1));
+    std::vector<double> vl((size_t)std::max(nnz, 1));
+    for (int e = 0; e < nnz; ++e) rp[(size_t)rowidx[e] + 1]++;
+    for (int i = 0; i < n; ++i) rp[(size_t)i + 1] += rp[(size_t)i];
+    {
+        std::vector<int> nx(rp.begin(), rp.end() - 1);
+        for (int c = 0; c < n; ++c)
+            for (int e = colptr[c]; e < colptr[c + 1]; ++e) {
+                const int o = nx[(size_t)rowidx[e]]++;
+                cl[(size_t)o] = c;
+                vl[(size_t)o] = val[e];
+            }
+    }
+    // order index o -> row i; nnz-balanced blocks of the order
+    auto row_of = [&](int o) { return bwd ? n - 1 - o : o; };
+    std::vector<int> ob(ngpu + 1, n);
+    ob[0] = 0;
+    {
+        long long acc = 0;
+        int d = 1;
+        for (int o = 0; o < n && d < ngpu; ++o) {
+            const int i = row_of(o);
+            acc += rp[(size_t)i + 1] - rp[(size_t)i];
+            while (d < ngpu && acc >= (long long)nnz * d / ngpu) ob[d++] = o + 1;
+        }
+        for (; d < ngpu; ++d) ob[d] = n;
+    }
+    struct Dev {
+        int phys;
+        int *rowptr = nullptr, *col = nullptr;
+        double *val = nullptr, *b = nullptr;
+        unsigned long long *x = nullptr;
+        unsigned long long **xs = nullptr;
+        unsigned *ctl = nullptr;
+    };
+    std::vector<Dev> D(ngpu);
+    std::vector<hipStream_t> streams(count, nullptr);
+    int st = SBLAS_OK;
+    auto cleanup = [&]() {
+        for (auto &q : D) {
+            DeviceGuard g(q.phys);
+            (void)hipFree(q.rowptr);
+            (void)hipFree(q.col);
+            (void)hipFree(q.val);
+            (void)hipFree(q.b);
+            (void)hipFree(q.x);
+            (void)hipFree(q.xs);
+            (void)hipFree(q.ctl);
+        }
+        for (int p = 0; p < count; ++p)
+            if (streams[p]) {
+                DeviceGuard g(p);
+                (void)hipStreamDestroy(streams[p]);
+            }
+    };
+#define MG(expr)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error("trsv_mgpu: %s -> %s", #expr, hipGetErrorString(e_));    \
+            cleanup();                                                         \
+            return SBLAS_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+    for (int d = 0; d < ngpu; ++d) D[d].phys = d % count;
+    for (int p = 0; p < std::min(count, ngpu); ++p) {
+        DeviceGuard g(p);
+        MG(hipStreamCreateWithFlags(&streams[p], hipStreamNonBlocking));
+        for (int q = 0; q < std::min(count, ngpu); ++q) {
+            if (q == p) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, p, q) == hipSuccess && can) {
+                hipError_t e = hipDeviceEnablePeerAccess(q, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) MG(e);
+                (void)hipGetLastError();
+            }
+        }
+    }
+    std::vector<unsigned long long *> xs(ngpu);
+    for (int d = 0; d < ngpu; ++d) {
+        Dev &q = D[d];
+        DeviceGuard g(q.phys);
+        const int nloc = ob[d + 1] - ob[d];
+        std::vector<int> lrp((size_t)nloc + 1, 0), lcol;
+        std::vector<double> lval, lb((size_t)std::max(nloc, 1));
+        for (int t = 0; t < nloc; ++t) {
+            const int i = row_of(ob[d] + t);
+            for (int e = rp[(size_t)i]; e < rp[(size_t)i + 1]; ++e) {
+                lcol.push_back(cl[(size_t)e]);
+                lval.push_back(vl[(size_t)e]);
+            }
+            lrp[(size_t)t + 1] = (int)lcol.size();
+            lb[(size_t)t] = b[i];
+        }
+        MG(hipMalloc(&q.rowptr, sizeof(int) * ((size_t)nloc + 1)));
+        MG(hipMalloc(&q.col, sizeof(int) * std::max<size_t>(lcol.size(), 1)));
+        MG(hipMalloc(&q.val, sizeof(double) * std::max<size_t>(lval.size(), 1)));
+        MG(hipMalloc(&q.b, sizeof(double) * std::max(nloc, 1)));
+        MG(hipMalloc(&q.ctl, kCtlBytes));
+        MG(hipExtMallocWithFlags((void **)&q.x, sizeof(double) * std::max(n, 1), hipDeviceMallocFinegrained));
+        MG(hipMalloc(&q.xs, sizeof(void *) * ngpu));
+        MG(hipMemcpy(q.rowptr, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
+        if (!lcol.empty()) {
+            MG(hipMemcpy(q.col, lcol.data(), sizeof(int) * lcol.size(), hipMemcpyHostToDevice));
+            MG(hipMemcpy(q.val, lval.data(), sizeof(double) * lval.size(), hipMemcpyHostToDevice));
+        }
+        if (nloc) MG(hipMemcpy(q.b, lb.data(), sizeof(double) * nloc, hipMemcpyHostToDevice));
+        xs[d] = q.x;
+    }
+    for (int d = 0; d < ngpu; ++d) {
+        DeviceGuard g(D[d].phys);
+        MG(hipMemcpy(D[d].xs, xs.data(), sizeof(void *) * ngpu, hipMemcpyHostToDevice));
+    }
+    // reset: sentinel x everywhere, zero control words
+    for (int d = 0; d < ngpu; ++d) {
+        DeviceGuard g(D[d].phys);
+        hipStream_t s = streams[D[d].phys];
+        hipLaunchKernelGGL(k_fill_pending, dim3((n + 255) / 256), dim3(256), 0, s, D[d].x, n);
+        MG(hipMemsetAsync(D[d].ctl, 0, kCtlBytes, s));
+    }
+    for (int p = 0; p < std::min(count, ngpu); ++p) {
+        DeviceGuard g(p);
+        MG(hipStreamSynchronize(streams[p]));
+    }
+    const double t0 = sblas_get_time();
+    for (int d = 0; d < ngpu; ++d) {
+        Dev &q = D[d];
+        DeviceGuard g(q.phys);
+        TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], ob[d + 1] - ob[d], n, bwd ? 1 : 0};
+        if (P.nloc > 0)
+            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid_for(q.phys)), dim3(256), 0, streams[q.phys], P,
+                               q.ctl);
+        MG(hipGetLastError());
+    }
+    for (int p = 0; p < std::min(count, ngpu); ++p) {
+        DeviceGuard g(p);
+        MG(hipStreamSynchronize(streams[p]));
+    }
+    if (solve_ms) *solve_ms = (sblas_get_time() - t0) * 1e3;
+    for (int d = 0; d < ngpu && st == SBLAS_OK; ++d) {
+        Dev &q = D[d];
+        DeviceGuard g(q.phys);
+        unsigned h[kCtlBytes / 4] = {0};
+        MG(hipMemcpy(h, q.ctl, kCtlBytes, hipMemcpyDeviceToHost));
+        if (h[kAbort]) {
+            set_error("trsv_mgpu: partition %d exceeded its spin limit", d);
+            st = SBLAS_ERR_HIP;
+            break;
+        }
+        // x rows of this block: contiguous rows in row space
+        const int nloc = ob[d + 1] - ob[d];
+        if (nloc == 0) continue;
+        const int ia = bwd ? n - ob[d + 1] : ob[d];
+        MG(hipMemcpy(x + ia, (double *)q.x + ia, sizeof(double) * nloc, hipMemcpyDeviceToHost));
+    }
+#undef MG
+    cleanup();
+    return st;
+}
 }  // extern "C"

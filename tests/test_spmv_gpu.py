@@ -14,21 +14,19 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = [1, 2, 4]
+# (algorithm, forced panel count).  The panel algorithm (4) picks ~4 MiB of x
+# per panel, i.e. one panel for these small matrices; 3 and 8 panels are
+# forced too so the multi-panel path (interleaved grid + partial reduce) runs.
+ALGOS = [(1, None), (2, None), (4, None), (4, 3), (4, 8)]
+ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8"]
 
 
-@pytest.fixture(autouse=True, params=["auto", "3", "8"])
-def panels(request, monkeypatch):
-    """The panel algorithm (4) picks ~4 MiB of x per panel, i.e. one panel for
-    these small matrices; force 3 and 8 panels too so the multi-panel path
-    (interleaved grid + partial reduce) is exercised.  Other algorithms
-    ignore SBLAS_PANELS, so only algo 4 tests are repeated."""
-    algo = request.node.callspec.params.get("algo") if hasattr(request.node, "callspec") else None
-    if request.param != "auto":
-        if algo != 4:
-            pytest.skip("panel count only affects algo 4")
-        monkeypatch.setenv("SBLAS_PANELS", request.param)
-    yield
+@pytest.fixture(params=ALGOS, ids=ALGO_IDS)
+def algo(request, monkeypatch):
+    a, panels = request.param
+    if panels is not None:
+        monkeypatch.setenv("SBLAS_PANELS", str(panels))
+    return a
 
 
 def random_csr(rng, m, n, density_rows, long_rows=(), empty_frac=0.1):
@@ -65,7 +63,6 @@ def check(orc, rp, col, val, x, alpha, beta, y0, got):
     assert np.all(np.abs(got - want) <= 1e-3 * np.maximum(1.0, np.abs(want)))
 
 
-@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("mode", [0, 1])
 def test_qh768(torch_cuda, sb, orc, algo, mode):
     path = os.path.join(GOLDEN, "qh768.mtx")
@@ -77,7 +74,6 @@ def test_qh768(torch_cuda, sb, orc, algo, mode):
     check(orc, rp, col, val, x, alpha, beta, y0, got)
 
 
-@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("prefix", [False, True])
 def test_synthetic(torch_cuda, sb, orc, algo, prefix):
     n = 20000
@@ -89,7 +85,6 @@ def test_synthetic(torch_cuda, sb, orc, algo, prefix):
     check(orc, rp, col, val, x, alpha, beta, y0, got)
 
 
-@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("beta", [0.0, 0.75])
 def test_ragged_long_empty(torch_cuda, sb, orc, algo, beta):
     rng = np.random.default_rng(7)
@@ -105,7 +100,6 @@ def test_ragged_long_empty(torch_cuda, sb, orc, algo, beta):
     check(orc, rp, col, val, x, 1.25, beta, y0c, got)
 
 
-@pytest.mark.parametrize("algo", ALGOS)
 def test_edge_shapes(torch_cuda, sb, orc, algo):
     rng = np.random.default_rng(3)
     # all rows empty
