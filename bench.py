@@ -9,9 +9,12 @@ distinct uniform-random sorted columns (seed 42), values U[0,1), x U[0,1)
 the whole matrix with every input already resident in HBM; at N > 1 the
 matrix is split by nnz over the ranks (x replicated) and a step also
 includes the RCCL allgather of the y slices plus their device-side merge
-(strong scaling: the same matrix at every N).
+(strong scaling: the same matrix at every N).  Timing is cold-cache by
+default: at N = 8 a rank's slice (~67 MB) would otherwise
+sit in the 256 MB Infinity Cache between back-to-back steps; the warm number
+is reported beside it.
 
-  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5]
+  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5] [--cache cold|warm]
 
 Default kernel: `panel` = the row-split kernel run over XCD-affine column
 panels (x slice ~4 MiB per panel, panel p's row blocks on workgroups with
@@ -111,6 +114,11 @@ def main() -> int:
     ap.add_argument("--check", action="store_true",
                     help="after timing, verify the assembled y of one fresh step against the "
                          "oracle (rank 0; small n only)")
+    ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
+                    help="cold (default, SURVEY M1-cache): a 1 GiB scrub before every timed step "
+                         "evicts the 256 MB Infinity Cache and the L2s, each step is bracketed "
+                         "by its own barrier + synchronize; warm: K back-to-back steps.  The other "
+                         "mode is always measured too and reported under `warm`/`cold`.")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -169,23 +177,48 @@ def main() -> int:
             ev[1].record(stream)
         op.exchange(sp)
 
+    scrub = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
+
+    def sync_barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def run_warm():
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        sync_barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        sync_barrier()
+        return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    def run_cold():
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        el = 0.0
+        for k in range(args.steps):
+            scrub.add_(1)  # 1 GiB read+write: evicts MALL (256 MB) and L2
+            sync_barrier()
+            t0 = time.perf_counter()
+            step(evs[k])
+            sync_barrier()
+            el += time.perf_counter() - t0
+        return el, float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(evs[k])
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        if args.cache == "cold":
+            el, kern_ms = run_cold()
+            el_o, kern_o = run_warm()
+        else:
+            el, kern_ms = run_warm()
+            el_o, kern_o = run_cold()
+    del scrub
 
     check = None
     if args.check:
@@ -205,7 +238,7 @@ def main() -> int:
             bound = orc.spmv_bound(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
             check = bool(np.all(np.abs(y_dev - want) <= bound))
     stats_dev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
-    stats = torch.tensor([el, kern_ms, local_bytes, local_flops], dtype=torch.float64,
+    stats = torch.tensor([el, kern_ms, local_bytes, local_flops, el_o, kern_o], dtype=torch.float64,
                          device=stats_dev)
     if dist is not None:
         mx = stats.clone()
@@ -213,9 +246,10 @@ def main() -> int:
         sm = stats.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         el, kern_ms_max = float(mx[0]), float(mx[1])
+        el_o, kern_o_max = float(mx[4]), float(mx[5])
         tot_bytes = float(sm[2])
     else:
-        kern_ms_max, tot_bytes = kern_ms, float(local_bytes)
+        kern_ms_max, tot_bytes, kern_o_max = kern_ms, float(local_bytes), kern_o
     ms_step = el / args.steps * 1e3
     total_flops = 2.0 * nnz
 
@@ -260,6 +294,14 @@ def main() -> int:
             "algorithmic_bytes_per_launch": int(local_bytes),
             "algorithmic_bytes_all_ranks": int(tot_bytes),
             "host_gen_s": round(t_gen, 2),
+            "cache": args.cache,
+            ("warm" if args.cache == "cold" else "cold"): {
+                "value": round(total_flops / (el_o / args.steps) / 1e9, 3),
+                "ms_per_step": round(el_o / args.steps * 1e3, 5),
+                "kernel_ms": round(kern_o, 5),
+                "kernel_ms_max_over_ranks": round(kern_o_max, 5),
+                "roofline_frac": round(local_bytes / (kern_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
         }
         if world > 1 and args.dist_backend != "nccl":
             out["note"] = f"rehearsal: {world} ranks on {ndev} GPU(s) over {args.dist_backend}"

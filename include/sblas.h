@@ -139,13 +139,18 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x,
                      void *stream);
 int sblas_trsv_levels(sblas_trsv T, int *nlevel);
 int sblas_trsv_destroy(sblas_trsv T);
+/* SpTRSM, rhs right-hand sides (sptrsm_syncfree_cuda_executor,
+ * sptrsv_v1/src/sptrsv_syncfree_cuda.h:170-282): d_b, d_x device n x rhs
+ * row-major.  Pull executor; rhs == 1 is sblas_trsv_solve(T, 1, ...). */
+int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream);
 /* Multi-GPU sync-free solve (replaces sptrsv_v3's NVSHMEM):
  * HOST CSC in, x out.  nnz-balanced blocks of the solve order, one per device
  * ordinal (d % count); full-length x per device in fine-grained memory;
  * producers push x_i to every later block over xGMI; consumers poll local
- * memory.  solve_ms (optional) = wall time of the kernels. */
+ * memory.  b, x: n x rhs row-major (x[i*rhs+k], the reference's layout).
+ * solve_ms (optional) = wall time of the kernels. */
 int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val,
-                          int n, int substitution, const double *b, double *x,
+                          int n, int substitution, int rhs, const double *b, double *x,
                           int ngpu, double *solve_ms);
 
 /* Multi-partition y assembly after an allgather of padded slices: partition

@@ -257,7 +257,8 @@ int sblas_csrmm_mgpu(int m, int n, int k, const double *alpha, int nnz_A, int *c
 // Single-device solve for sblas_sptrsv_syncfree: upload, analyse, one warm-up
 // and one timed solve (the reference times exactly one executor run).
 static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int n,
-                             int nnz, int substitution, int opt, double *x, const double *b, double *ms)
+                             int nnz, int substitution, int rhs, int opt, double *x, const double *b,
+                             double *ms)
 {
     DeviceGuard g(0);
     DevBuf dcp, dri, dv, db, dx;
@@ -265,25 +266,32 @@ static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const d
     SBLAS_HIP(hipMalloc(&dcp.p, sizeof(int) * ((size_t)n + 1)));
     SBLAS_HIP(hipMalloc(&dri.p, sizeof(int) * std::max(nnz, 1)));
     SBLAS_HIP(hipMalloc(&dv.p, sizeof(double) * std::max(nnz, 1)));
-    SBLAS_HIP(hipMalloc(&db.p, sizeof(double) * std::max(n, 1)));
-    SBLAS_HIP(hipMalloc(&dx.p, sizeof(double) * std::max(n, 1)));
+    const size_t nr = (size_t)std::max(n, 1) * rhs;
+    SBLAS_HIP(hipMalloc(&db.p, sizeof(double) * nr));
+    SBLAS_HIP(hipMalloc(&dx.p, sizeof(double) * nr));
     SBLAS_HIP(hipMemcpy(dcp.p, cscColPtr, sizeof(int) * ((size_t)n + 1), hipMemcpyHostToDevice));
     if (nnz) {
         SBLAS_HIP(hipMemcpy(dri.p, cscRowIdx, sizeof(int) * nnz, hipMemcpyHostToDevice));
         SBLAS_HIP(hipMemcpy(dv.p, cscVal, sizeof(double) * nnz, hipMemcpyHostToDevice));
     }
-    SBLAS_HIP(hipMemcpy(db.p, b, sizeof(double) * n, hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(db.p, b, sizeof(double) * n * rhs, hipMemcpyHostToDevice));
     sblas_trsv T = nullptr;
     SBLAS_TRY(sblas_trsv_create(&T, 0, n, nnz, (const int *)dcp.p, (const int *)dri.p,
                                 (const double *)dv.p, substitution, nullptr));
+    // rhs == 1: opt 1 (OPT_WARP_NNZ) -> CSC push (reference algorithm), else
+    // CSR pull; rhs > 1: the SpTRSM pull executor
     const int algo = opt == 1 ? 0 : 1;
-    int st = sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr);  // warm-up
+    auto solve = [&]() {
+        return rhs == 1 ? sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr)
+                        : sblas_trsv_solve_rhs(T, rhs, (const double *)db.p, (double *)dx.p, nullptr);
+    };
+    int st = solve();  // warm-up
     const double t0 = sblas_get_time();
-    if (st == SBLAS_OK) st = sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr);
+    if (st == SBLAS_OK) st = solve();
     *ms = (sblas_get_time() - t0) * 1e3;
     sblas_trsv_destroy(T);
     if (st != SBLAS_OK) return st;
-    SBLAS_HIP(hipMemcpy(x, dx.p, sizeof(double) * n, hipMemcpyDeviceToHost));
+    SBLAS_HIP(hipMemcpy(x, dx.p, sizeof(double) * n * rhs, hipMemcpyDeviceToHost));
     return SBLAS_OK;
 }
 
@@ -301,16 +309,16 @@ int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const doub
         printf("This is not a square matrix, return.\n");
         return -1;
     }
-    if (rhs != 1 || n < 0 || nnz < 0 || ngpu <= 0 || !cscColPtr || !x || !b) return SBLAS_ERR_INVALID;
+    if (rhs <= 0 || n < 0 || nnz < 0 || ngpu <= 0 || !cscColPtr || !x || !b) return SBLAS_ERR_INVALID;
     int count;
     if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
     double ms = 0.0;
     if (ngpu > 1) {
         double warm = 0.0;
-        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, b, x, ngpu, &warm));
-        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, b, x, ngpu, &ms));
+        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, rhs, b, x, ngpu, &warm));
+        SBLAS_TRY(sblas_trsv_mgpu_solve(cscColPtr, cscRowIdx, cscVal, n, substitution, rhs, b, x, ngpu, &ms));
     } else {
-        SBLAS_TRY(sptrsv_one_device(cscColPtr, cscRowIdx, cscVal, n, nnz, substitution, opt, x, b, &ms));
+        SBLAS_TRY(sptrsv_one_device(cscColPtr, cscRowIdx, cscVal, n, nnz, substitution, rhs, opt, x, b, &ms));
     }
     const double flop = 2.0 * rhs * (double)nnz;
     printf("cuda syncfree SpTRSV solve used %4.2f ms, throughput is %4.2f gflops\n", ms,

@@ -134,10 +134,18 @@ __global__ __launch_bounds__(256) void k_trsv_push(
 // backward (upper, rows processed from n-1 down) = diagonal FIRST.
 constexpr unsigned long long kXPending = 0x7FF4DEADBEEF5A5AULL;
 
-__global__ void k_fill_pending(unsigned long long *__restrict__ x, int n)
+__global__ void k_fill_pending(unsigned long long *__restrict__ x, long long n)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) x[i] = kXPending;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        x[i] = kXPending;
+}
+
+static void fill_pending(unsigned long long *x, long long n, hipStream_t s)
+{
+    if (n <= 0) return;
+    const long long blocks = std::min<long long>((n + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(k_fill_pending, dim3((unsigned)blocks), dim3(256), 0, s, x, n);
 }
 
 __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long *p)
@@ -348,6 +356,116 @@ __global__ __launch_bounds__(256) void k_trsv_pull_part(const TrsvPart P, unsign
     }
 }
 
+// ---- SpTRSM: rhs > 1 (sptrsm_syncfree_cuda_executor, sptrsv_v1/src/
+// sptrsv_syncfree_cuda.h:170-282; x and b are n x rhs row-major,
+// x[i*rhs + k]).  Pull form: RP lanes per row (power of two <= 64) span the
+// right-hand sides, 64/RP rows per wave from the monotone ticket; every x
+// element is its own ready flag (sentinel), so each lane waits only for the
+// element it reads and no fences are needed.  rhs > 64 runs in chunks of 64.
+// Works single-device (by_row: CSR indexed by row, xs = {x}) and per block of
+// the multi-device split (CSR/b indexed by local solve order, xs = peers).
+struct TrsmArgs {
+    const int *rowptr, *col;
+    const double *val, *b;
+    unsigned long long *xown;             // this block's x (polled)
+    unsigned long long *const *xs;        // [g] peers' x (only q > d used); null if g == 1
+    int g, d, o0, nloc, n, rhs, backward, by_row;
+};
+
+template <int RP>
+__global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *ctl)
+{
+    constexpr int R = 64 / RP;
+    const int lane = threadIdx.x & 63;
+    const int slot = lane / RP, kl = lane % RP;
+    const unsigned long long *xl = P.xown;
+    for (;;) {
+        int t0 = 0;
+        if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? P.nloc : (int)atomicAdd(&ctl[0], (unsigned)R);
+        t0 = __shfl(t0, 0, 64);
+        if (t0 >= P.nloc) return;
+        const int t = t0 + slot;
+        const bool live = t < P.nloc;
+        const int o = P.o0 + (live ? t : 0);
+        const int i = P.backward ? P.n - 1 - o : o;
+        const int ri = P.by_row ? i : (live ? t : 0);
+        int j0 = 0, jend = 0;
+        double diag = 1.0;
+        if (live) {
+            const int a = P.rowptr[ri], e = P.rowptr[ri + 1];
+            if (P.backward) {
+                diag = P.val[a];
+                j0 = a + 1;
+                jend = e;
+            } else {
+                diag = P.val[e - 1];
+                j0 = a;
+                jend = e - 1;
+            }
+        }
+        for (int kc = 0; kc < P.rhs; kc += RP) {
+            const int k = kc + kl;
+            bool pending = live && k < P.rhs;
+            int j = j0;
+            double sum = 0.0;
+            unsigned spins = 0;
+            int cj = (pending && j < jend) ? P.col[j] : 0;
+            double vj = (pending && j < jend) ? P.val[j] : 0.0;
+            while (__any(pending)) {
+                if (pending && j < jend) {
+                    const unsigned long long xv = ld_sys_u64(xl + (size_t)cj * P.rhs + k);
+                    if (xv != kXPending) {
+                        sum += vj * __longlong_as_double((long long)xv);
+                        if (++j < jend) {
+                            cj = P.col[j];
+                            vj = P.val[j];
+                        }
+                    }
+                }
+                if (pending && j == jend) {
+                    const double xi = (P.b[(size_t)ri * P.rhs + k] - sum) / diag;
+                    const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
+                    const size_t at = (size_t)i * P.rhs + k;
+                    __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    for (int q = P.d + 1; q < P.g; ++q)
+                        __hip_atomic_store(P.xs[q] + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    pending = false;
+                }
+                if (__any(pending)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((++spins & 1023u) == 0) {
+                        if (spins > kSpinLimit) {
+                            if (lane == 0) atomicOr(&ctl[kAbort], 1u);
+                            return;
+                        }
+                        if (ld_sc1_i32((const int *)&ctl[kAbort])) return;
+                    }
+                }
+            }
+        }
+    }
+}
+
+static int trsm_lanes(int rhs)
+{
+    int rp = 1;
+    while (rp < rhs && rp < 64) rp *= 2;
+    return rp;
+}
+
+static void launch_trsm(const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t s)
+{
+    switch (trsm_lanes(P.rhs)) {
+    case 1: hipLaunchKernelGGL(k_trsm_pull<1>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 2: hipLaunchKernelGGL(k_trsm_pull<2>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 4: hipLaunchKernelGGL(k_trsm_pull<4>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 8: hipLaunchKernelGGL(k_trsm_pull<8>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 16: hipLaunchKernelGGL(k_trsm_pull<16>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 32: hipLaunchKernelGGL(k_trsm_pull<32>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    default: hipLaunchKernelGGL(k_trsm_pull<64>, dim3(grid), dim3(256), 0, s, P, ctl); break;
+    }
+}
+
 static int grid_for(int dev)
 {
     hipDeviceProp_t p;
@@ -439,8 +557,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
         hipLaunchKernelGGL(k_trsv_push, dim3(grid), dim3(256), 0, s, T->colptr, T->rowidx, T->val,
                            T->in_degree, T->n, T->substitution, d_b, d_x, T->done, T->left, T->ctl);
     } else {
-        hipLaunchKernelGGL(k_fill_pending, dim3((T->n + 255) / 256), dim3(256), 0, s,
-                           (unsigned long long *)d_x, T->n);
+        fill_pending((unsigned long long *)d_x, T->n, s);
         hipLaunchKernelGGL(k_trsv_pull, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
                            T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl);
     }
@@ -450,6 +567,29 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     SBLAS_HIP(hipStreamSynchronize(s));
     if (h[kAbort]) {
         set_error("sptrsv: spin limit exceeded (matrix not triangular or missing diagonal?)");
+        return SBLAS_ERR_HIP;
+    }
+    return SBLAS_OK;
+}
+
+int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream)
+{
+    if (!T || !d_b || !d_x || rhs <= 0) return SBLAS_ERR_INVALID;
+    if (rhs == 1) return sblas_trsv_solve(T, 1, d_b, d_x, stream);
+    if (T->n == 0) return SBLAS_OK;
+    DeviceGuard g(T->device);
+    hipStream_t s = (hipStream_t)stream;
+    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
+    fill_pending((unsigned long long *)d_x, (long long)T->n * rhs, s);
+    TrsmArgs P{T->rrowptr, T->rcol, T->rval, d_b, (unsigned long long *)d_x, nullptr,
+               1, 0, 0, T->n, T->n, rhs, T->substitution, 1};
+    launch_trsm(P, T->ctl, grid_for(T->device), s);
+    SBLAS_HIP(hipGetLastError());
+    unsigned h[kCtlBytes / 4] = {0};
+    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, kCtlBytes, hipMemcpyDeviceToHost, s));
+    SBLAS_HIP(hipStreamSynchronize(s));
+    if (h[kAbort]) {
+        set_error("sptrsm: spin limit exceeded (matrix not triangular or missing diagonal?)");
         return SBLAS_ERR_HIP;
     }
     return SBLAS_OK;
@@ -504,9 +644,10 @@ int sblas_trsv_destroy(sblas_trsv T)
 // d % count; partitions sharing a GPU run in order on that GPU's stream,
 // different GPUs run concurrently (peer access + fine-grained x).
 int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val, int n,
-                          int substitution, const double *b, double *x, int ngpu, double *solve_ms)
+                          int substitution, int rhs, const double *b, double *x, int ngpu,
+                          double *solve_ms)
 {
-    if (n < 0 || ngpu <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
+    if (n < 0 || ngpu <= 0 || rhs <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
     const int nnz = colptr[n];
@@ -597,7 +738,7 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
         DeviceGuard g(q.phys);
         const int nloc = ob[d + 1] - ob[d];
         std::vector<int> lrp((size_t)nloc + 1, 0), lcol;
-        std::vector<double> lval, lb((size_t)std::max(nloc, 1));
+        std::vector<double> lval, lb((size_t)std::max(nloc, 1) * rhs);
         for (int t = 0; t < nloc; ++t) {
             const int i = row_of(ob[d] + t);
             for (int e = rp[(size_t)i]; e < rp[(size_t)i + 1]; ++e) {
@@ -605,21 +746,22 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
                 lval.push_back(vl[(size_t)e]);
             }
             lrp[(size_t)t + 1] = (int)lcol.size();
-            lb[(size_t)t] = b[i];
+            for (int k = 0; k < rhs; ++k) lb[(size_t)t * rhs + k] = b[(size_t)i * rhs + k];
         }
         MG(hipMalloc(&q.rowptr, sizeof(int) * ((size_t)nloc + 1)));
         MG(hipMalloc(&q.col, sizeof(int) * std::max<size_t>(lcol.size(), 1)));
         MG(hipMalloc(&q.val, sizeof(double) * std::max<size_t>(lval.size(), 1)));
-        MG(hipMalloc(&q.b, sizeof(double) * std::max(nloc, 1)));
+        MG(hipMalloc(&q.b, sizeof(double) * std::max(nloc, 1) * rhs));
         MG(hipMalloc(&q.ctl, kCtlBytes));
-        MG(hipExtMallocWithFlags((void **)&q.x, sizeof(double) * std::max(n, 1), hipDeviceMallocFinegrained));
+        MG(hipExtMallocWithFlags((void **)&q.x, sizeof(double) * std::max(n, 1) * rhs,
+                                 hipDeviceMallocFinegrained));
         MG(hipMalloc(&q.xs, sizeof(void *) * ngpu));
         MG(hipMemcpy(q.rowptr, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
         if (!lcol.empty()) {
             MG(hipMemcpy(q.col, lcol.data(), sizeof(int) * lcol.size(), hipMemcpyHostToDevice));
             MG(hipMemcpy(q.val, lval.data(), sizeof(double) * lval.size(), hipMemcpyHostToDevice));
         }
-        if (nloc) MG(hipMemcpy(q.b, lb.data(), sizeof(double) * nloc, hipMemcpyHostToDevice));
+        if (nloc) MG(hipMemcpy(q.b, lb.data(), sizeof(double) * nloc * rhs, hipMemcpyHostToDevice));
         xs[d] = q.x;
     }
     for (int d = 0; d < ngpu; ++d) {
@@ -630,7 +772,7 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
     for (int d = 0; d < ngpu; ++d) {
         DeviceGuard g(D[d].phys);
         hipStream_t s = streams[D[d].phys];
-        hipLaunchKernelGGL(k_fill_pending, dim3((n + 255) / 256), dim3(256), 0, s, D[d].x, n);
+        fill_pending(D[d].x, (long long)n * rhs, s);
         MG(hipMemsetAsync(D[d].ctl, 0, kCtlBytes, s));
     }
     for (int p = 0; p < std::min(count, ngpu); ++p) {
@@ -641,10 +783,15 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
     for (int d = 0; d < ngpu; ++d) {
         Dev &q = D[d];
         DeviceGuard g(q.phys);
-        TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], ob[d + 1] - ob[d], n, bwd ? 1 : 0};
-        if (P.nloc > 0)
+        const int nloc = ob[d + 1] - ob[d];
+        if (nloc > 0 && rhs == 1) {
+            TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
             hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid_for(q.phys)), dim3(256), 0, streams[q.phys], P,
                                q.ctl);
+        } else if (nloc > 0) {
+            TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0};
+            launch_trsm(P, q.ctl, grid_for(q.phys), streams[q.phys]);
+        }
         MG(hipGetLastError());
     }
     for (int p = 0; p < std::min(count, ngpu); ++p) {
@@ -665,8 +812,8 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
         // x rows of this block: contiguous rows in row space
         const int nloc = ob[d + 1] - ob[d];
         if (nloc == 0) continue;
-        const int ia = bwd ? n - ob[d + 1] : ob[d];
-        MG(hipMemcpy(x + ia, (double *)q.x + ia, sizeof(double) * nloc, hipMemcpyDeviceToHost));
+        const size_t ia = (size_t)(bwd ? n - ob[d + 1] : ob[d]) * rhs;
+        MG(hipMemcpy(x + ia, (double *)q.x + ia, sizeof(double) * nloc * rhs, hipMemcpyDeviceToHost));
     }
 #undef MG
     cleanup();

@@ -81,7 +81,8 @@ _sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
 _sig("sblas_trsv_solve", _i, _p, _i, _p, _p, _p)
 _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
-_sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _p, _p, _i, _p)
+_sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
+_sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
 _sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
 _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
@@ -176,18 +177,20 @@ def gen_lower_banded(n: int, offd: int, band: int, seed: int = 47):
     return cp, ri[:nnz], v[:nnz]
 
 
-def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int = 0):
-    """Multi-device sync-free solve from host CSC (sblas_trsv_mgpu_solve).
-    Returns (x, kernel wall ms)."""
+def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int = 0,
+                    rhs: int = 1):
+    """Multi-device sync-free solve from host CSC (sblas_trsv_mgpu_solve);
+    b is n x rhs row-major (or length n for rhs 1).  Returns (x, kernel ms)."""
     cp = np.ascontiguousarray(colptr, np.int32)
     ri = np.ascontiguousarray(rowidx, np.int32)
     v = np.ascontiguousarray(val, np.float64)
     bb = np.ascontiguousarray(b, np.float64)
-    x = np.zeros(max(n, 1), np.float64)
+    x = np.zeros(max(n, 1) * rhs, np.float64)
     ms = C.c_double(0.0)
-    check(lib.sblas_trsv_mgpu_solve(ptr(cp), ptr(ri), ptr(v), n, substitution, ptr(bb), ptr(x),
-                                    ngpu, C.byref(ms)), "trsv_mgpu_solve")
-    return x[:n], ms.value
+    check(lib.sblas_trsv_mgpu_solve(ptr(cp), ptr(ri), ptr(v), n, substitution, rhs, ptr(bb),
+                                    ptr(x), ngpu, C.byref(ms)), "trsv_mgpu_solve")
+    x = x[:n * rhs]
+    return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
 
 
 def gen_vector(n: int, seed: int) -> np.ndarray:
@@ -284,6 +287,10 @@ class DeviceTRSV:
 
     def solve(self, algo: int, b_ptr: int, x_ptr: int, stream=None) -> None:
         check(lib.sblas_trsv_solve(self.h, algo, b_ptr, x_ptr, stream), "trsv_solve")
+
+    def solve_rhs(self, rhs: int, b_ptr: int, x_ptr: int, stream=None) -> None:
+        """SpTRSM: b, x device n x rhs row-major."""
+        check(lib.sblas_trsv_solve_rhs(self.h, rhs, b_ptr, x_ptr, stream), "trsv_solve_rhs")
 
     def levels(self) -> int:
         n = C.c_int()

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--band", type=int, default=80_000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rhs", default="",
+                    help="comma list of rhs counts for the SpTRSM executor (x, b n x rhs)")
     ap.add_argument("--mgpu", default="",
                     help="comma list of block counts for the multi-device executor "
                          "(blocks wrap onto the visible GPUs; kernel wall time reported)")
@@ -74,6 +76,31 @@ def main():
         res[name] = {"ms": round(t, 4), "gflops": round(2.0 * nnz / t / 1e6, 3),
                      "gbps_algorithmic": round(abytes / t / 1e6, 1),
                      "rel_l1_vs_xref": rel}
+    for r in [int(t) for t in args.rhs.split(",") if t]:
+        X = np.floor(np.random.default_rng(r).random((n, r)) * 10.0) + 1.0
+        # B = L X on the host, one column at a time
+        B = np.empty((n, r))
+        for k in range(r):
+            B[:, k] = np.bincount(ri, weights=v * X[cols, k], minlength=n)
+        dX = torch.from_numpy(X).to(dev)
+        dB = torch.from_numpy(B).to(dev)
+        dXs = torch.zeros_like(dB)
+        with torch.cuda.stream(s):
+            T.solve_rhs(r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(args.steps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                T.solve_rhs(r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                ms.append(e0.elapsed_time(e1))
+        t = float(np.median(ms))
+        res[f"trsm_pull_rhs{r}"] = {
+            "ms": round(t, 4), "gflops": round(2.0 * nnz * r / t / 1e6, 3),
+            "rel_l1_vs_xref": float((dXs - dX).abs().sum() / dX.abs().sum())}
+        del dX, dB, dXs
     T.close()
     for g in [int(t) for t in args.mgpu.split(",") if t]:
         sblas.trsv_mgpu_solve(cp, ri, v, n, b, g, 0)  # warm-up

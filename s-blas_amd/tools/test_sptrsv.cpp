@@ -1,6 +1,6 @@
 // test_sptrsv -- CLI clone of sptrsv/sptrsv_v1/src/main.cu:
 //
-//   test_sptrsv -n <ngpu> -rhs 1 -forward|-backward -mtx <A.mtx> [-seed s] [-opt 1|3]
+//   test_sptrsv -n <ngpu> -rhs <k> -forward|-backward -mtx <A.mtx> [-seed s] [-opt 1|3]
 //
 // L (U) = strict lower (upper) pattern of A with values rand()%10+1 plus a
 // unit diagonal (main.cu:150-186), CSC by a stable transpose (tranpose.h),
@@ -50,8 +50,8 @@ int main(int argc, char **argv)
     printf("Using %i GPU(s).\n", ngpu);
     printf("rhs = %i\n", rhs);
     printf("substitution = %i\n", substitution);
-    if (!filename || rhs != 1) {
-        printf("only -rhs 1 with -mtx <file> is supported\n");
+    if (!filename || rhs <= 0) {
+        printf("usage: -rhs <k >= 1> with -mtx <file>\n");
         return -1;
     }
     printf("-------------- %s --------------\n", filename);
@@ -118,10 +118,14 @@ int main(int argc, char **argv)
     const int pmax = nlevel ? *max_element(hist.begin(), hist.end()) : 0;
     printf("This matrix/graph has %i levels, its parallelism is %4.2f (min: %i ; avg: %i ; max: %i )\n",
            nlevel, nlevel ? (double)m / nlevel : 0.0, pmin, nlevel ? m / nlevel : 0, pmax);
-    vector<double> x_ref((size_t)n), b((size_t)m, 0.0), x((size_t)n, 0.0);
-    for (int i = 0; i < n; ++i) x_ref[(size_t)i] = (double)(rand() % 10 + 1);
+    // x_ref / b / x are n x rhs row-major (main.cu:330-352)
+    const size_t R = (size_t)rhs;
+    vector<double> x_ref((size_t)n * R), b((size_t)m * R, 0.0), x((size_t)n * R, 0.0);
+    for (size_t i = 0; i < (size_t)n * R; ++i) x_ref[i] = (double)(rand() % 10 + 1);
     for (int c = 0; c < n; ++c)
-        for (int j = cp[(size_t)c]; j < cp[(size_t)c + 1]; ++j) b[(size_t)ri[(size_t)j]] += cv[(size_t)j] * x_ref[(size_t)c];
+        for (int j = cp[(size_t)c]; j < cp[(size_t)c + 1]; ++j)
+            for (size_t k = 0; k < R; ++k)
+                b[(size_t)ri[(size_t)j] * R + k] += cv[(size_t)j] * x_ref[(size_t)c * R + k];
     printf("----------------------------start-----------------------------------------------------\n");
     double gflops = 0;
     const int rc = sptrsv_syncfree_cuda(cp.data(), ri.data(), cv.data(), m, n, nnzTR, substitution,

@@ -225,6 +225,58 @@ def test_sptrsv_reference_api_mgpu(torch_cuda, sb, capfd):
     assert "executor passed!" in capfd.readouterr().out
 
 
+def csc_matmat(cp, ri, cv, X):
+    """B = L X for CSC L (exact for the integer KAT systems)."""
+    B = np.zeros_like(X)
+    for c in range(len(cp) - 1):
+        s, e = cp[c], cp[c + 1]
+        B[ri[s:e]] += cv[s:e, None] * X[c][None, :]
+    return B
+
+
+@pytest.mark.parametrize("name", ["qh768", "ash85"])
+@pytest.mark.parametrize("sub", ["fwd", "bwd"])
+@pytest.mark.parametrize("rhs", [2, 3, 8, 64, 100])
+def test_sptrsm_kat(torch_cuda, sb, name, sub, rhs):
+    """SpTRSM (rhs > 1): integer L (unit diagonal) and integer
+    X, so B = L X and the solve are exact in fp64."""
+    torch = torch_cuda
+    g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
+    cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
+    n = len(cp) - 1
+    X = np.random.default_rng(rhs).integers(1, 11, (n, rhs)).astype(np.float64)
+    B = csc_matmat(cp, ri, cv, X)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, B)]
+    xd = torch.zeros((n, rhs), dtype=torch.float64, device="cuda")
+    T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                      0 if sub == "fwd" else 1)
+    for _ in range(2):
+        xd.zero_()
+        T.solve_rhs(rhs, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xd.cpu().numpy(), X)
+    T.close()
+    for ngpu in (1, 3):
+        x, _ = sb.trsv_mgpu_solve(cp, ri, cv, n, B, ngpu, 0 if sub == "fwd" else 1, rhs)
+        assert np.array_equal(x, X)
+
+
+def test_sptrsm_reference_api(torch_cuda, sb, capfd):
+    g = np.load(os.path.join(GOLDEN, "trsv_qh768_fwd.npz"))
+    cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
+    n, rhs = len(cp) - 1, 5
+    X = np.random.default_rng(1).integers(1, 11, (n, rhs)).astype(np.float64)
+    B = csc_matmat(cp, ri, cv, X)
+    x = np.zeros((n, rhs))
+    gf = np.zeros(1)
+    for ngpu in (1, 2):
+        x[:] = 0
+        rc = sb.lib.sblas_sptrsv_syncfree(sb.ptr(cp), sb.ptr(ri), sb.ptr(cv), n, n, len(ri), 0,
+                                          rhs, 3, sb.ptr(x), sb.ptr(B), sb.ptr(X), sb.ptr(gf), ngpu)
+        assert rc == 0 and np.array_equal(x, X)
+    assert "executor passed!" in capfd.readouterr().out
+
+
 # ------------------------------------------------------------ assembly ----
 def test_assemble_slices(torch_cuda, sb):
     torch = torch_cuda
