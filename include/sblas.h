@@ -171,6 +171,14 @@ int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
  * mode 2 = test_spmv 'b' (values 1e-5).  Call with rowptr==NULL to size. */
 int sblas_mm_read(const char *path, int mode, int *m, int *n, long long *nnz,
                   long long *rowptr, int *col, double *val);
+/* Binary CSR cache.  sblas_mm_read keeps one automatically
+ * when SBLAS_MM_CACHE is set ("1": <file>.m<mode>.csrbin beside the .mtx;
+ * otherwise a directory), keyed by the source's size and mtime.  These two
+ * write/read a standalone .csrbin (two-call protocol as sblas_mm_read). */
+int sblas_csrbin_write(const char *path, int m, int n, long long nnz, const long long *rowptr,
+                       const int *col, const double *val);
+int sblas_csrbin_read(const char *path, int *m, int *n, long long *nnz, long long *rowptr,
+                      int *col, double *val);
 
 /* nnz-balanced partition of spMV_mgpu_v1 (dspmv_mgpu_v1.cu:60-94, Q5 fixed).
  * Arrays of g entries. */

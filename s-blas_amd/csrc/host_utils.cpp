@@ -5,12 +5,18 @@
 // our own: the MM reader slurps the file once and parses in place (the
 // reference fscanf's entry by entry, dspmv_test.cu:122-136), and the
 // generator is row-parallel (one counter-based stream per row).
+#include <sys/stat.h>
 #include <sys/time.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include <algorithm>
 #include <cctype>
 #include <cmath>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -146,6 +152,302 @@ inline const char *parse_dbl(const char *p, double &v)
     return e == p ? nullptr : e;
 }
 
+
+// ---- parsed CSR, memo, parallel parse, .csrbin cache ----------------------
+struct HostCsr {
+    int m = 0, n = 0;
+    long long nnz = 0;
+    std::vector<long long> rowptr;
+    std::vector<int> col;
+    std::vector<double> val;
+};
+
+struct FileId {
+    long long size = -1, mtime = 0;
+};
+
+FileId file_id(const char *path)
+{
+    struct stat st;
+    FileId f;
+    if (::stat(path, &st) == 0) {
+        f.size = (long long)st.st_size;
+        f.mtime = (long long)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec;
+    }
+    return f;
+}
+
+struct Memo {
+    std::string path;
+    int mode = -1;
+    FileId id;
+    HostCsr A;
+};
+thread_local Memo g_memo;
+
+HostCsr *memo_lookup(const char *path, int mode)
+{
+    if (g_memo.mode != mode || g_memo.path != path) return nullptr;
+    const FileId f = file_id(path);
+    if (f.size != g_memo.id.size || f.mtime != g_memo.id.mtime) return nullptr;
+    return &g_memo.A;
+}
+
+HostCsr &memo_slot(const char *path, int mode)
+{
+    g_memo = Memo();
+    g_memo.path = path;
+    g_memo.mode = mode;
+    g_memo.id = file_id(path);
+    return g_memo.A;
+}
+
+void memo_clear() { g_memo = Memo(); }
+
+// .csrbin: "SBLASCSR" | u32 version | i32 mode (-1: written by the user) |
+// i64 source size | i64 source mtime | i32 m | i32 n | i64 nnz |
+// i64 rowptr[m+1] | i32 col[nnz] | f64 val[nnz]
+constexpr char kBinMagic[8] = {'S', 'B', 'L', 'A', 'S', 'C', 'S', 'R'};
+constexpr uint32_t kBinVersion = 1;
+
+int csrbin_store(const char *path, int mode, long long src_size, long long src_mtime, int m, int n,
+                 long long nnz, const long long *rowptr, const int *col, const double *val)
+{
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) {
+        set_error("cannot write %s", tmp.c_str());
+        return SBLAS_ERR_IO;
+    }
+    const int32_t mode32 = mode, m32 = m, n32 = n;
+    const int64_t sz = src_size, mt = src_mtime, nz = nnz;
+    bool ok = std::fwrite(kBinMagic, 1, 8, f) == 8 && std::fwrite(&kBinVersion, 4, 1, f) == 1 &&
+              std::fwrite(&mode32, 4, 1, f) == 1 && std::fwrite(&sz, 8, 1, f) == 1 &&
+              std::fwrite(&mt, 8, 1, f) == 1 && std::fwrite(&m32, 4, 1, f) == 1 &&
+              std::fwrite(&n32, 4, 1, f) == 1 && std::fwrite(&nz, 8, 1, f) == 1 &&
+              std::fwrite(rowptr, 8, (size_t)m + 1, f) == (size_t)m + 1 &&
+              (nnz == 0 || (std::fwrite(col, 4, (size_t)nnz, f) == (size_t)nnz &&
+                            std::fwrite(val, 8, (size_t)nnz, f) == (size_t)nnz));
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path) != 0) {
+        std::remove(tmp.c_str());
+        set_error("cannot write %s", path);
+        return SBLAS_ERR_IO;
+    }
+    return SBLAS_OK;
+}
+
+// mode >= 0: the file must have been made from a source with this size/mtime
+int csrbin_load(const char *path, int mode, long long src_size, long long src_mtime, HostCsr &A)
+{
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        set_error("cannot open %s", path);
+        return SBLAS_ERR_IO;
+    }
+    char magic[8];
+    uint32_t ver = 0;
+    int32_t mode32 = 0, m32 = 0, n32 = 0;
+    int64_t sz = 0, mt = 0, nz = 0;
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kBinMagic, 8) == 0 &&
+              std::fread(&ver, 4, 1, f) == 1 && ver == kBinVersion && std::fread(&mode32, 4, 1, f) == 1 &&
+              std::fread(&sz, 8, 1, f) == 1 && std::fread(&mt, 8, 1, f) == 1 &&
+              std::fread(&m32, 4, 1, f) == 1 && std::fread(&n32, 4, 1, f) == 1 &&
+              std::fread(&nz, 8, 1, f) == 1 && m32 >= 0 && n32 >= 0 && nz >= 0;
+    if (ok && mode >= 0) ok = mode32 == mode && sz == src_size && mt == src_mtime;
+    if (ok) {
+        A.m = m32;
+        A.n = n32;
+        A.nnz = nz;
+        A.rowptr.resize((size_t)m32 + 1);
+        A.col.resize((size_t)nz);
+        A.val.resize((size_t)nz);
+        ok = std::fread(A.rowptr.data(), 8, (size_t)m32 + 1, f) == (size_t)m32 + 1 &&
+             (nz == 0 || (std::fread(A.col.data(), 4, (size_t)nz, f) == (size_t)nz &&
+                          std::fread(A.val.data(), 8, (size_t)nz, f) == (size_t)nz)) &&
+             A.rowptr[0] == 0 && A.rowptr[(size_t)m32] == nz;
+    }
+    std::fclose(f);
+    if (!ok) {
+        set_error("%s: not a valid .csrbin (or stale for this source)", path);
+        return SBLAS_ERR_IO;
+    }
+    return SBLAS_OK;
+}
+
+// Parses the entries of F (from F.pos) in parallel, in file order.
+int parse_entries(const MMFile &F, int mode, const char *path, std::vector<int> &ri,
+                  std::vector<int> &ci, std::vector<double> &vi)
+{
+    const char *base = F.buf.c_str();
+    const size_t b0 = F.pos, b1 = F.buf.size() - 1;  // trailing '\0'
+    const long long nz = F.nz;
+    int T = 1;
+#ifdef _OPENMP
+    T = std::max(1, std::min(omp_get_max_threads(), 64));
+#endif
+    if ((long long)(b1 - b0) < (1LL << 20)) T = 1;
+    std::vector<size_t> cut((size_t)T + 1);
+    cut[0] = b0;
+    cut[(size_t)T] = b1;
+    for (int t = 1; t < T; ++t) {
+        size_t c = b0 + (b1 - b0) * (size_t)t / (size_t)T;
+        while (c < b1 && base[c - 1] != '\n') ++c;  // start of a line
+        cut[(size_t)t] = std::max(c, cut[(size_t)t - 1]);
+    }
+    struct Part {
+        std::vector<int> r, c;
+        std::vector<double> v;
+        long long bad = -1;  // byte offset of the first malformed entry
+    };
+    std::vector<Part> parts((size_t)T);
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+    for (int t = 0; t < T; ++t) {
+        Part &P = parts[(size_t)t];
+        const size_t guess = (size_t)((double)nz * (double)(cut[(size_t)t + 1] - cut[(size_t)t]) /
+                                      (double)std::max<size_t>(b1 - b0, 1)) + 16;
+        P.r.reserve(guess);
+        P.c.reserve(guess);
+        P.v.reserve(guess);
+        const char *p = base + cut[(size_t)t];
+        const char *end = base + cut[(size_t)t + 1];
+        while (true) {
+            p = skip_ws(p);
+            if (p >= end || *p == 0) break;
+            const char *line = p;
+            long long r, c;
+            double v = 0.0;
+            bool ok = (p = parse_int(p, r)) && (p = parse_int(p, c));
+            if (ok) {
+                if (mode == 0) {
+                    if (F.real || F.complex_) {
+                        ok = (p = parse_dbl(p, v)) != nullptr;
+                        double im;
+                        if (ok && F.complex_) ok = (p = parse_dbl(p, im)) != nullptr;
+                    } else if (F.integer) {
+                        long long iv;
+                        ok = (p = parse_int(p, iv)) != nullptr;
+                        v = (double)iv;
+                    } else {
+                        v = 1.0;
+                    }
+                } else if (mode == 1) {
+                    ok = (p = parse_dbl(p, v)) != nullptr;
+                } else {
+                    v = 0.00001;
+                }
+            }
+            if (ok && (r < 1 || c < 1 || r > F.m || c > F.n)) ok = false;
+            if (!ok) {
+                P.bad = (long long)(line - base);
+                break;
+            }
+            P.r.push_back((int)(r - 1));
+            P.c.push_back((int)(c - 1));
+            P.v.push_back(v);
+            while (p < end && *p != '\n') ++p;  // rest of the line
+        }
+    }
+    long long total = 0;
+    for (int t = 0; t < T; ++t) {
+        const Part &P = parts[(size_t)t];
+        if (P.bad >= 0) {
+            set_error("%s: entry %lld malformed or out of range (byte %lld)", path,
+                      total + (long long)P.r.size(), P.bad);
+            return SBLAS_ERR_IO;
+        }
+        total += (long long)P.r.size();
+    }
+    if (total < nz) {
+        set_error("%s: entry %lld malformed (file has %lld of %lld entries)", path, total, total, nz);
+        return SBLAS_ERR_IO;
+    }
+    ri.resize((size_t)nz);
+    ci.resize((size_t)nz);
+    vi.resize((size_t)nz);
+    long long off = 0;
+    for (int t = 0; t < T && off < nz; ++t) {  // entries past nz are ignored, as fscanf does
+        const Part &P = parts[(size_t)t];
+        const size_t k = (size_t)std::min<long long>((long long)P.r.size(), nz - off);
+        std::memcpy(&ri[(size_t)off], P.r.data(), k * sizeof(int));
+        std::memcpy(&ci[(size_t)off], P.c.data(), k * sizeof(int));
+        std::memcpy(&vi[(size_t)off], P.v.data(), k * sizeof(double));
+        off += (long long)k;
+    }
+    return SBLAS_OK;
+}
+
+int mm_to_csr(const MMFile &F, int mode, const char *path, HostCsr &A)
+{
+    std::vector<int> ri, ci;
+    std::vector<double> vi;
+    const int st = parse_entries(F, mode, path, ri, ci, vi);
+    if (st != SBLAS_OK) return st;
+    const long long nz = F.nz;
+    const bool expand = mode == 0 && F.sym;
+    std::vector<long long> cnt((size_t)F.m + 1, 0);
+    for (long long i = 0; i < nz; ++i) {
+        cnt[(size_t)ri[(size_t)i] + 1]++;
+        if (expand && ri[(size_t)i] != ci[(size_t)i]) cnt[(size_t)ci[(size_t)i] + 1]++;
+    }
+    for (int i = 0; i < F.m; ++i) cnt[(size_t)i + 1] += cnt[(size_t)i];
+    A.m = F.m;
+    A.n = F.n;
+    A.nnz = cnt[(size_t)F.m];
+    A.rowptr = cnt;
+    if (mode != 0) {
+        // Q1: col/val keep FILE order; only the row counts build rowptr.
+        A.col = std::move(ci);
+        A.val = std::move(vi);
+        return SBLAS_OK;
+    }
+    A.col.resize((size_t)A.nnz);
+    A.val.resize((size_t)A.nnz);
+    std::vector<long long> next(cnt.begin(), cnt.end() - 1);
+    for (long long i = 0; i < nz; ++i) {  // stable scatter in file order
+        const int r = ri[(size_t)i], c = ci[(size_t)i];
+        long long o = next[(size_t)r]++;
+        A.col[(size_t)o] = c;
+        A.val[(size_t)o] = vi[(size_t)i];
+        if (expand && r != c) {
+            o = next[(size_t)c]++;
+            A.col[(size_t)o] = r;
+            A.val[(size_t)o] = vi[(size_t)i];
+        }
+    }
+    return SBLAS_OK;
+}
+
+// SBLAS_MM_CACHE: "1" -> <file>.m<mode>.csrbin next to the file; any other
+// non-empty value -> that directory.
+std::string cache_path(const char *path, int mode)
+{
+    const char *env = std::getenv("SBLAS_MM_CACHE");
+    if (!env || !*env || !std::strcmp(env, "0")) return std::string();
+    std::string p = path;
+    if (std::strcmp(env, "1") != 0) {
+        const size_t sl = p.find_last_of('/');
+        p = std::string(env) + "/" + (sl == std::string::npos ? p : p.substr(sl + 1));
+    }
+    return p + ".m" + std::to_string(mode) + ".csrbin";
+}
+
+int load_matrix(const char *path, int mode, HostCsr &A)
+{
+    const FileId id = file_id(path);
+    const std::string cp = cache_path(path, mode);
+    if (!cp.empty() && id.size >= 0 && csrbin_load(cp.c_str(), mode, id.size, id.mtime, A) == SBLAS_OK)
+        return SBLAS_OK;
+    MMFile F;
+    if (!mm_open(path, F)) return SBLAS_ERR_IO;
+    const int st = mm_to_csr(F, mode, path, A);
+    if (st != SBLAS_OK) return st;
+    if (!cp.empty())  // best effort: an unwritable cache directory is not an error
+        (void)csrbin_store(cp.c_str(), mode, id.size, id.mtime, A.m, A.n, A.nnz, A.rowptr.data(),
+                           A.col.data(), A.val.data());
+    return SBLAS_OK;
+}
+
 }  // namespace
 }  // namespace sblas
 
@@ -169,82 +471,62 @@ int sblas_get_row_from_index(int n, long long *a, long long idx)
 
 // mode 0: mmio_data (sptrsv_v1/src/mmio_highlevel.h:137-296)
 // mode 1/2: test_spmv 'f'/'b' loader (spmv/test/dspmv_test.cu:101-136,217-251)
+//
+// the entries are parsed in parallel (OpenMP, one chunk of
+// whole lines per thread, concatenated in file order, so the result is
+// identical to a sequential parse), the two-call size/data protocol parses
+// the file once (thread-local memo keyed by path, mode, size and mtime), and
+// with SBLAS_MM_CACHE set the CSR is also kept in a binary .csrbin file that
+// later loads read directly (see sblas_csrbin_write).
 int sblas_mm_read(const char *path, int mode, int *m, int *n, long long *nnz,
                   long long *rowptr, int *col, double *val)
 {
-    MMFile F;
     if (!path || !m || !n || !nnz || mode < 0 || mode > 2) return SBLAS_ERR_INVALID;
-    if (!mm_open(path, F)) return SBLAS_ERR_IO;
-    const long long nz = F.nz;
-    std::vector<int> ri((size_t)nz), ci((size_t)nz);
-    std::vector<double> vi((size_t)nz);
-    const char *p = F.buf.c_str() + F.pos;
-    for (long long i = 0; i < nz; ++i) {
-        long long r, c;
-        double v = 0.0;
-        if (!(p = parse_int(p, r)) || !(p = parse_int(p, c))) {
-            set_error("%s: entry %lld malformed", path, i);
-            return SBLAS_ERR_IO;
+    HostCsr *A = memo_lookup(path, mode);
+    if (!A) {
+        const int st = load_matrix(path, mode, memo_slot(path, mode));
+        if (st != SBLAS_OK) {
+            memo_clear();
+            return st;
         }
-        if (mode == 0) {
-            if (F.real || F.complex_) {
-                if (!(p = parse_dbl(p, v))) return SBLAS_ERR_IO;
-                if (F.complex_) {
-                    double im;
-                    if (!(p = parse_dbl(p, im))) return SBLAS_ERR_IO;
-                }
-            } else if (F.integer) {
-                long long iv;
-                if (!(p = parse_int(p, iv))) return SBLAS_ERR_IO;
-                v = (double)iv;
-            } else {
-                v = 1.0;
-            }
-        } else if (mode == 1) {
-            if (!(p = parse_dbl(p, v))) return SBLAS_ERR_IO;
-        } else {
-            v = 0.00001;
-        }
-        if (r < 1 || c < 1 || r > F.m || c > F.n) {
-            set_error("%s: entry %lld (%lld,%lld) out of range", path, i, r, c);
-            return SBLAS_ERR_IO;
-        }
-        ri[(size_t)i] = (int)(r - 1);
-        ci[(size_t)i] = (int)(c - 1);
-        vi[(size_t)i] = v;
-        if (mode == 0) {
-            // skip the rest of the line (mmio_data reads exactly its fields)
-        }
+        A = memo_lookup(path, mode);
     }
-    const bool expand = mode == 0 && F.sym;
-    std::vector<long long> cnt((size_t)F.m + 1, 0);
-    for (long long i = 0; i < nz; ++i) {
-        cnt[(size_t)ri[(size_t)i] + 1]++;
-        if (expand && ri[(size_t)i] != ci[(size_t)i]) cnt[(size_t)ci[(size_t)i] + 1]++;
-    }
-    for (int i = 0; i < F.m; ++i) cnt[(size_t)i + 1] += cnt[(size_t)i];
-    *m = F.m;
-    *n = F.n;
-    *nnz = cnt[(size_t)F.m];
+    *m = A->m;
+    *n = A->n;
+    *nnz = A->nnz;
     if (!rowptr) return SBLAS_OK;
-    std::memcpy(rowptr, cnt.data(), sizeof(long long) * ((size_t)F.m + 1));
-    if (mode != 0) {
-        // Q1: col/val keep FILE order; only the row counts build rowptr.
-        std::memcpy(col, ci.data(), sizeof(int) * (size_t)nz);
-        std::memcpy(val, vi.data(), sizeof(double) * (size_t)nz);
-        return SBLAS_OK;
+    std::memcpy(rowptr, A->rowptr.data(), sizeof(long long) * ((size_t)A->m + 1));
+    if (A->nnz) {
+        std::memcpy(col, A->col.data(), sizeof(int) * (size_t)A->nnz);
+        std::memcpy(val, A->val.data(), sizeof(double) * (size_t)A->nnz);
     }
-    std::vector<long long> next(cnt.begin(), cnt.end() - 1);
-    for (long long i = 0; i < nz; ++i) {
-        const int r = ri[(size_t)i], c = ci[(size_t)i];
-        long long o = next[(size_t)r]++;
-        col[o] = c;
-        val[o] = vi[(size_t)i];
-        if (expand && r != c) {
-            o = next[(size_t)c]++;
-            col[o] = r;
-            val[o] = vi[(size_t)i];
-        }
+    memo_clear();  // the data call ends the protocol
+    return SBLAS_OK;
+}
+
+int sblas_csrbin_write(const char *path, int m, int n, long long nnz, const long long *rowptr,
+                       const int *col, const double *val)
+{
+    if (!path || m < 0 || n < 0 || nnz < 0 || !rowptr || (nnz && (!col || !val)))
+        return SBLAS_ERR_INVALID;
+    return csrbin_store(path, -1, 0, 0, m, n, nnz, rowptr, col, val);
+}
+
+int sblas_csrbin_read(const char *path, int *m, int *n, long long *nnz, long long *rowptr,
+                      int *col, double *val)
+{
+    if (!path || !m || !n || !nnz) return SBLAS_ERR_INVALID;
+    HostCsr A;
+    const int st = csrbin_load(path, -1, 0, 0, A);
+    if (st != SBLAS_OK) return st;
+    *m = A.m;
+    *n = A.n;
+    *nnz = A.nnz;
+    if (!rowptr) return SBLAS_OK;
+    std::memcpy(rowptr, A.rowptr.data(), sizeof(long long) * ((size_t)A.m + 1));
+    if (A.nnz) {
+        std::memcpy(col, A.col.data(), sizeof(int) * (size_t)A.nnz);
+        std::memcpy(val, A.val.data(), sizeof(double) * (size_t)A.nnz);
     }
     return SBLAS_OK;
 }

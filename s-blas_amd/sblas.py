@@ -85,6 +85,8 @@ _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
 _sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
 _sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
 _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
+_sig("sblas_csrbin_write", _i, C.c_char_p, _i, _i, _ll, _p, _p, _p)
+_sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)
 _sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
@@ -129,6 +131,26 @@ def mm_read(path: str, mode: int = 0):
     v = np.zeros(max(nnz.value, 1), np.float64)
     check(lib.sblas_mm_read(path.encode(), mode, C.byref(m), C.byref(n), C.byref(nnz),
                             ptr(rp), ptr(ci), ptr(v)), f"mm_read {path}")
+    return m.value, n.value, rp, ci[:nnz.value], v[:nnz.value]
+
+
+def csrbin_write(path: str, m: int, n: int, rowptr, col, val) -> None:
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    ci = np.ascontiguousarray(col, np.int32)
+    v = np.ascontiguousarray(val, np.float64)
+    check(lib.sblas_csrbin_write(path.encode(), m, n, int(rp[-1]), ptr(rp), ptr(ci), ptr(v)),
+          f"csrbin_write {path}")
+
+
+def csrbin_read(path: str):
+    m, n, nnz = C.c_int(), C.c_int(), C.c_longlong()
+    check(lib.sblas_csrbin_read(path.encode(), C.byref(m), C.byref(n), C.byref(nnz), None, None,
+                                None), f"csrbin_read {path}")
+    rp = np.zeros(m.value + 1, np.int64)
+    ci = np.zeros(max(nnz.value, 1), np.int32)
+    v = np.zeros(max(nnz.value, 1), np.float64)
+    check(lib.sblas_csrbin_read(path.encode(), C.byref(m), C.byref(n), C.byref(nnz), ptr(rp),
+                                ptr(ci), ptr(v)), f"csrbin_read {path}")
     return m.value, n.value, rp, ci[:nnz.value], v[:nnz.value]
 
 

@@ -113,3 +113,87 @@ def test_get_row_from_index_fixed(sb):
     rp = np.array([0, 2, 2, 2, 5, 7], np.int64)
     assert sb.lib.sblas_get_row_from_index(5, sb.ptr(rp), 2) == 3
     assert sb.lib.sblas_get_row_from_index(5, sb.ptr(rp), 6) == 4
+
+
+def write_mtx(path, m, n, r, c, v, field="real", symm="general"):
+    with open(path, "w") as fh:
+        fh.write(f"%%MatrixMarket matrix coordinate {field} {symm}\n% generated\n")
+        fh.write(f"{m} {n} {len(r)}\n")
+        if field == "pattern":
+            fh.writelines(f"{a + 1} {b + 1}\n" for a, b in zip(r, c))
+        elif field == "integer":
+            fh.writelines(f"{a + 1} {b + 1} {int(x)}\n" for a, b, x in zip(r, c, v))
+        else:
+            fh.writelines(f"{a + 1} {b + 1} {float(x)!r}\n" for a, b, x in zip(r, c, v))
+
+
+@pytest.mark.parametrize("field,symm", [("real", "general"), ("real", "symmetric"),
+                                        ("integer", "general"), ("pattern", "symmetric")])
+def test_mm_read_parallel_matches_oracle(sb, orc, tmp_path, field, symm):
+    """> 1 MB of entries, so the parser splits the file across
+    threads; the CSR must equal the sequential oracle loader exactly."""
+    rng = np.random.default_rng(5)
+    m = n = 30000
+    k = 120000
+    r = rng.integers(0, m, k)
+    c = rng.integers(0, n, k)
+    if symm == "symmetric":
+        r, c = np.maximum(r, c), np.minimum(r, c)
+    v = rng.integers(-50, 50, k) if field == "integer" else rng.standard_normal(k)
+    path = str(tmp_path / "big.mtx")
+    write_mtx(path, m, n, r, c, v, field, symm)
+    assert os.path.getsize(path) > (1 << 20)
+    got = sb.mm_read(path, 0)
+    want = orc.load_mmio(path)
+    assert got[:2] == want[:2]
+    assert np.array_equal(got[2], want[2].astype(np.int64))
+    assert np.array_equal(got[3], want[3]) and np.array_equal(got[4], want[4])
+    if field == "real":
+        got1 = sb.mm_read(path, 1)
+        want1 = orc.load_testspmv(path, "f")
+        assert all(np.array_equal(a, b) for a, b in zip(got1[2:], want1[2:]))
+
+
+def test_mm_cache_roundtrip_and_staleness(sb, orc, tmp_path, monkeypatch):
+    rng = np.random.default_rng(6)
+    m, n, k = 500, 400, 3000
+    r, c, v = rng.integers(0, m, k), rng.integers(0, n, k), rng.standard_normal(k)
+    path = str(tmp_path / "a.mtx")
+    write_mtx(path, m, n, r, c, v)
+    cache = tmp_path / "cache"
+    cache.mkdir()
+    monkeypatch.setenv("SBLAS_MM_CACHE", str(cache))
+    first = sb.mm_read(path, 0)
+    assert (cache / "a.mtx.m0.csrbin").exists()
+    second = sb.mm_read(path, 0)  # served from the cache
+    for a, b in zip(first[2:], second[2:]):
+        assert np.array_equal(a, b)
+    # a changed source invalidates the cache entry
+    write_mtx(path, m, n, r[:-10], c[:-10], v[:-10])
+    os.utime(path, ns=(1, 1))
+    third = sb.mm_read(path, 0)
+    assert third[2][-1] == k - 10
+    want = orc.load_mmio(path)
+    assert np.array_equal(third[3], want[3]) and np.array_equal(third[4], want[4])
+
+
+def test_csrbin_write_read(sb, tmp_path):
+    rp = np.array([0, 2, 2, 5], np.int64)
+    col = np.array([0, 3, 1, 2, 3], np.int32)
+    val = np.arange(5, dtype=np.float64) / 3
+    p = str(tmp_path / "x.csrbin")
+    sb.csrbin_write(p, 3, 4, rp, col, val)
+    m, n, rp2, col2, val2 = sb.csrbin_read(p)
+    assert (m, n) == (3, 4)
+    assert np.array_equal(rp, rp2) and np.array_equal(col, col2) and np.array_equal(val, val2)
+    with open(p, "r+b") as fh:
+        fh.write(b"X")
+    with pytest.raises(sb.SblasError):
+        sb.csrbin_read(p)
+
+
+def test_mm_read_truncated(sb, tmp_path):
+    p = tmp_path / "t.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate real general\n3 3 4\n1 1 1.0\n2 2 2.0\n")
+    with pytest.raises(sb.SblasError, match="entries"):
+        sb.mm_read(str(p))
