@@ -143,6 +143,21 @@ int sblas_trsv_destroy(sblas_trsv T);
  * sptrsv_v1/src/sptrsv_syncfree_cuda.h:170-282): d_b, d_x device n x rhs
  * row-major.  Pull executor; rhs == 1 is sblas_trsv_solve(T, 1, ...). */
 int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream);
+/* Multi-GPU CSR -> CSC transpose (replaces kernal_sptrans,
+ * sptrans/sptrans_v1/src/sptrans_kernal.h:80-555).  HOST arrays in and out
+ * (int32 rowptr as the reference).  nnz-balanced whole-row blocks, block d
+ * transposed on device d % count, pieces composed on device 0; the result is
+ * the stable global transpose (rows ascending within a column), bit-exact.
+ * ms_transpose / ms_compose (optional): wall times of the two phases. */
+int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *rowptr, const int *col,
+                       const double *val, int *colptr, int *rowidx, double *cval,
+                       double *ms_transpose, double *ms_compose);
+/* sptrans driver (cuda_sptrans / kernal_sptrans): transposes on ngpu devices,
+ * prints the reference's timing lines and its value/pointer checks against
+ * the *_ref arrays (when given), plus a row-index check. */
+int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const int *csrColIdx,
+                  const double *csrVal, int *cscRowIdx, int *cscColPtr, double *cscVal,
+                  const int *cscRowIdx_ref, const int *cscColPtr_ref, const double *cscVal_ref);
 /* Multi-GPU sync-free solve (replaces sptrsv_v3's NVSHMEM):
  * HOST CSC in, x out.  nnz-balanced blocks of the solve order, one per device
  * ordinal (d % count); full-length x per device in fine-grained memory;

@@ -339,6 +339,59 @@ int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const doub
     return SBLAS_OK;
 }
 
+
+// cuda_sptrans / kernal_sptrans (sptrans/sptrans_v1/src/sptrans_cuda.h:11-220,
+// sptrans_kernal.h:80-555): transpose, print the timing lines, compare with
+// the reference CSC the driver computed on the CPU (main.cu:150-200).
+int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const int *csrColIdx,
+                  const double *csrVal, int *cscRowIdx, int *cscColPtr, double *cscVal,
+                  const int *cscRowIdx_ref, const int *cscColPtr_ref, const double *cscVal_ref)
+{
+    double t_tr = 0.0, t_co = 0.0;
+    const int st = sblas_csr2csc_mgpu(m, n, nnz, ngpu, csrRowPtr, csrColIdx, csrVal, cscColPtr,
+                                      cscRowIdx, cscVal, &t_tr, &t_co);
+    if (st != SBLAS_OK) {
+        printf("sptrans failed: %s\n", sblas_last_error());
+        return st;
+    }
+    const char *where = ngpu == 1 ? "single GPU" : "multiple GPU";
+    if (ngpu == 1) {
+        printf("HIP trans used %4.2f ms,\n", t_tr + t_co);
+    } else {
+        printf("HIP transposition on multiple gpu used %4.8f ms,\n", t_tr);
+        printf("HIP composition used %4.8f ms,\n", t_co);
+        printf("SpTrans computation time: %.3f ms \n", t_tr + t_co);
+    }
+    auto report = [&](const char *what, double ref, double res) {
+        res = ref == 0 ? res : res / ref;
+        printf("sptrans %s test on %s: %s |x-xref|/|xref| = %8.2e\n", what, where,
+               res < 1e-4 ? "passed!" : "_NOT_ passed!", res);
+    };
+    if (cscVal_ref) {
+        double ref = 0.0, res = 0.0;
+        for (int i = 0; i < nnz; ++i) {
+            ref += std::fabs(cscVal_ref[i]);
+            res += std::fabs(cscVal_ref[i] - cscVal[i]);
+        }
+        report("value", ref, res);
+    }
+    if (cscColPtr_ref) {
+        double ref = 0.0, res = 0.0;
+        for (int i = 0; i <= n; ++i) {
+            ref += std::fabs((double)cscColPtr_ref[i]);
+            res += std::fabs((double)cscColPtr_ref[i] - cscColPtr[i]);
+        }
+        report("pointer", ref, res);
+    }
+    if (cscRowIdx_ref) {
+        long long bad = 0;
+        for (int i = 0; i < nnz; ++i) bad += cscRowIdx_ref[i] != cscRowIdx[i];
+        printf("sptrans row index test on %s: %s (%lld mismatches)\n", where,
+               bad == 0 ? "passed!" : "_NOT_ passed!", bad);
+    }
+    return SBLAS_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
@@ -388,4 +441,22 @@ int sptrsv_syncfree_cuda(const int *cscColPtrTR, const int *cscRowIdxTR, const d
 {
     return sblas_sptrsv_syncfree(cscColPtrTR, cscRowIdxTR, cscValTR, m, n, nnzTR, substitution, rhs,
                                  opt, x, b, x_ref, gflops, ngpu);
+}
+
+int cuda_sptrans(const int m, const int n, const int nnz, const int *csrRowPtr,
+                 const int *csrColIdx, const double *csrVal, int *cscRowIdx, int *cscColPtr,
+                 double *cscVal, const int *cscRowIdx_ref, const int *cscColPtr_ref,
+                 const double *cscVal_ref)
+{
+    return sblas_sptrans(m, n, nnz, 1, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr, cscVal,
+                         cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
+}
+
+int kernal_sptrans(const int m, const int n, const int nnz, int ngpu, const int *csrRowPtr,
+                   const int *csrColIdx, const double *csrVal, int *cscRowIdx, int *cscColPtr,
+                   double *cscVal, const int *cscRowIdx_ref, const int *cscColPtr_ref,
+                   const double *cscVal_ref)
+{
+    return sblas_sptrans(m, n, nnz, ngpu, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr,
+                         cscVal, cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
 }

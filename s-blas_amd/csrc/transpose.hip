@@ -15,6 +15,7 @@
 //   5. gather: rowidx = row of e (binary search of rowptr), cval = val[e].
 #include <algorithm>
 #include <climits>
+#include <vector>
 
 #include "sblas_internal.hpp"
 
@@ -272,4 +273,218 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     return SBLAS_OK;
 }
 
+
+// ---- multi-device CSR -> CSC (sptrans_v1 kernal_sptrans,
+// sptrans/sptrans_v1/src/sptrans_kernal.h:80-555) -------------------------
+// Rows are split into g nnz-balanced blocks of whole rows; block d is
+// transposed on device d % count by the single-device path above (stable:
+// rows ascend within a column).  The pieces then travel to device 0 (peer DMA
+// over xGMI) and one element-parallel kernel composes them: block d's column
+// c lands after blocks 0..d-1's entries of c, so the result is the global
+// stable transpose, bit for bit.  (The reference's compose leaves row indices
+// block-local, a quirk not inherited.)
+__global__ void k_compose_ptr(const int *__restrict__ ptrs, int g, int n, int *__restrict__ colptr,
+                              int *__restrict__ base)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > n) return;
+    int tot = 0;
+    for (int d = 0; d < g; ++d) tot += ptrs[(size_t)d * (n + 1) + c];
+    colptr[c] = tot;
+    if (c == n) return;
+    int acc = tot;
+    for (int d = 0; d < g; ++d) {
+        base[(size_t)d * n + c] = acc;
+        acc += ptrs[(size_t)d * (n + 1) + c + 1] - ptrs[(size_t)d * (n + 1) + c];
+    }
+}
+
+__global__ void k_compose_val(const int *__restrict__ ptrs, const int *__restrict__ base,
+                              const long long *__restrict__ start, const int *__restrict__ row0,
+                              int g, int n, long long nnz, const int *__restrict__ rid_cat,
+                              const double *__restrict__ val_cat, int *__restrict__ rowidx,
+                              double *__restrict__ cval)
+{
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nnz) return;
+    int d = 0;
+    while (d + 1 < g && start[d + 1] <= p) ++d;
+    const int e = (int)(p - start[d]);
+    const int *cp = ptrs + (size_t)d * (n + 1);
+    int lo = 0, hi = n - 1;  // column c: cp[c] <= e < cp[c+1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (cp[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    const int dst = base[(size_t)d * n + lo] + (e - cp[lo]);
+    rowidx[dst] = rid_cat[p] + row0[d];
+    cval[dst] = val_cat[p];
+}
+
+}  // namespace sblas
+
+extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *rowptr, const int *col,
+                                  const double *val, int *colptr_out, int *rowidx_out,
+                                  double *cval_out, double *ms_transpose, double *ms_compose)
+{
+    using namespace sblas;
+    if (m < 0 || n < 0 || nnz < 0 || ngpu <= 0 || !rowptr || !colptr_out ||
+        (nnz && (!col || !val || !rowidx_out || !cval_out)) || rowptr[m] != nnz)
+        return SBLAS_ERR_INVALID;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
+    const int g = ngpu;
+    // nnz-balanced whole-row blocks
+    std::vector<int> rb(g + 1, m);
+    rb[0] = 0;
+    for (int d = 1; d < g; ++d) {
+        const long long target = (long long)nnz * d / g;
+        int lo = rb[d - 1], hi = m;  // first row r with rowptr[r] >= target
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (rowptr[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        rb[d] = lo;
+    }
+    struct Blk {
+        int phys = 0;
+        sblas_csr_s A;
+        int *cp = nullptr, *ri = nullptr;
+        double *cv = nullptr;
+        hipStream_t s = nullptr;
+    };
+    std::vector<Blk> B(g);
+    int *h_ptrs = nullptr, *h_base = nullptr, *h_rid = nullptr, *h_row0 = nullptr, *h_cp = nullptr,
+        *h_ri = nullptr;
+    double *h_val = nullptr, *h_cv = nullptr;
+    long long *h_start = nullptr;
+    hipStream_t s0 = nullptr;
+    auto cleanup = [&]() {
+        for (auto &b : B) {
+            DeviceGuard gd(b.phys);
+            (void)hipFree(b.A.rowptr);
+            (void)hipFree(b.A.col);
+            (void)hipFree(b.A.val);
+            (void)hipFree(b.cp);
+            (void)hipFree(b.ri);
+            (void)hipFree(b.cv);
+            if (b.s) (void)hipStreamDestroy(b.s);
+        }
+        DeviceGuard gd(0);
+        for (void *p : {(void *)h_ptrs, (void *)h_base, (void *)h_rid, (void *)h_row0, (void *)h_cp,
+                        (void *)h_ri, (void *)h_val, (void *)h_cv, (void *)h_start})
+            (void)hipFree(p);
+        if (s0) (void)hipStreamDestroy(s0);
+    };
+#define TG(expr)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error("csr2csc_mgpu: %s -> %s", #expr, hipGetErrorString(e_)); \
+            cleanup();                                                         \
+            return SBLAS_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+    // upload the blocks
+    std::vector<long long> start(g + 1, 0);
+    for (int d = 0; d < g; ++d) {
+        Blk &b = B[d];
+        b.phys = d % count;
+        DeviceGuard gd(b.phys);
+        TG(hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
+        const int r0 = rb[d], r1 = rb[d + 1];
+        const int e0 = rowptr[r0], e1 = rowptr[r1];
+        std::vector<int> lrp((size_t)(r1 - r0) + 1);
+        for (int r = r0; r <= r1; ++r) lrp[(size_t)(r - r0)] = rowptr[r] - e0;
+        b.A.device = b.phys;
+        b.A.m = r1 - r0;
+        b.A.n = n;
+        b.A.nnz = e1 - e0;
+        start[d + 1] = start[d] + (e1 - e0);
+        TG(hipMalloc(&b.A.rowptr, sizeof(int) * lrp.size()));
+        TG(hipMalloc(&b.A.col, sizeof(int) * std::max(e1 - e0, 1)));
+        TG(hipMalloc(&b.A.val, sizeof(double) * std::max(e1 - e0, 1)));
+        TG(hipMalloc(&b.cp, sizeof(int) * ((size_t)n + 1)));
+        TG(hipMalloc(&b.ri, sizeof(int) * std::max(e1 - e0, 1)));
+        TG(hipMalloc(&b.cv, sizeof(double) * std::max(e1 - e0, 1)));
+        TG(hipMemcpy(b.A.rowptr, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
+        if (e1 > e0) {
+            TG(hipMemcpy(b.A.col, col + e0, sizeof(int) * (e1 - e0), hipMemcpyHostToDevice));
+            TG(hipMemcpy(b.A.val, val + e0, sizeof(double) * (e1 - e0), hipMemcpyHostToDevice));
+        }
+    }
+    {
+        DeviceGuard gd(0);
+        TG(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+        TG(hipMalloc(&h_ptrs, sizeof(int) * (size_t)g * (n + 1)));
+        TG(hipMalloc(&h_base, sizeof(int) * std::max<size_t>((size_t)g * n, 1)));
+        TG(hipMalloc(&h_rid, sizeof(int) * std::max(nnz, 1)));
+        TG(hipMalloc(&h_val, sizeof(double) * std::max(nnz, 1)));
+        TG(hipMalloc(&h_row0, sizeof(int) * g));
+        TG(hipMalloc(&h_start, sizeof(long long) * (g + 1)));
+        TG(hipMalloc(&h_cp, sizeof(int) * ((size_t)n + 1)));
+        TG(hipMalloc(&h_ri, sizeof(int) * std::max(nnz, 1)));
+        TG(hipMalloc(&h_cv, sizeof(double) * std::max(nnz, 1)));
+        TG(hipMemcpy(h_row0, rb.data(), sizeof(int) * g, hipMemcpyHostToDevice));
+        TG(hipMemcpy(h_start, start.data(), sizeof(long long) * (g + 1), hipMemcpyHostToDevice));
+    }
+    for (int p = 0; p < std::min(count, g); ++p) {
+        DeviceGuard gd(p);
+        TG(hipDeviceSynchronize());
+    }
+    // 1) block transposes, concurrently on their devices
+    const double t0 = sblas_get_time();
+    for (int d = 0; d < g; ++d) {
+        Blk &b = B[d];
+        DeviceGuard gd(b.phys);
+        const int st = launch_transpose(b.A, b.cp, b.ri, b.cv, b.s);
+        if (st != SBLAS_OK) {
+            cleanup();
+            return st;
+        }
+    }
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(B[d].phys);
+        TG(hipStreamSynchronize(B[d].s));
+    }
+    const double t1 = sblas_get_time();
+    // 2) pieces to device 0 (peer DMA) and compose there
+    {
+        DeviceGuard gd(0);
+        for (int d = 0; d < g; ++d) {
+            const Blk &b = B[d];
+            const long long k = start[d + 1] - start[d];
+            TG(hipMemcpyPeerAsync(h_ptrs + (size_t)d * (n + 1), 0, b.cp, b.phys, sizeof(int) * ((size_t)n + 1), s0));
+            if (k) {
+                TG(hipMemcpyPeerAsync(h_rid + start[d], 0, b.ri, b.phys, sizeof(int) * k, s0));
+                TG(hipMemcpyPeerAsync(h_val + start[d], 0, b.cv, b.phys, sizeof(double) * k, s0));
+            }
+        }
+        hipLaunchKernelGGL(k_compose_ptr, dim3((n + 1 + 255) / 256), dim3(256), 0, s0, h_ptrs, g, n, h_cp,
+                           h_base);
+        if (nnz && n > 0)
+            hipLaunchKernelGGL(k_compose_val, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s0, h_ptrs,
+                               h_base, h_start, h_row0, g, n, (long long)nnz, h_rid, h_val, h_ri, h_cv);
+        TG(hipGetLastError());
+        TG(hipStreamSynchronize(s0));
+    }
+    const double t2 = sblas_get_time();
+    if (ms_transpose) *ms_transpose = (t1 - t0) * 1e3;
+    if (ms_compose) *ms_compose = (t2 - t1) * 1e3;
+    {
+        DeviceGuard gd(0);
+        TG(hipMemcpy(colptr_out, h_cp, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToHost));
+        if (nnz) {
+            TG(hipMemcpy(rowidx_out, h_ri, sizeof(int) * nnz, hipMemcpyDeviceToHost));
+            TG(hipMemcpy(cval_out, h_cv, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+        }
+    }
+#undef TG
+    cleanup();
+    return SBLAS_OK;
+}
+
+namespace sblas {
 }  // namespace sblas

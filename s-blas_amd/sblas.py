@@ -83,6 +83,8 @@ _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
 _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
 _sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
+_sig("sblas_csr2csc_mgpu", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p)
+_sig("sblas_sptrans", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
 _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
 _sig("sblas_csrbin_write", _i, C.c_char_p, _i, _i, _ll, _p, _p, _p)
@@ -213,6 +215,22 @@ def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int
                                     ptr(x), ngpu, C.byref(ms)), "trsv_mgpu_solve")
     x = x[:n * rhs]
     return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
+
+
+def csr2csc_mgpu(m: int, n: int, rowptr, col, val, ngpu: int):
+    """Multi-device CSR -> CSC of host arrays (sblas_csr2csc_mgpu).
+    Returns (colptr, rowidx, val, ms_transpose, ms_compose)."""
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    nnz = int(rp[-1])
+    ci = np.ascontiguousarray(col, np.int32)
+    v = np.ascontiguousarray(val, np.float64)
+    cp = np.zeros(n + 1, np.int32)
+    ri = np.zeros(max(nnz, 1), np.int32)
+    cv = np.zeros(max(nnz, 1), np.float64)
+    t1, t2 = C.c_double(), C.c_double()
+    check(lib.sblas_csr2csc_mgpu(m, n, nnz, ngpu, ptr(rp), ptr(ci), ptr(v), ptr(cp), ptr(ri),
+                                 ptr(cv), C.byref(t1), C.byref(t2)), "csr2csc_mgpu")
+    return cp, ri[:nnz], cv[:nnz], t1.value, t2.value
 
 
 def gen_vector(n: int, seed: int) -> np.ndarray:

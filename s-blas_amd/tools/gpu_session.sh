@@ -22,7 +22,8 @@ if [[ $STEP == all || $STEP == cli ]]; then
   timeout -k 10 300 ./s-blas_amd/bin/test_sptrsv -n 1 -rhs 1 -forward -mtx tests/golden/ash85.mtx > $O/cli_sptrsv.log 2>&1 &&
   timeout -k 10 300 ./s-blas_amd/bin/test_sptrsv -n 1 -rhs 1 -backward -mtx tests/golden/qh768.mtx -opt 1 > $O/cli_sptrsv_b.log 2>&1 &&
   timeout -k 10 300 ./s-blas_amd/bin/test_sptrsv -n 3 -rhs 1 -forward -mtx tests/golden/qh768.mtx > $O/cli_sptrsv_mgpu.log 2>&1 &&
-  timeout -k 10 300 ./s-blas_amd/bin/test_sptrsv -n 2 -rhs 4 -backward -mtx tests/golden/ash85.mtx > $O/cli_sptrsm.log 2>&1 || { echo cli failed; tail -5 $O/cli_*.log; exit 1; }
+  timeout -k 10 300 ./s-blas_amd/bin/test_sptrsv -n 2 -rhs 4 -backward -mtx tests/golden/ash85.mtx > $O/cli_sptrsm.log 2>&1 &&
+  timeout -k 10 300 ./s-blas_amd/bin/test_sptrans -n 4 -csr -mtx tests/golden/qh768.mtx > $O/cli_sptrans.log 2>&1 || { echo cli failed; tail -5 $O/cli_*.log; exit 1; }
   tail -n 2 $O/cli_*.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
