@@ -244,6 +244,7 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     const size_t need = (size_t)(n + 1) + 2 * (size_t)nnz + 4 + 2 * (size_t)n + scan_ints;
     TransposeScratch &S = g_tscratch[A.device & 63];
     if (S.ints < need) {
+        if (S.buf) SBLAS_HIP(hipStreamSynchronize(s));  // earlier work on s may still use it
         (void)hipFree(S.buf);
         S.buf = nullptr;
         S.ints = 0;
@@ -356,6 +357,9 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
         hipStream_t s = nullptr;
     };
     std::vector<Blk> B(g);
+    // one stream per physical device: blocks that wrap onto the same GPU run
+    // in order (they share that device's transpose scratch)
+    std::vector<hipStream_t> streams((size_t)std::min(count, g), nullptr);
     int *h_ptrs = nullptr, *h_base = nullptr, *h_rid = nullptr, *h_row0 = nullptr, *h_cp = nullptr,
         *h_ri = nullptr;
     double *h_val = nullptr, *h_cv = nullptr;
@@ -370,8 +374,12 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
             (void)hipFree(b.cp);
             (void)hipFree(b.ri);
             (void)hipFree(b.cv);
-            if (b.s) (void)hipStreamDestroy(b.s);
         }
+        for (size_t p = 0; p < streams.size(); ++p)
+            if (streams[p]) {
+                DeviceGuard gd((int)p);
+                (void)hipStreamDestroy(streams[p]);
+            }
         DeviceGuard gd(0);
         for (void *p : {(void *)h_ptrs, (void *)h_base, (void *)h_rid, (void *)h_row0, (void *)h_cp,
                         (void *)h_ri, (void *)h_val, (void *)h_cv, (void *)h_start})
@@ -393,7 +401,8 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
         Blk &b = B[d];
         b.phys = d % count;
         DeviceGuard gd(b.phys);
-        TG(hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
+        if (!streams[(size_t)b.phys]) TG(hipStreamCreateWithFlags(&streams[(size_t)b.phys], hipStreamNonBlocking));
+        b.s = streams[(size_t)b.phys];
         const int r0 = rb[d], r1 = rb[d + 1];
         const int e0 = rowptr[r0], e1 = rowptr[r1];
         std::vector<int> lrp((size_t)(r1 - r0) + 1);
