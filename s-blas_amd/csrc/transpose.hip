@@ -3,16 +3,11 @@
 // Semantics of sptrsv/sptrsv_v1/src/tranpose.h:6-43 (matrix_transposition):
 // column histogram, exclusive scan, then a STABLE scatter in row order, so
 // row indices ascend inside every column and equal-(row,col) duplicates keep
-// their CSR order.  GPU form:
-//   1. histogram of columns (int atomics) into colptr[c+1];
-//   2. in-place inclusive scan (multi-block, recursive) -> colptr;
-//   3. scatter the CSR element index e of every nonzero to an atomic slot of
-//      its column (order inside a column is arbitrary here);
-//   4. segmented sort of each column's element indices (e ascending == CSR
-//      order == the reference's stable order): per-thread insertion sort for
-//      short columns, LDS bitonic sort per workgroup up to 4096, a
-//      global-memory merge sort per workgroup beyond;
-//   5. gather: rowidx = row of e (binary search of rowptr), cval = val[e].
+// their CSR order.  GPU form: a stable LSD radix sort of the nonzeros (in
+// CSR order) keyed by column, carrying (row, value), 8 bits per pass
+// (ceil(log2 n / 8) passes); stability makes rows ascend inside each column
+// exactly as the reference's ordered scatter does.  colptr is read off the
+// sorted keys.
 #include <algorithm>
 #include <climits>
 #include <vector>
@@ -87,193 +82,212 @@ int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s)
     return SBLAS_OK;
 }
 
-__global__ void k_col_hist(const int *__restrict__ col, long long nnz, int *__restrict__ cnt1)
+// ---- stable LSD radix sort of (col, row, val) by col -----------------------
+// Tiles of kRxTile consecutive nonzeros; 8-bit digits; per pass
+//   k_rx_count   : per-tile digit histogram in LDS -> counts[digit][tile]
+//   scan         : inclusive scan of counts (digit-major) -> global offsets
+//   k_rx_scatter : stable in-tile ranking (wave ballots per digit bit, wave
+//                  order through LDS), tile staged in LDS in digit order, then
+//                  written out as per-digit runs.
+// No global atomics (they execute memory-side, one 64-B request per lane).
+constexpr int kRxThreads = 256;
+constexpr int kRxItems = 16;
+constexpr int kRxTile = kRxThreads * kRxItems;
+constexpr int kRxWaves = kRxThreads / 64;
+
+__global__ void k_expand_rows(const int *__restrict__ rowptr, int m, int *__restrict__ rows)
 {
-    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < nnz) atomicAdd(&cnt1[col[e] + 1], 1);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) rows[e] = r;
 }
 
-__global__ void k_col_scatter(const int *__restrict__ col, long long nnz, int *__restrict__ next,
-                              int *__restrict__ perm)
+__global__ __launch_bounds__(kRxThreads) void k_rx_count(const int *__restrict__ keys, long long nnz,
+                                                         int shift, int ntiles, int *__restrict__ counts)
 {
-    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < nnz) perm[atomicAdd(&next[col[e]], 1)] = (int)e;
+    __shared__ int h[256];
+    const int t = threadIdx.x;
+    h[t] = 0;
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * kRxTile;
+#pragma unroll
+    for (int j = 0; j < kRxItems; ++j) {
+        const long long i = base + j * kRxThreads + t;
+        if (i < nnz) atomicAdd(&h[(keys[i] >> shift) & 255], 1);
+    }
+    __syncthreads();
+    counts[(size_t)t * ntiles + blockIdx.x] = h[t];
 }
 
-// Short columns sorted in place by their own thread; others queued.
-__global__ void k_sort_short(const int *__restrict__ colptr, int n, int *__restrict__ perm,
-                             int *__restrict__ qcount, int *__restrict__ qmed,
-                             int *__restrict__ qbig)
+__global__ __launch_bounds__(kRxThreads, 2) void k_rx_scatter(
+    const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
+    int shift, int ntiles, const int *__restrict__ incl, int *__restrict__ kout, int *__restrict__ rout,
+    double *__restrict__ vout)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    const int a = colptr[c], b = colptr[c + 1];
-    const int len = b - a;
-    if (len <= 32) {
-        for (int i = a + 1; i < b; ++i) {
-            const int key = perm[i];
-            int j = i - 1;
-            while (j >= a && perm[j] > key) {
-                perm[j + 1] = perm[j];
-                --j;
-            }
-            perm[j + 1] = key;
+    __shared__ int wcnt[kRxWaves][256];
+    __shared__ int run[256], lstart[256], gbase[256], wtot[kRxWaves];
+    __shared__ int skey[kRxTile], srow[kRxTile];
+    __shared__ double sval[kRxTile];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    run[t] = 0;
+#pragma unroll
+    for (int q = 0; q < kRxWaves; ++q) wcnt[q][t] = 0;
+    const long long base = (long long)blockIdx.x * kRxTile;
+    const int valid = (int)min((long long)kRxTile, nnz - base);
+    int kk[kRxItems], rr[kRxItems], lp[kRxItems];
+    double vv[kRxItems];
+#pragma unroll
+    for (int j = 0; j < kRxItems; ++j) {
+        const int li = j * kRxThreads + t;
+        if (li < valid) {
+            kk[j] = kin[base + li];
+            rr[j] = rin[base + li];
+            vv[j] = vin[base + li];
+        } else {
+            kk[j] = -1;  // digit 255, ranked after every real element
+            rr[j] = 0;
+            vv[j] = 0.0;
         }
-    } else if (len <= 4096) {
-        qmed[atomicAdd(&qcount[0], 1)] = c;
-    } else {
-        qbig[atomicAdd(&qcount[1], 1)] = c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRxItems; ++j) {
+        const int d = (kk[j] >> shift) & 255;
+        unsigned long long mm = ~0ull;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const unsigned long long bal = __ballot((d >> b) & 1);
+            mm &= ((d >> b) & 1) ? bal : ~bal;
+        }
+        const int rank = __popcll(mm & lt);
+        if (rank == 0) wcnt[w][d] = __popcll(mm);
+        __syncthreads();
+        int pre = run[d];
+        for (int q = 0; q < w; ++q) pre += wcnt[q][d];
+        lp[j] = pre + rank;
+        __syncthreads();
+        int add = 0;
+#pragma unroll
+        for (int q = 0; q < kRxWaves; ++q) {
+            add += wcnt[q][t];
+            wcnt[q][t] = 0;
+        }
+        run[t] += add;
+        __syncthreads();
+    }
+    if (t == 255) run[255] -= kRxTile - valid;  // padding is not part of the output
+    __syncthreads();
+    // exclusive scan of the tile's digit counts -> lstart
+    const int c = run[t];
+    const int inc = wave_incl_scan(c);
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    int woff = 0;
+    for (int q = 0; q < w; ++q) woff += wtot[q];
+    lstart[t] = woff + inc - c;
+    gbase[t] = incl[(size_t)t * ntiles + blockIdx.x] - c;  // inclusive scan -> exclusive
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRxItems; ++j) {
+        const int li = j * kRxThreads + t;
+        if (li < valid) {
+            const int pos = lstart[(kk[j] >> shift) & 255] + lp[j];
+            skey[pos] = kk[j];
+            srow[pos] = rr[j];
+            sval[pos] = vv[j];
+        }
+    }
+    __syncthreads();
+    for (int li = t; li < valid; li += kRxThreads) {
+        const int k = skey[li];
+        const int d = (k >> shift) & 255;
+        const long long g = (long long)gbase[d] + (li - lstart[d]);
+        kout[g] = k;
+        rout[g] = srow[li];
+        vout[g] = sval[li];
     }
 }
 
-__global__ __launch_bounds__(256) void k_sort_medium(const int *__restrict__ colptr,
-                                                     int *__restrict__ perm,
-                                                     const int *__restrict__ qcount,
-                                                     const int *__restrict__ qmed)
-{
-    __shared__ int sk[4096];
-    const int nq = qcount[0];
-    for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-        const int c = qmed[q];
-        const int a = colptr[c], len = colptr[c + 1] - a;
-        int P = 64;
-        while (P < len) P <<= 1;
-        for (int i = threadIdx.x; i < P; i += 256) sk[i] = i < len ? perm[a + i] : INT_MAX;
-        __syncthreads();
-        for (int k = 2; k <= P; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = threadIdx.x; i < P; i += 256) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const bool up = (i & k) == 0;
-                        const int x = sk[i], y = sk[ixj];
-                        if (up ? x > y : x < y) {
-                            sk[i] = y;
-                            sk[ixj] = x;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int i = threadIdx.x; i < len; i += 256) perm[a + i] = sk[i];
-        __syncthreads();
-    }
-}
-
-// Bottom-up merge sort of one long column per workgroup in global memory
-// (ping-pong with tmp, same offsets).  Keys are unique.
-__global__ __launch_bounds__(256) void k_sort_big(const int *__restrict__ colptr,
-                                                  int *__restrict__ perm, int *__restrict__ tmp,
-                                                  const int *__restrict__ qcount,
-                                                  const int *__restrict__ qbig)
-{
-    const int nq = qcount[1];
-    for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-        const int c = qbig[q];
-        const int a = colptr[c], len = colptr[c + 1] - a;
-        int *src = perm + a, *dst = tmp + a;
-        for (int w = 1; w < len; w <<= 1) {
-            for (int i = threadIdx.x; i < len; i += 256) {
-                const int run = i / (2 * w);
-                const int s0 = run * 2 * w;
-                const int m0 = min(s0 + w, len), e0 = min(s0 + 2 * w, len);
-                const int key = src[i];
-                int pos;
-                if (i < m0) {  // left run: count right-run keys < key
-                    int lo = m0, hi = e0;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (src[mid] < key) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    pos = s0 + (i - s0) + (lo - m0);
-                } else {  // right run: count left-run keys < key
-                    int lo = s0, hi = m0;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (src[mid] < key) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    pos = s0 + (i - m0) + (lo - s0);
-                }
-                dst[pos] = key;
-            }
-            __syncthreads();
-            int *t = src;
-            src = dst;
-            dst = t;
-        }
-        if (src != perm + a)
-            for (int i = threadIdx.x; i < len; i += 256) perm[a + i] = src[i];
-        __syncthreads();
-    }
-}
-
-__global__ void k_gather_csc(const int *__restrict__ rowptr, int m, const double *__restrict__ val,
-                             const int *__restrict__ perm, long long nnz, int *__restrict__ rowidx,
-                             double *__restrict__ cval)
+// colptr from the sorted keys: colptr[c] = first position whose key >= c
+__global__ void k_colptr_sorted(const int *__restrict__ keys, long long nnz, int n, int *__restrict__ colptr)
 {
     const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= nnz) return;
-    const int e = perm[p];
-    int lo = 0, hi = m - 1;  // row r: rowptr[r] <= e < rowptr[r+1]
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (rowptr[mid] <= e) lo = mid;
-        else hi = mid - 1;
-    }
-    if (rowidx) rowidx[p] = lo;
-    if (cval) cval[p] = val[e];
+    const int k = keys[p];
+    const int prev = p == 0 ? -1 : keys[p - 1];
+    for (int c = prev + 1; c <= k; ++c) colptr[c] = (int)p;
+    if (p == nnz - 1)
+        for (int c = k + 1; c <= n; ++c) colptr[c] = (int)nnz;
 }
 
 struct TransposeScratch {
-    int *buf = nullptr;
-    size_t ints = 0;
+    void *buf = nullptr;
+    size_t bytes = 0;
 };
 static thread_local TransposeScratch g_tscratch[64];
 
 int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cval, hipStream_t s)
 {
     const long long nnz = A.nnz;
-    const int n = A.n;
-    SBLAS_HIP(hipMemsetAsync(colptr, 0, sizeof(int) * ((size_t)n + 1), s));
-    if (nnz == 0) return SBLAS_OK;
-    // scratch: next[n+1] | perm[nnz] | tmp[nnz] | q[2] | qmed[n] | qbig[n] | scan
-    const size_t scan_ints = (size_t)((n + 1) / kScanTile + 64) * 2;
-    const size_t need = (size_t)(n + 1) + 2 * (size_t)nnz + 4 + 2 * (size_t)n + scan_ints;
+    const int n = A.n, m = A.m;
+    if (nnz == 0) {
+        SBLAS_HIP(hipMemsetAsync(colptr, 0, sizeof(int) * ((size_t)n + 1), s));
+        return SBLAS_OK;
+    }
+    int nbits = 0;
+    while (nbits < 31 && (n - 1) >> nbits) ++nbits;
+    const int passes = std::max(1, (nbits + 7) / 8);
+    const int ntiles = (int)((nnz + kRxTile - 1) / kRxTile);
+    const long long ncnt = 256LL * ntiles;
+    const size_t scan_ints = (size_t)(ncnt / kScanTile + 64) * 2;
+    // scratch: keysA rowsA valsA | keysB rowsB valsB | counts | scan (+ outputs when null)
+    const size_t z = (size_t)nnz;
+    const size_t need = z * 32 + (size_t)ncnt * 4 + scan_ints * 4 + (rowidx ? 0 : z * 4) +
+                        (cval ? 0 : z * 8) + 256;
     TransposeScratch &S = g_tscratch[A.device & 63];
-    if (S.ints < need) {
+    if (S.bytes < need) {
         if (S.buf) SBLAS_HIP(hipStreamSynchronize(s));  // earlier work on s may still use it
         (void)hipFree(S.buf);
         S.buf = nullptr;
-        S.ints = 0;
-        SBLAS_HIP(hipMalloc(&S.buf, need * sizeof(int)));
-        S.ints = need;
+        S.bytes = 0;
+        SBLAS_HIP(hipMalloc(&S.buf, need));
+        S.bytes = need;
     }
-    int *next = S.buf;
-    int *perm = next + (n + 1);
-    int *tmp = perm + nnz;
-    int *qc = tmp + nnz;
-    int *qmed = qc + 4;
-    int *qbig = qmed + n;
-    int *scan = qbig + n;
-    const unsigned gb = (unsigned)((nnz + 255) / 256);
-    hipLaunchKernelGGL(k_col_hist, dim3(gb), dim3(256), 0, s, A.col, nnz, colptr);
-    SBLAS_TRY(scan_inclusive(colptr, (long long)n + 1, scan, s));
-    SBLAS_HIP(hipMemcpyAsync(next, colptr, sizeof(int) * ((size_t)n + 1), hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL(k_col_scatter, dim3(gb), dim3(256), 0, s, A.col, nnz, next, perm);
-    SBLAS_HIP(hipMemsetAsync(qc, 0, sizeof(int) * 4, s));
-    hipLaunchKernelGGL(k_sort_short, dim3((n + 255) / 256), dim3(256), 0, s, colptr, n, perm, qc,
-                       qmed, qbig);
-    hipLaunchKernelGGL(k_sort_medium, dim3(1024), dim3(256), 0, s, colptr, perm, qc, qmed);
-    hipLaunchKernelGGL(k_sort_big, dim3(256), dim3(256), 0, s, colptr, perm, tmp, qc, qbig);
-    hipLaunchKernelGGL(k_gather_csc, dim3(gb), dim3(256), 0, s, A.rowptr, A.m, A.val, perm, nnz,
-                       rowidx, cval);
+    char *p = (char *)S.buf;
+    double *valsA = (double *)p;
+    double *valsB = valsA + z;
+    int *keysA = (int *)(valsB + z);
+    int *rowsA = keysA + z;
+    int *keysB = rowsA + z;
+    int *rowsB = keysB + z;
+    int *counts = rowsB + z;
+    int *scan = counts + ncnt;
+    int *rout_final = rowidx ? rowidx : scan + scan_ints;
+    double *vout_final = cval ? cval : (double *)(((uintptr_t)(rout_final + (rowidx ? 0 : z)) + 7) & ~(uintptr_t)7);
+    hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
+    const int *kin = A.col, *rin = rowsB;
+    const double *vin = A.val;
+    for (int ps = 0; ps < passes; ++ps) {
+        const int shift = 8 * ps;
+        const bool last = ps == passes - 1;
+        // pass ps reads set (ps even: input/B, odd: A) and writes the other
+        int *ko = (ps & 1) ? keysB : keysA;
+        int *ro = last ? rout_final : ((ps & 1) ? rowsB : rowsA);
+        double *vo = last ? vout_final : ((ps & 1) ? valsB : valsA);
+        hipLaunchKernelGGL(k_rx_count, dim3(ntiles), dim3(kRxThreads), 0, s, kin, nnz, shift, ntiles, counts);
+        SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
+        hipLaunchKernelGGL(k_rx_scatter, dim3(ntiles), dim3(kRxThreads), 0, s, kin, rin, vin, nnz, shift,
+                           ntiles, counts, ko, ro, vo);
+        kin = ko;
+        rin = ro;
+        vin = vo;
+    }
+    hipLaunchKernelGGL(k_colptr_sorted, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, kin, nnz, n,
+                       colptr);
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;
 }
-
 
 // ---- multi-device CSR -> CSC (sptrans_v1 kernal_sptrans,
 // sptrans/sptrans_v1/src/sptrans_kernal.h:80-555) -------------------------
