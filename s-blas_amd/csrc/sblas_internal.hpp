@@ -106,6 +106,7 @@ struct SpmmPlan {
     int *ucol = nullptr;       // [4*chunks] union columns (padded)
     double *atile = nullptr;   // [chunks*64] A fragments, lane-major
     int nsparse = 0;           // rows handled by the row-wave kernel
+    long long sparse_nnz = 0;  // their nonzeros
     int *srows = nullptr;
     double fill_thresh = 0.25;
     bool ready = false;

@@ -76,6 +76,64 @@ __global__ __launch_bounds__(256) void k_spmm_rowwave(
     }
 }
 
+// Long rows (rail4284: ~2,600 nnz per row, only m = 4,284 rows): one
+// WORKGROUP per (row, 64-column slab), the row's nonzeros split over its 4
+// waves, 16 B-row gathers in flight per lane, partial sums combined in LDS.
+// A wave-per-row kernel leaves each wave walking ~2,600 dependent B-row
+// gathers 8 at a time -- latency-bound with only m waves in the grid.
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmm_rowsplitk(
+    const int *__restrict__ rbeg, const int *__restrict__ rend, const int *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ B, long long ldb,
+    int m, int n, int nslab, double alpha, double beta, double *__restrict__ C,
+    long long ldc, const int *__restrict__ rows)
+{
+    __shared__ double part[3][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long blk = blockIdx.x;
+    const int r = rows ? rows[blk / nslab] : (int)(blk / nslab);
+    const int c = (int)(blk % nslab) * 64 + lane;
+    const bool live = c < n;
+    const int cc = live ? c : 0;
+    const int a0 = rbeg[r], a1 = rend[r];
+    const int len = a1 - a0;
+    const int q0 = a0 + (int)((long long)len * wv / 4), q1 = a0 + (int)((long long)len * (wv + 1) / 4);
+    double acc = 0.0, acc2 = 0.0;
+    for (int base = q0; base < q1; base += 64) {
+        const int cnt = min(64, q1 - base);
+        const int my_j = lane < cnt ? col[base + lane] : 0;
+        const double my_a = lane < cnt ? val[base + lane] : 0.0;
+        int q = 0;
+        for (; q + 16 <= cnt; q += 16) {
+            double b[16], a[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int j = __shfl(my_j, q + u, 64);
+                a[u] = __shfl(my_a, q + u, 64);
+                b[u] = B[(long long)j * ldb + cc];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; u += 2) {
+                acc += a[u] * b[u];
+                acc2 += a[u + 1] * b[u + 1];
+            }
+        }
+        for (; q < cnt; ++q) {
+            const int j = __shfl(my_j, q, 64);
+            const double a = __shfl(my_a, q, 64);
+            acc += a * B[(long long)j * ldb + cc];
+        }
+    }
+    acc += acc2;
+    if (wv > 0) part[wv - 1][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && live) {
+        acc += part[0][lane] + part[1][lane] + part[2][lane];
+        double *o = C + (long long)c * ldc + r;
+        *o = kBeta ? alpha * acc + beta * *o : alpha * acc;
+    }
+}
+
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 // One wave per (MFMA block, 64-column group of C): 4 accumulators of
@@ -142,6 +200,8 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     }
     std::vector<int> mblock, mchunk{0}, ucol, srows;
     std::vector<double> atile;
+    P.sparse_nnz = 0;
+
     std::vector<int> U;
     const int nblk = (m + 15) / 16;
     for (int b = 0; b < nblk; ++b) {
@@ -154,6 +214,7 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
                            (double)nz >= P.fill_thresh * 16.0 * (double)U.size();
         if (!dense) {
             for (int r = r0; r < r1; ++r) srows.push_back(r);
+            P.sparse_nnz += nz;
             continue;
         }
         const int nch = ((int)U.size() + 3) / 4;
@@ -250,7 +311,20 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     // rows of sparse blocks (all rows when no plan / no dense block)
     const int nrows = P.ready ? P.nsparse : A.m;
     const int *rows = P.ready ? P.srows : nullptr;
-    if (nrows > 0) {
+    // long rows on average -> a workgroup per (row, slab); env override for
+    // experiments: SBLAS_SPMM_SPLITK=0/1
+    const long long nnz_rows = P.ready ? P.sparse_nnz : A.nnz;
+    bool splitk = nrows > 0 && nnz_rows >= 256LL * nrows;
+    if (const char *e = std::getenv("SBLAS_SPMM_SPLITK")) splitk = nrows > 0 && std::atoi(e) != 0;
+    if (splitk) {
+        const unsigned nb = (unsigned)((long long)nrows * nslab);
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmm_rowsplitk<true>, dim3(nb), dim3(256), 0, s, A.rowptr, A.rowptr + 1,
+                               A.col, A.val, Brow, ldr, nrows, n, nslab, alpha, beta, C, (long long)ldc, rows);
+        else
+            hipLaunchKernelGGL(k_spmm_rowsplitk<false>, dim3(nb), dim3(256), 0, s, A.rowptr, A.rowptr + 1,
+                               A.col, A.val, Brow, ldr, nrows, n, nslab, alpha, beta, C, (long long)ldc, rows);
+    } else if (nrows > 0) {
         const long long waves = (long long)nrows * nslab;
         const unsigned nb = (unsigned)((waves + 3) / 4);
         if (beta != 0.0)

@@ -33,10 +33,15 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
+@pytest.mark.parametrize("splitk", ["auto", "0", "1"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
-def test_spmm(torch_cuda, sb, orc, ncols, layout):
+def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
+    """Both row kernels: wave per row and workgroup per row (split over its
+    nonzeros; picked automatically for long rows)."""
     torch = torch_cuda
+    if splitk != "auto":
+        monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
     rng = np.random.default_rng(ncols + 10 * layout)
     m, k = 700, 5000
     rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
