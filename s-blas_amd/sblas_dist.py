@@ -133,3 +133,82 @@ class DistSpMV:
 
     def close(self):
         self.A.close()
+
+
+# ---------------------------------------------------------------------------
+# SpMM: rows of A split by nnz into whole-row blocks, B
+# replicated on every rank, C row slices disjoint -> one all-gather, no
+# split-row fix-up.  (The reference's alternative, B split by columns with A
+# replicated, needs no exchange at all; the row split is the one that scales
+# A's footprint and bytes with the rank count.)
+# ---------------------------------------------------------------------------
+def row_blocks_by_nnz(rowptr: np.ndarray, world: int) -> np.ndarray:
+    """world+1 row boundaries; block d holds whole rows, ~nnz/world nonzeros
+    (first row whose start reaches d*nnz/world)."""
+    rp = np.asarray(rowptr, np.int64)
+    nnz = int(rp[-1])
+    targets = (np.arange(world + 1, dtype=np.int64) * nnz) // max(world, 1)
+    rb = np.searchsorted(rp, targets, side="left").astype(np.int64)
+    rb[0], rb[-1] = 0, len(rp) - 1
+    return np.maximum.accumulate(rb)
+
+
+class DistSpMM:
+    """One rank's share of C = alpha*A*B + beta*C (B row-major k x ncols on
+    every rank; C column-major m x ncols, kept as a (ncols, m) tensor)."""
+
+    def __init__(self, rowptr, col, val, k: int, ncols: int, world: int, rank: int, device: int,
+                 torch, dist=None):
+        self.torch, self.dist, self.world, self.rank = torch, dist, world, rank
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        self.m, self.ncols = len(rp) - 1, ncols
+        self.rb = row_blocks_by_nnz(rp, world)
+        r0, r1 = int(self.rb[rank]), int(self.rb[rank + 1])
+        i0, i1 = int(rp[r0]), int(rp[r1])
+        self.r0, self.r1 = r0, r1
+        self.A = sblas.DeviceCSR.upload_slice(device, k, rp, np.ascontiguousarray(col, np.int32),
+                                              np.ascontiguousarray(val, np.float64), r0, r1, i0, i1)
+        self.stride = int(max(1, np.diff(self.rb).max()))
+        dev = torch.device("cuda", device)
+        f64 = torch.float64
+        self.c_local = torch.zeros((ncols, self.stride), dtype=f64, device=dev)  # ld = stride
+        self.gathered = torch.zeros((world, ncols, self.stride), dtype=f64, device=dev)
+        self.c_full = torch.zeros((ncols, self.m), dtype=f64, device=dev)
+
+    def load_c(self, c_full) -> None:
+        """Set C (a (ncols, m) device tensor) as the next call's input."""
+        self.c_full.copy_(c_full)
+        self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[:, self.r0:self.r1])
+
+    def kernel(self, alpha: float, B, beta: float, stream=None) -> None:
+        if self.r1 > self.r0:
+            self.A.spmm(self.ncols, alpha, B.data_ptr(), self.ncols, 1, beta,
+                        self.c_local.data_ptr(), self.stride, stream)
+
+    def exchange(self) -> None:
+        if self.world == 1:
+            return
+        if self.dist.get_backend() == "nccl":
+            self.dist.all_gather_into_tensor(self.gathered.view(-1), self.c_local.reshape(-1))
+        else:  # gloo rehearsal (CPU staging)
+            parts = [torch_zeros_like_cpu(self.c_local) for _ in range(self.world)]
+            self.dist.all_gather(parts, self.c_local.cpu())
+            self.gathered.copy_(self.torch.stack(parts).to(self.gathered.device))
+        for d in range(self.world):
+            a, b = int(self.rb[d]), int(self.rb[d + 1])
+            if b > a:
+                self.c_full[:, a:b].copy_(self.gathered[d, :, : b - a])
+        self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[:, self.r0:self.r1])
+
+    def result(self):
+        if self.world == 1:
+            return self.c_local[:, : self.m]
+        return self.c_full
+
+    def close(self) -> None:
+        self.A.close()
+
+
+def torch_zeros_like_cpu(t):
+    import torch
+    return torch.zeros(t.shape, dtype=t.dtype)

@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
-"""SpMM benchmark (BASELINE configs[3]), one GPU.
+"""SpMM benchmark (BASELINE configs[3]), 1..N GPUs.
 
 rail4284 is not in the container: synthetic stand-in with its shape, m =
-4,284, k = 1,092,610, nnz = 11,279,748 (2,633 nnz/row, uniform-random sorted
-columns, seed 44), B k x 64 U[0,1) (seed 45), C0 m x 64 U[0,1) (seed 46),
-alpha = -0.7, beta = 0.8 (dspmm_baseline_test.cu:518-519).  B is resident
-row-major (our layout); C column-major (ld = m).
+4,284, k = 1,092,610, nnz = 11,279,748 (2,633 nnz/row, uniform-random
+distinct sorted columns, seed 44), B k x 64 U[0,1) (seed 45), C0 m x 64
+U[0,1) (seed 46), alpha = -0.7, beta = 0.8 (dspmm_baseline_test.cu:518-519).
+B is resident row-major; C column-major (ld = m).
+
+  python bench_spmm.py                      # 1 GPU
+  torchrun --nproc-per-node N bench_spmm.py # N ranks: rows of A split by nnz,
+                                            # B replicated, C slices all-gathered
 
 Algorithmic bytes: 12*nnz + 4(m+1) + 8*k*n + 16*m*n;
-GFLOP/s = 2*nnz*n/t.  The traffic-aware floor is higher: every nonzero pulls
-a 512-B row of B (nnz*512 B = 5.8 GB through L2), reported as gbps_l2.
+GFLOP/s = 2*nnz*n/t.  The traffic-aware bound is the gather of a 512-B B row
+per nonzero (nnz*512 B = 5.8 GB through L2), reported as gbps_brow against the
+measured random-row gather rates of MI355X_MICROARCH.md (8.6 TB/s from the
+Infinity Cache, 5.7 TB/s from HBM).
 """
 import argparse
 import json
@@ -23,94 +29,162 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
+def rail_like(m, k, nnz, seed):
+    rng = np.random.default_rng(seed)
+    base, extra = divmod(nnz, m)
+    lens = np.full(m, base, np.int64)
+    lens[:extra] += 1
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.empty(nnz, np.int32)
+    for r in range(m):  # distinct sorted columns per row
+        L = int(lens[r])
+        c = np.unique(rng.integers(0, k, L + L // 8 + 16))
+        while len(c) < L:
+            c = np.unique(np.concatenate([c, rng.integers(0, k, L)]))
+        col[rp[r]:rp[r + 1]] = np.sort(rng.permutation(c)[:L])
+    return rp, col
+
+
+def blocky(m, k, width, seed):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for _ in range(m // 16):
+        cols = np.sort(rng.choice(k, width, replace=False))
+        for _ in range(16):
+            rows.append(cols[rng.random(width) < 0.9])
+    lens = np.array([len(r) for r in rows], np.int64)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return rp, np.concatenate(rows).astype(np.int32)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--m", type=int, default=4284)
-    ap.add_argument("--k", type=int, default=1_092_610)
+    ap.add_argument("--mrows", type=int, default=4284)
+    ap.add_argument("--kcols", type=int, default=1_092_610)
     ap.add_argument("--nnz", type=int, default=11_279_748)
     ap.add_argument("--ncols", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--layout", choices=["row", "col"], default="row")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--layout", choices=["row", "col"], default="row",
+                    help="B layout (1 GPU only; the multi-rank path keeps B row-major)")
     ap.add_argument("--blocky", type=int, default=0,
                     help="instead of the rail4284 shape: 16-row blocks each dense (~90%%) over "
                          "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
     args = ap.parse_args()
     import torch
     import sblas
+    import sblas_dist
 
-    m, k, n = args.m, args.k, args.ncols
-    rng = np.random.default_rng(44)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_idx = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    m, k, n = args.mrows, args.kcols, args.ncols
     if args.blocky:
-        rows = []
-        for _ in range(m // 16):
-            cols = np.sort(rng.choice(k, args.blocky, replace=False))
-            for _ in range(16):
-                rows.append(cols[rng.random(args.blocky) < 0.9])
-        m = len(rows)
-        lens = np.array([len(r) for r in rows], np.int64)
-        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-        col = np.concatenate(rows).astype(np.int32)
-        args.nnz = int(rp[-1])
+        rp, col = blocky(m, k, args.blocky, 44)
+        m = len(rp) - 1
     else:
-        base, extra = divmod(args.nnz, m)
-        lens = np.full(m, base, np.int64)
-        lens[:extra] += 1
-        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-        col = np.empty(args.nnz, np.int32)
-        for r in range(m):  # distinct sorted columns per row
-            col[rp[r]:rp[r + 1]] = np.sort(rng.choice(k, size=int(lens[r]), replace=False))
-    val = np.random.default_rng(45).random(args.nnz)
-    dev = torch.device("cuda", 0)
+        rp, col = rail_like(m, k, args.nnz, 44)
+    nnz = int(rp[-1])
+    val = np.random.default_rng(45).random(nnz)
     B = torch.rand((k, n), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(45))
     C0 = torch.rand((n, m), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(46))
-    if args.layout == "col":
+    s = torch.cuda.Stream(device=dev)
+    if world == 1 and args.layout == "col":
         Bd, ldb, lay = B.t().contiguous(), k, 0
     else:
         Bd, ldb, lay = B, n, 1
-    A = sblas.DeviceCSR.upload(0, k, rp, col, val)
-    C = C0.clone()
-    s = torch.cuda.Stream(device=dev)
-    with torch.cuda.stream(s):
-        A.spmm(n, -0.7, Bd.data_ptr(), ldb, lay, 0.8, C.data_ptr(), m, s.cuda_stream)
+    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(s)
+        if lay == 1:
+            op.kernel(-0.7, Bd, 0.8, s.cuda_stream)
+        else:
+            op.A.spmm(n, -0.7, Bd.data_ptr(), ldb, 0, 0.8, op.c_local.data_ptr(), op.stride,
+                      s.cuda_stream)
+        if ev is not None:
+            ev[1].record(s)
+        op.exchange()
+
+    def sync_barrier():
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(args.steps):
-            A.spmm(n, -0.7, Bd.data_ptr(), ldb, lay, 0.8, C.data_ptr(), m, s.cuda_stream)
-        e1.record(s)
+        if dist is not None:
+            dist.barrier()
         torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
-    # spot check 32 rows against a float64 reference on the host
-    Ch = C0.clone()
+
     with torch.cuda.stream(s):
-        A.spmm(n, -0.7, Bd.data_ptr(), ldb, lay, 0.8, Ch.data_ptr(), m, s.cuda_stream)
-    torch.cuda.synchronize()
-    rows = np.random.default_rng(0).choice(m, 32, replace=False)
-    Bh = B.cpu().numpy()
-    C0h = C0.cpu().numpy()
-    got = Ch.cpu().numpy()
-    err = 0.0
-    for r in rows:
-        a, b_ = rp[r], rp[r + 1]
-        want = -0.7 * (val[a:b_] @ Bh[col[a:b_], :]) + 0.8 * C0h[:, r]
-        err = max(err, float(np.max(np.abs(got[:, r] - want) / (np.abs(want) + 1e-300))))
-    abytes = 12 * args.nnz + 4 * (m + 1) + 8 * k * n + 16 * m * n
-    out = {
-        "metric": "fp64 CSR SpMM GFLOP/s (2*nnz*n/t), 1 MI355X",
-        "value": round(2.0 * args.nnz * n / ms / 1e6, 3), "unit": "GFLOP/s", "n_gpus": 1,
-        "steps": args.steps, "ms_per_step": round(ms, 4), "higher_is_better": True,
-        "dtype": "f64", "data": "synthetic rail4284-shaped (DESIGN.md)",
-        "config": {"workload": "C = -0.7*A*B + 0.8*C", "m": m, "k": k, "nnz": args.nnz, "ncols": n,
-                   "b_layout": args.layout, "structure": f"blocky{args.blocky}" if args.blocky
-                   else "rail4284-shaped uniform random",
-                   "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.25")},
-        "roofline": {"bound": "hbm", "achieved": round(abytes / ms / 1e6, 1), "peak": 8000.0,
-                     "unit": "GB/s", "frac": round(abytes / ms / 1e6 / 8000.0, 4)},
-        "gbps_l2_brow_traffic": round(args.nnz * n * 8 / ms / 1e6, 1),
-        "max_rel_err_32_rows": err,
-    }
-    A.close()
-    print(json.dumps(out), flush=True)
+        op.load_c(C0)
+        for _ in range(args.warmup):
+            step()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        sync_barrier()
+        t0 = time.perf_counter()
+        for q in range(args.steps):
+            step(evs[q])
+        sync_barrier()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        # one fresh step from C0 for the check
+        op.load_c(C0)
+        step()
+        torch.cuda.synchronize()
+    got = op.result().cpu().numpy()
+    stats = torch.tensor([el, kern_ms], dtype=torch.float64,
+                         device=dev if dist is None or args.dist_backend == "nccl" else "cpu")
+    if dist is not None:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    el, kern_max = float(stats[0]), float(stats[1])
+    if rank == 0:
+        rows = np.random.default_rng(0).choice(m, min(32, m), replace=False)
+        Bh = B.cpu().numpy()
+        C0h = C0.cpu().numpy()
+        err = 0.0
+        for r in rows:
+            a, b_ = rp[r], rp[r + 1]
+            want = -0.7 * (val[a:b_] @ Bh[col[a:b_], :]) + 0.8 * C0h[:, r]
+            err = max(err, float(np.max(np.abs(got[:, r] - want) / (np.abs(want) + 1e-300))))
+        ms = el / args.steps * 1e3
+        abytes = 12 * nnz + 4 * (m + 1) + 8 * k * n + 16 * m * n
+        out = {
+            "metric": "fp64 CSR SpMM GFLOP/s (2*nnz*n/t)",
+            "value": round(2.0 * nnz * n / ms / 1e6, 3), "unit": "GFLOP/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "kernel_ms_max_over_ranks": round(kern_max, 4),
+            "kernel_only_gflops": round(2.0 * nnz * n / kern_max / 1e6, 3),
+            "higher_is_better": True, "scaling": "strong", "dtype": "f64",
+            "data": "synthetic rail4284-shaped (DESIGN.md)",
+            "config": {"workload": "C = -0.7*A*B + 0.8*C", "m": m, "k": k, "nnz": nnz, "ncols": n,
+                       "b_layout": "row" if lay == 1 else "col",
+                       "structure": f"blocky{args.blocky}" if args.blocky
+                       else "rail4284-shaped uniform random",
+                       "partition": "whole-row blocks by nnz, B replicated, C all-gathered"
+                       if world > 1 else "single GPU",
+                       "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.25")},
+            "roofline": {"bound": "hbm", "achieved": round(abytes / kern_max / 1e6, 1), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(abytes / kern_max / 1e6 / 8000.0, 4)},
+            "gbps_brow": round(nnz * n * 8 / kern_max / 1e6 / max(world, 1), 1),
+            "max_rel_err_32_rows": err,
+        }
+        if world > 1 and args.dist_backend != "nccl":
+            out["note"] = f"rehearsal: {world} ranks over gloo"
+        print(json.dumps(out), flush=True)
+    op.close()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -19,3 +19,13 @@ done; done; done
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
   --master-port $((port+1)) bench.py --gpus 1 --no-cpu-baseline --check --nrows 200000 > $O/rehearsal_1_nccl.log 2>&1 || exit 1
 grep -h '^{' $O/rehearsal_1_nccl.log | cut -c1-200
+# SpMM (G2): rows of A by nnz, B replicated, C slices all-gathered
+for np in 2 3; do
+  port=$((port+7))
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
+    --master-addr 127.0.0.1 --master-port $port s-blas_amd/tools/bench_spmm.py --dist-backend gloo \
+    --mrows 1000 --kcols 100000 --nnz 500000 --steps 3 --warmup 1 > $O/rehearsal_spmm_${np}.log 2>&1 || { echo "FAIL spmm np=$np"; tail -20 $O/rehearsal_spmm_${np}.log; exit 1; }
+  grep -h '^{' $O/rehearsal_spmm_${np}.log | python3 -c "
+import sys,json
+d=json.loads(sys.stdin.read()); e=d['max_rel_err_32_rows']; print('spmm np=$np err=', e); sys.exit(0 if e < 1e-12 else 1)" || exit 1
+done

@@ -83,3 +83,57 @@ def test_gloo_protocol(world):
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res)
     assert any(c for _, _, c in res)  # the split actually crossed a row
+
+
+def _spmm_worker(rank, world, port, result_q):
+    """SpMM row-block protocol: whole-row blocks by nnz, B
+    replicated, each rank's C slice (ncols x stride, ld = stride) all-gathered
+    and placed back by the block boundaries -- as sblas_dist.DistSpMM does on
+    the GPU.  The rank-local product is the oracle (checker)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import orc
+    import sblas_dist
+    rng = np.random.default_rng(3)
+    m, k, ncols = 301, 450, 7
+    lens = rng.integers(0, 40, m)
+    lens[5] = 400  # one heavy row
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(k, L, replace=False)) for L in lens]).astype(np.int32)
+    val = rng.standard_normal(int(rp[-1]))
+    B = rng.standard_normal((k, ncols))
+    C0 = rng.standard_normal((m, ncols))
+    rb = sblas_dist.row_blocks_by_nnz(rp, world)
+    stride = int(max(1, np.diff(rb).max()))
+    r0, r1 = int(rb[rank]), int(rb[rank + 1])
+    lrp = rp[r0:r1 + 1] - rp[r0]
+    part = orc.spmm(r1 - r0, ncols, k, -0.7, lrp, col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]], B, 0.8,
+                    C0[r0:r1]) if r1 > r0 else np.zeros((0, ncols))
+    buf = torch.zeros((ncols, stride), dtype=torch.float64)
+    buf[:, : r1 - r0] = torch.from_numpy(np.ascontiguousarray(part.T))
+    out = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf)
+    C = np.zeros((ncols, m))
+    for d in range(world):
+        a, b = int(rb[d]), int(rb[d + 1])
+        C[:, a:b] = out[d].numpy()[:, : b - a]
+    want = orc.spmm(m, ncols, k, -0.7, rp, col, val, B, 0.8, C0).T
+    ok = bool(np.allclose(C, want, rtol=1e-12, atol=1e-12))
+    balanced = bool(np.all(np.diff(rb) >= 0) and rb[0] == 0 and rb[-1] == m)
+    result_q.put((rank, ok and balanced))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_spmm_protocol(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spmm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
