@@ -143,6 +143,15 @@ int sblas_trsv_destroy(sblas_trsv T);
  * sptrsv_v1/src/sptrsv_syncfree_cuda.h:170-282): d_b, d_x device n x rhs
  * row-major.  Pull executor; rhs == 1 is sblas_trsv_solve(T, 1, ...). */
 int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream);
+/* Out-of-core SpMV (the task pool + streams of spMV_mgpu_v2,
+ * dspmv_mgpu_v2.cu:33-441).  HOST CSR (int64 rowptr), x and y: the matrix is
+ * streamed through ngpu devices in nnz-balanced chunks of chunk_nnz, over
+ * nstreams streams per device (H2D of one chunk overlaps the kernel of the
+ * previous), so it may exceed the aggregate HBM.  y = alpha*A*x + beta*y.
+ * stats (optional, 4 doubles): seconds, H2D GB/s, chunks, devices. */
+int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const long long *rowptr,
+                   const int *col, const double *val, const double *x, double beta, double *y,
+                   int ngpu, long long chunk_nnz, int nstreams, double *stats);
 /* Multi-GPU CSR -> CSC transpose (replaces kernal_sptrans,
  * sptrans/sptrans_v1/src/sptrans_kernal.h:80-555).  HOST arrays in and out
  * (int32 rowptr as the reference).  nnz-balanced whole-row blocks, block d

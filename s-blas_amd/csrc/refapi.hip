@@ -177,10 +177,10 @@ int sblas_spMV_mgpu_v1(int m, int n, long long nnz, double *alpha, double *csrVa
                      algo_of_kernel(kernel));
 }
 
-// dspmv_mgpu_v2.cu:33-441: T = ceil(nnz/nb) nnz-chunk tasks, contiguous task
-// quotas per device (:125-126), merged like v1.  q (copy_of_workspace) only
-// caps nb here (:43); x stays resident per device instead of being re-sent
-// per task.
+// dspmv_mgpu_v2.cu:33-441: T = ceil(nnz/nb) nnz-chunk tasks taken by one host
+// thread per device and streamed over q = copy_of_workspace streams each
+// (nb capped as :43); x stays resident per device instead of being re-sent
+// per task; split rows merged like v1.
 int sblas_spMV_mgpu_v2(int m, int n, long long nnz, double *alpha, double *csrVal,
                        long long *csrRowPtr, int *csrColIndex, double *x, double *beta, double *y,
                        int ngpu, int kernel, long long nb, int copy_of_workspace)
@@ -189,22 +189,15 @@ int sblas_spMV_mgpu_v2(int m, int n, long long nnz, double *alpha, double *csrVa
     if (kernel < 1 || kernel > 3 || copy_of_workspace <= 0) return SBLAS_ERR_INVALID;
     int count;
     if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
+    // v2's task pool: nnz-balanced tasks of nb nonzeros streamed from host
+    // memory over copy_of_workspace streams per device (stream.hip)
     const double freegb = min_free_gb(ngpu);
     const long long cap = (long long)(0.8 * freegb * 1e9 / 16.0) / copy_of_workspace;
     nb = std::min(nb, cap);
     if (nb <= 0) return -1;
-    const long long T = std::max<long long>(1, (nnz + nb - 1) / nb);
-    if (T > std::numeric_limits<int>::max()) return SBLAS_ERR_INVALID;
-    const int t = (int)T;
-    std::vector<long long> si(t), ei(t);
-    std::vector<int> sr(t), er(t), sf(t);
-    sblas_partition_nnz(m, nnz, csrRowPtr, t, si.data(), ei.data(), sr.data(), er.data(), sf.data());
-    std::vector<Part> parts;
-    for (int d = 0; d < ngpu; ++d)
-        for (long long k = T * d / ngpu; k < T * (d + 1) / ngpu; ++k)
-            parts.push_back({d, sr[k], er[k], si[k], ei[k], sf[k] != 0});
-    return run_parts(parts, n, alpha, csrVal, csrRowPtr, csrColIndex, x, beta, y,
-                     algo_of_kernel(kernel));
+    (void)kernel;  // every task runs the row-split kernel
+    return sblas_spmv_ooc(m, n, nnz, *alpha, csrRowPtr, csrColIndex, csrVal, x, *beta, y, ngpu, nb,
+                          copy_of_workspace, nullptr);
 }
 
 // cusparse_mgpu_csrmm[_omp] (spmm/src/dspmm_mgpu_baseline.cu:83-524) with

@@ -161,6 +161,11 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
                 hipStream_t s);
 int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx,
                      double *cval, hipStream_t s);
+void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
+                     std::vector<int4> &longs, int &nslots);
+int launch_rowsplit_raw(const int *rowptr, const int *col, const double *val, const double *x,
+                        const RowBlock *blocks, int nblocks, const int4 *long_rows, int nlong,
+                        double *partial, double alpha, double beta, double *y, hipStream_t s);
 
 // Scoped device switch.
 struct DeviceGuard {

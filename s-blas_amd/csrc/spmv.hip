@@ -237,6 +237,30 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
     return SBLAS_OK;
 }
 
+// Row-split launch on raw device arrays (the out-of-core executor's chunks,
+// stream.hip).
+int launch_rowsplit_raw(const int *rowptr, const int *col, const double *val, const double *x,
+                        const RowBlock *blocks, int nblocks, const int4 *long_rows, int nlong,
+                        double *partial, double alpha, double beta, double *y, hipStream_t s)
+{
+    if (nblocks == 0) return SBLAS_OK;
+    if (beta != 0.0) {
+        hipLaunchKernelGGL(k_spmv_rowsplit<true>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
+                           x, blocks, alpha, beta, y, partial);
+        if (nlong)
+            hipLaunchKernelGGL(k_spmv_long_finalize<true>, dim3((nlong + 63) / 64), dim3(64), 0, s,
+                               long_rows, nlong, partial, alpha, beta, y);
+    } else {
+        hipLaunchKernelGGL(k_spmv_rowsplit<false>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
+                           x, blocks, alpha, beta, y, partial);
+        if (nlong)
+            hipLaunchKernelGGL(k_spmv_long_finalize<false>, dim3((nlong + 63) / 64), dim3(64), 0, s,
+                               long_rows, nlong, partial, alpha, beta, y);
+    }
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
 int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
                          double beta, double *y, hipStream_t s)
 {

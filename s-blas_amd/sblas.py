@@ -83,6 +83,7 @@ _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
 _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
 _sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
+_sig("sblas_spmv_ooc", _i, _i, _i, _ll, _d, _p, _p, _p, _p, _d, _p, _i, _ll, _i, _p)
 _sig("sblas_csr2csc_mgpu", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_sptrans", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
@@ -215,6 +216,22 @@ def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int
                                     ptr(x), ngpu, C.byref(ms)), "trsv_mgpu_solve")
     x = x[:n * rhs]
     return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
+
+
+def spmv_ooc(m: int, n: int, rowptr, col, val, x, alpha: float, beta: float, y, ngpu: int = 1,
+             chunk_nnz: int = 1 << 24, nstreams: int = 2):
+    """Out-of-core y = alpha*A*x + beta*y streaming host CSR through the GPUs
+    (sblas_spmv_ooc).  y (host float64) is updated in place.  Returns the
+    stats dict."""
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    ci = np.ascontiguousarray(col, np.int32)
+    v = np.ascontiguousarray(val, np.float64)
+    xx = np.ascontiguousarray(x, np.float64)
+    assert y.dtype == np.float64 and y.flags.c_contiguous
+    st = np.zeros(4)
+    check(lib.sblas_spmv_ooc(m, n, int(rp[-1]), alpha, ptr(rp), ptr(ci), ptr(v), ptr(xx), beta,
+                             ptr(y), ngpu, chunk_nnz, nstreams, ptr(st)), "spmv_ooc")
+    return {"seconds": st[0], "h2d_gbps": st[1], "chunks": int(st[2]), "devices": int(st[3])}
 
 
 def csr2csc_mgpu(m: int, n: int, rowptr, col, val, ngpu: int):

@@ -160,3 +160,26 @@ def test_reference_api(torch_cuda, sb, orc, version, ngpu):
         if version != "v2":
             y_ref_flow = orc.spmv_mgpu(version, m, n, rp, col, val, x, alpha, beta, y0, ngpu)
             assert np.all(np.abs(y - y_ref_flow) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+
+
+@pytest.mark.parametrize("chunk", [37, 1000, 20000, 1 << 30])
+@pytest.mark.parametrize("nstreams", [1, 3])
+@pytest.mark.parametrize("ngpu", [1, 2])
+@pytest.mark.parametrize("beta_zero", [False, True])
+def test_spmv_out_of_core(torch_cuda, sb, orc, chunk, nstreams, ngpu, beta_zero):
+    """Out-of-core executor: host CSR streamed in chunks; tiny
+    chunks make rows span many chunks (continuations), a 9000-nnz row spans
+    chunks and the 8192-nnz long-row path, empty rows stay beta*y0."""
+    rng = np.random.default_rng(chunk + 7 * nstreams)
+    m, n = 3000, 12000
+    rp, col, val = random_csr(rng, m, n, 30, long_rows=[(17, 9000)], empty_frac=0.2)
+    x = rng.standard_normal(n)
+    alpha, beta = orc.alpha_beta()
+    if beta_zero:
+        beta = 0.0
+    y0 = rng.standard_normal(m)
+    y = y0.copy()
+    st = sb.spmv_ooc(m, n, rp, col, val, x, alpha, beta, y, ngpu=ngpu, chunk_nnz=chunk,
+                     nstreams=nstreams)
+    assert st["chunks"] == max(1, -(-int(rp[-1]) // min(chunk, 1 << 30)))
+    check(orc, rp, col, val, x, alpha, beta, y0, y)
