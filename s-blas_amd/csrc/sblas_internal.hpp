@@ -108,6 +108,14 @@ struct SpmmPlan {
     int nsparse = 0;           // rows handled by the row-wave kernel
     long long sparse_nnz = 0;  // their nonzeros
     int *srows = nullptr;
+    // L2-slice form (few rows, tall B): A cut into S slices of W columns (W
+    // rows of B, <= 1 MiB per 64-column slab), slice-major CSR; slices dealt
+    // to XCDs by index (blockIdx % 8), partial C per XCD, then reduced.
+    int l2_S = 0, l2_W = 0;
+    int *l2_rp = nullptr;                // [S][m+1] offsets into l2_col/l2_val
+    unsigned short *l2_col = nullptr;    // column - s*W
+    double *l2_val = nullptr;
+    double *l2_part = nullptr;           // [8][m][64]
     double fill_thresh = 0.25;
     bool ready = false;
 };

@@ -24,6 +24,7 @@
 //    matrix like rail4284 has no dense blocks and stays on the row-wave
 //    kernel.
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <type_traits>
 #include <vector>
@@ -185,6 +186,149 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(
     }
 }
 
+// ---- L2-slice SpMM (few rows, tall B) -------------------------------------
+// With m small (rail4284: 4,284 rows) and B far larger than the chip's 32 MB
+// of L2 (559 MB), every nonzero's 512-B B row comes over the fabric: the
+// row kernels run at the ~7-8.6 TB/s random-row gather rate.  Here A is cut
+// into slices of W columns (W rows of B, 1 MiB at n = 64) and slice s is
+// worked only by the workgroups with blockIdx % 8 == s % 8, i.e. one XCD
+// under round-robin placement: each B slice is fetched into ONE L2 and
+// re-read there by all of that XCD's waves, which walk the slices in step.
+// Every XCD covers all m rows (each wave owns RW consecutive rows, partial
+// sums in LDS, a register run per row); the 8 XCD partials are reduced after.
+constexpr int kL2Xcd = 8;
+constexpr int kL2WgPerXcd = 128;  // 4 workgroups per CU: all resident at 106 VGPRs
+constexpr int kL2MaxRows = 32;    // rows per wave (LDS: 4 waves x RW x 64 f64)
+constexpr int kL2Batch = 16;      // B-row gathers in flight per lane
+
+__global__ __launch_bounds__(256) void k_spmm_l2slice(
+    const int *__restrict__ srp, const unsigned short *__restrict__ scol,
+    const double *__restrict__ sval, int S, int W, int m, int RW,
+    const double *__restrict__ B, long long ldb, int n, int slab, double *__restrict__ part)
+{
+    extern __shared__ double l2acc[];  // [4][RW][64]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double *acc = l2acc + (size_t)wv * RW * 64 + lane;  // acc[i * 64] = row i
+    const int xcd = blockIdx.x % kL2Xcd, wgx = blockIdx.x / kL2Xcd;
+    const int gw = wgx * 4 + wv;
+    const int rb = gw * RW, nr = min(m, rb + RW) - rb;
+    for (int i = 0; i < RW; ++i) acc[i * 64] = 0.0;
+    if (nr <= 0) return;
+    const int c = slab * 64 + lane;
+    const int cc = c < n ? c : 0;
+    double cur = 0.0;
+    int cur_row = 0;
+    // software pipeline: the next slice's row boundaries and each slice's
+    // next 64-element chunk are loaded one step ahead
+    auto load_bnd = [&](int sl) {
+        return (sl < S && lane <= nr) ? srp[(size_t)sl * (m + 1) + rb + lane] : INT_MAX;
+    };
+    int bnd_next = load_bnd(xcd);
+    for (int s = xcd; s < S; s += kL2Xcd) {
+        const int bnd = bnd_next;
+        bnd_next = load_bnd(s + kL2Xcd);
+        const int e0 = __shfl(bnd, 0, 64), e1 = __shfl(bnd, nr, 64);
+        const long long jbase = (long long)s * W;
+        int cnt_n = min(64, e1 - e0);
+        int j_n = lane < cnt_n ? (int)(jbase + scol[e0 + lane]) : 0;
+        double a_n = lane < cnt_n ? sval[e0 + lane] : 0.0;
+        for (int eb = e0; eb < e1; eb += 64) {
+            const int cnt = cnt_n;
+            const int my_j = j_n;
+            const double my_a = a_n;
+            const int ebn = eb + 64;
+            cnt_n = min(64, e1 - ebn);
+            if (cnt_n > 0) {
+                j_n = lane < cnt_n ? (int)(jbase + scol[ebn + lane]) : 0;
+                a_n = lane < cnt_n ? sval[ebn + lane] : 0.0;
+            }
+            for (int q = 0; q < cnt; q += kL2Batch) {
+                double a[kL2Batch], b[kL2Batch];
+                int row[kL2Batch];
+#pragma unroll
+                for (int u = 0; u < kL2Batch; ++u) {
+                    const int idx = q + u;
+                    const int j = __shfl(my_j, idx & 63, 64);
+                    a[u] = __shfl(my_a, idx & 63, 64);  // 0 past cnt
+                    b[u] = B[(long long)j * ldb + cc];
+                    row[u] = idx < cnt ? __popcll(__ballot(bnd <= eb + idx)) - 1 : cur_row;
+                }
+#pragma unroll
+                for (int u = 0; u < kL2Batch; ++u) {
+                    if (row[u] != cur_row) {
+                        acc[cur_row * 64] += cur;
+                        cur = 0.0;
+                        cur_row = row[u];
+                    }
+                    cur += a[u] * b[u];
+                }
+            }
+        }
+    }
+    acc[cur_row * 64] += cur;
+    double *out = part + ((size_t)xcd * m + rb) * 64 + lane;
+    for (int i = 0; i < nr; ++i) out[(size_t)i * 64] = acc[i * 64];
+}
+
+// C[:, slab] = alpha * sum_x part[x] (+ beta * C); 4 rows x 64 columns per WG
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmm_l2reduce(const double *__restrict__ part, int m, int n, int slab,
+                                                       double alpha, double beta, double *__restrict__ C,
+                                                       long long ldc)
+{
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int c = slab * 64 + lane;
+    if (r >= m || c >= n) return;
+    double s = 0.0;
+#pragma unroll
+    for (int x = 0; x < kL2Xcd; ++x) s += part[((size_t)x * m + r) * 64 + lane];
+    double *o = C + (long long)c * ldc + r;
+    *o = kBeta ? alpha * s + beta * *o : alpha * s;
+}
+
+// host: slice-major CSR of A (columns cut every W)
+static int build_l2slice(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
+                         const std::vector<double> &hval, int W)
+{
+    SpmmPlan &P = A.mm;
+    const int m = A.m;
+    const int S = (A.n + W - 1) / W;
+    std::vector<int> off((size_t)S * (m + 1) + 1, 0);
+    for (int r = 0; r < m; ++r)
+        for (int e = rp[r]; e < rp[r + 1]; ++e) off[(size_t)(hcol[e] / W) * (m + 1) + r + 1]++;
+    // exclusive prefix over (slice, row), slice-major
+    long long run = 0;
+    for (int sl = 0; sl < S; ++sl) {
+        int *o = off.data() + (size_t)sl * (m + 1);
+        o[0] = (int)run;
+        for (int r = 0; r < m; ++r) {
+            run += o[r + 1];
+            o[r + 1] = (int)run;
+        }
+    }
+    std::vector<unsigned short> scol((size_t)std::max<long long>(A.nnz, 1));
+    std::vector<double> sval((size_t)std::max<long long>(A.nnz, 1));
+    std::vector<int> next(off.begin(), off.end());
+    for (int r = 0; r < m; ++r)
+        for (int e = rp[r]; e < rp[r + 1]; ++e) {
+            const int sl = hcol[e] / W;
+            const int o = next[(size_t)sl * (m + 1) + r]++;
+            scol[(size_t)o] = (unsigned short)(hcol[e] - sl * W);
+            sval[(size_t)o] = hval[e];
+        }
+    SBLAS_HIP(hipMalloc(&P.l2_rp, sizeof(int) * (size_t)S * (m + 1)));
+    SBLAS_HIP(hipMalloc(&P.l2_col, sizeof(unsigned short) * scol.size()));
+    SBLAS_HIP(hipMalloc(&P.l2_val, sizeof(double) * sval.size()));
+    SBLAS_HIP(hipMalloc(&P.l2_part, sizeof(double) * (size_t)kL2Xcd * m * 64));
+    SBLAS_HIP(hipMemcpy(P.l2_rp, off.data(), sizeof(int) * (size_t)S * (m + 1), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(P.l2_col, scol.data(), sizeof(unsigned short) * scol.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(P.l2_val, sval.data(), sizeof(double) * sval.size(), hipMemcpyHostToDevice));
+    P.l2_S = S;
+    P.l2_W = W;
+    return SBLAS_OK;
+}
+
 int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.mm.ready) return SBLAS_OK;
@@ -243,6 +387,15 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     SBLAS_TRY(up(&P.ucol, ucol));
     SBLAS_TRY(up(&P.atile, atile));
     SBLAS_TRY(up(&P.srows, srows));
+    // L2-slice form: few rows (every XCD holds all m partial rows), B much
+    // taller than the L2s (k >= 2^17: >= 64 MiB at n = 64), no MFMA blocks.
+    // SBLAS_SPMM_L2SLICE=0/1 overrides the size rule; SBLAS_SPMM_L2W sets W.
+    const int rw = (m + kL2WgPerXcd * 4 - 1) / (kL2WgPerXcd * 4);
+    bool l2 = P.nmfma == 0 && m > 0 && rw <= kL2MaxRows && A.n >= (1 << 17);
+    if (const char *e = getenv("SBLAS_SPMM_L2SLICE")) l2 = atoi(e) != 0 && P.nmfma == 0 && m > 0 && rw <= kL2MaxRows;
+    int W = 8192;
+    if (const char *e = getenv("SBLAS_SPMM_L2W")) W = std::max(1, std::min(65536, atoi(e)));
+    if (l2) SBLAS_TRY(build_l2slice(A, rp, hcol, hval, W));
     (void)s;
     P.ready = true;
     return SBLAS_OK;
@@ -256,6 +409,10 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.ucol);
     (void)hipFree(P.atile);
     (void)hipFree(P.srows);
+    (void)hipFree(P.l2_rp);
+    (void)hipFree(P.l2_col);
+    (void)hipFree(P.l2_val);
+    (void)hipFree(P.l2_part);
     A.mm = SpmmPlan{};
 }
 
@@ -308,6 +465,23 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     }
     const SpmmPlan &P = A.mm;
     const int nslab = (n + 63) / 64;
+    if (P.ready && P.l2_S > 0) {
+        const int rw = (A.m + kL2WgPerXcd * 4 - 1) / (kL2WgPerXcd * 4);
+        for (int sl = 0; sl < nslab; ++sl) {
+            hipLaunchKernelGGL(k_spmm_l2slice, dim3(kL2Xcd * kL2WgPerXcd), dim3(256),
+                               sizeof(double) * 4 * 64 * (size_t)rw, s, P.l2_rp, P.l2_col,
+                               P.l2_val, P.l2_S, P.l2_W, A.m, rw, Brow, ldr, n, sl, P.l2_part);
+            const unsigned nb = (unsigned)((A.m + 3) / 4);
+            if (beta != 0.0)
+                hipLaunchKernelGGL(k_spmm_l2reduce<true>, dim3(nb), dim3(256), 0, s, P.l2_part, A.m, n, sl, alpha,
+                                   beta, C, (long long)ldc);
+            else
+                hipLaunchKernelGGL(k_spmm_l2reduce<false>, dim3(nb), dim3(256), 0, s, P.l2_part, A.m, n, sl, alpha,
+                                   beta, C, (long long)ldc);
+        }
+        SBLAS_HIP(hipGetLastError());
+        return SBLAS_OK;
+    }
     // rows of sparse blocks (all rows when no plan / no dense block)
     const int nrows = P.ready ? P.nsparse : A.m;
     const int *rows = P.ready ? P.srows : nullptr;

@@ -48,4 +48,13 @@ if [[ $STEP == all || $STEP == prof ]]; then
   done
   ls $O/pmc_*.json
 fi
+if [[ $STEP == prof2 ]]; then
+  # kernel-trace summaries of the non-SpMV rows (SpTRSV/SpTRSM, SpMM, transpose, out-of-core)
+  run prof2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_trsv -o run --output-format csv -- python s-blas_amd/tools/bench_sptrsv.py --rhs 8 --no-cpu-baseline --steps 3 > $O/prof_trsv.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_spmm -o run --output-format csv -- python s-blas_amd/tools/bench_spmm.py > $O/prof_spmm.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr -o run --output-format csv -- python s-blas_amd/tools/bench_transpose.py --mgpu 2 > $O/prof_tr.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_ooc -o run --output-format csv -- python s-blas_amd/tools/bench_ooc.py --reps 1 --chunks 16777216 --streams 2 > $O/prof_ooc.log 2>&1 || exit 1
+  ls $O/prof_trsv $O/prof_spmm $O/prof_tr $O/prof_ooc
+fi
 echo "[$(date +%T)] session done"

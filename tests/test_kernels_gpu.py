@@ -33,15 +33,20 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1"])
+@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     """Both row kernels: wave per row and workgroup per row (split over its
-    nonzeros; picked automatically for long rows)."""
+    nonzeros; picked automatically for long rows) and the L2-slice form
+    (forced: "l2" = 3 slices of 2048 columns, "l2w" = 79 slices of 64)."""
     torch = torch_cuda
-    if splitk != "auto":
+    if splitk in ("0", "1"):
         monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
+    if splitk.startswith("l2"):
+        monkeypatch.setenv("SBLAS_SPMM_L2SLICE", "1")
+        if splitk == "l2w":
+            monkeypatch.setenv("SBLAS_SPMM_L2W", "64")
     rng = np.random.default_rng(ncols + 10 * layout)
     m, k = 700, 5000
     rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
