@@ -148,7 +148,9 @@ int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, 
  * streamed through ngpu devices in nnz-balanced chunks of chunk_nnz, over
  * nstreams streams per device (H2D of one chunk overlaps the kernel of the
  * previous), so it may exceed the aggregate HBM.  y = alpha*A*x + beta*y.
- * stats (optional, 4 doubles): seconds, H2D GB/s, chunks, devices. */
+ * stats (optional, 6 doubles): total seconds, H2D GB/s of the streaming
+ * phase, chunks, devices, seconds pinning the caller's col/val, seconds
+ * (re)allocating the per-device pool (0 once warm). */
 int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const long long *rowptr,
                    const int *col, const double *val, const double *x, double beta, double *y,
                    int ngpu, long long chunk_nnz, int nstreams, double *stats);

@@ -14,11 +14,14 @@
 //     rowptr is rebased to int32 on the host into pinned staging, and the
 //     row-split plan of the chunk is built there too;
 //   * x is uploaded once per GPU (v2 re-sends the full x with every task);
+//   * streams, device buffers and pinned staging persist per device across
+//     calls (a call only grows them), so repeated calls pay only the DMA;
 //   * every chunk returns its rows of y; a chunk that starts inside a row
 //     (continuation) computes that row's partial with y0 zeroed and the
 //     partial is added after all chunks are merged -- the v1 fix-up
 //     (dspmv_mgpu_v1.cu:235-248) generalised to rows spanning many chunks.
 #include <atomic>
+#include <mutex>
 #include <cstring>
 #include <vector>
 
@@ -51,7 +54,38 @@ struct Slot {
     int4 *h_long = nullptr;
     double *h_y = nullptr;
     int chunk = -1;  // chunk whose result is in flight (-1: none)
+    int cap_rows = 0;
+    long long cap_nnz = 0;
 };
+
+// Per-device resources kept across calls (streams, events, device buffers
+// and pinned staging are costly to create; a call only grows them).
+struct DevPool {
+    std::mutex mu;
+    double *d_x = nullptr;
+    int cap_x = 0;
+    std::vector<Slot> slots;
+};
+DevPool g_pool[64];
+
+void free_slot(Slot &q)
+{
+    (void)hipFree(q.d_rowptr);
+    (void)hipFree(q.d_col);
+    (void)hipFree(q.d_val);
+    (void)hipFree(q.d_y);
+    (void)hipFree(q.d_partial);
+    (void)hipFree(q.d_blocks);
+    (void)hipFree(q.d_long);
+    (void)hipHostFree(q.h_rowptr);
+    (void)hipHostFree(q.h_blocks);
+    (void)hipHostFree(q.h_long);
+    (void)hipHostFree(q.h_y);
+    Slot keep;
+    keep.s = q.s;
+    keep.done = q.done;
+    q = keep;
+}
 
 }  // namespace
 
@@ -83,9 +117,8 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
         max_rows = std::max(max_rows, er[t] - sr[t] + 1);
         max_nnz = std::max(max_nnz, ei[t] - si[t] + 1);
     }
-    const int max_blocks = max_rows + (int)(max_nnz / kRsLongChunk) + 2;
-    const int max_slots = max_rows + (int)(max_nnz / kRsLongChunk) + 2;
     // pin the caller's arrays in place for the DMA
+    const double t_reg0 = sblas_get_time();
     bool reg_col = false, reg_val = false;
     if (nnz) {
         hipError_t e = hipHostRegister((void *)col, sizeof(int) * nnz, hipHostRegisterDefault);
@@ -95,8 +128,10 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
         reg_val = e == hipSuccess;
         if (e != hipSuccess) (void)hipGetLastError();
     }
+    const double t_reg = sblas_get_time() - t_reg0;
     std::vector<double> carry(T, 0.0);
     std::atomic<int> next{0};
+    std::atomic<long long> setup_ns{0};
     std::atomic<int> status{SBLAS_OK};
     std::atomic<long long> h2d_bytes{0};
     const int ndev = std::min(ngpu, count);
@@ -107,8 +142,10 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
 #ifdef _OPENMP
         dev = omp_get_thread_num();
 #endif
-        std::vector<Slot> slots(nstreams);
-        double *d_x = nullptr;
+        DevPool &pool = g_pool[dev & 63];
+        std::lock_guard<std::mutex> lock(pool.mu);
+        if ((int)pool.slots.size() < nstreams) pool.slots.resize(nstreams);
+        Slot *slots = pool.slots.data();
         auto fail = [&](int st) {
             int ok = SBLAS_OK;
             status.compare_exchange_strong(ok, st);
@@ -136,26 +173,49 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
             q.chunk = -1;
         };
         if (hipSetDevice(dev) == hipSuccess) {
-            bool ok = check(hipMalloc(&d_x, sizeof(double) * std::max(n, 1)), "malloc x") &&
-                      (n == 0 || check(hipMemcpy(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice), "x H2D"));
-            for (auto &q : slots) {
-                if (!ok) break;
-                ok = check(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking), "stream") &&
-                     check(hipEventCreateWithFlags(&q.done, hipEventDisableTiming), "event") &&
-                     check(hipMalloc(&q.d_rowptr, sizeof(int) * (max_rows + 1)), "malloc") &&
-                     check(hipMalloc(&q.d_col, sizeof(int) * (max_nnz + 8)), "malloc") &&
-                     check(hipMalloc(&q.d_val, sizeof(double) * (max_nnz + 8)), "malloc") &&
-                     check(hipMemset(q.d_col, 0, sizeof(int) * (max_nnz + 8)), "memset") &&
-                     check(hipMemset(q.d_val, 0, sizeof(double) * (max_nnz + 8)), "memset") &&
-                     check(hipMalloc(&q.d_y, sizeof(double) * max_rows), "malloc") &&
-                     check(hipMalloc(&q.d_partial, sizeof(double) * max_slots), "malloc") &&
-                     check(hipMalloc(&q.d_blocks, sizeof(RowBlock) * max_blocks), "malloc") &&
-                     check(hipMalloc(&q.d_long, sizeof(int4) * max_rows), "malloc") &&
-                     check(hipHostMalloc(&q.h_rowptr, sizeof(int) * (max_rows + 1), hipHostMallocDefault), "pinned") &&
-                     check(hipHostMalloc(&q.h_blocks, sizeof(RowBlock) * max_blocks, hipHostMallocDefault), "pinned") &&
-                     check(hipHostMalloc(&q.h_long, sizeof(int4) * max_rows, hipHostMallocDefault), "pinned") &&
-                     check(hipHostMalloc(&q.h_y, sizeof(double) * max_rows, hipHostMallocDefault), "pinned");
+            const double ts = sblas_get_time();
+            bool ok = true;
+            if (pool.cap_x < n) {
+                (void)hipFree(pool.d_x);
+                pool.d_x = nullptr;
+                pool.cap_x = 0;
+                ok = check(hipMalloc(&pool.d_x, sizeof(double) * std::max(n, 1)), "malloc x");
+                if (ok) pool.cap_x = n;
             }
+            double *d_x = pool.d_x;
+            ok = ok && (n == 0 || check(hipMemcpy(d_x, x, sizeof(double) * n, hipMemcpyHostToDevice), "x H2D"));
+            for (int qi = 0; qi < nstreams && ok; ++qi) {
+                Slot &q = slots[qi];
+                q.chunk = -1;
+                if (!q.s)
+                    ok = check(hipStreamCreateWithFlags(&q.s, hipStreamNonBlocking), "stream") &&
+                         check(hipEventCreateWithFlags(&q.done, hipEventDisableTiming), "event");
+                if (!ok || (q.cap_rows >= max_rows && q.cap_nnz >= max_nnz)) continue;
+                free_slot(q);
+                const int cr = std::max(max_rows, q.cap_rows);
+                const long long cn = std::max(max_nnz, q.cap_nnz);
+                const int cb = cr + (int)(cn / kRsLongChunk) + 2;
+                ok = check(hipMalloc(&q.d_rowptr, sizeof(int) * (cr + 1)), "malloc") &&
+                     check(hipMalloc(&q.d_col, sizeof(int) * (cn + 8)), "malloc") &&
+                     check(hipMalloc(&q.d_val, sizeof(double) * (cn + 8)), "malloc") &&
+                     check(hipMemset(q.d_col, 0, sizeof(int) * (cn + 8)), "memset") &&
+                     check(hipMemset(q.d_val, 0, sizeof(double) * (cn + 8)), "memset") &&
+                     check(hipMalloc(&q.d_y, sizeof(double) * cr), "malloc") &&
+                     check(hipMalloc(&q.d_partial, sizeof(double) * cb), "malloc") &&
+                     check(hipMalloc(&q.d_blocks, sizeof(RowBlock) * cb), "malloc") &&
+                     check(hipMalloc(&q.d_long, sizeof(int4) * cr), "malloc") &&
+                     check(hipHostMalloc(&q.h_rowptr, sizeof(int) * (cr + 1), hipHostMallocDefault), "pinned") &&
+                     check(hipHostMalloc(&q.h_blocks, sizeof(RowBlock) * cb, hipHostMallocDefault), "pinned") &&
+                     check(hipHostMalloc(&q.h_long, sizeof(int4) * cr, hipHostMallocDefault), "pinned") &&
+                     check(hipHostMalloc(&q.h_y, sizeof(double) * cr, hipHostMallocDefault), "pinned");
+                if (ok) {
+                    q.cap_rows = cr;
+                    q.cap_nnz = cn;
+                } else {
+                    free_slot(q);
+                }
+            }
+            setup_ns += (long long)((sblas_get_time() - ts) * 1e9);
             std::vector<RowBlock> blocks;
             std::vector<int4> longs;
             int k = 0;
@@ -205,27 +265,12 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
                 q.chunk = t;
                 h2d_bytes += (long long)cn * 12 + 4LL * (dm + 1) + (beta != 0.0 ? 8LL * dm : 0);
             }
-            for (auto &q : slots) merge(q);
+            for (int qi = 0; qi < nstreams; ++qi) merge(slots[qi]);
         } else {
             fail(SBLAS_ERR_HIP);
         }
-        for (auto &q : slots) {
-            if (q.s) (void)hipStreamSynchronize(q.s);
-            (void)hipFree(q.d_rowptr);
-            (void)hipFree(q.d_col);
-            (void)hipFree(q.d_val);
-            (void)hipFree(q.d_y);
-            (void)hipFree(q.d_partial);
-            (void)hipFree(q.d_blocks);
-            (void)hipFree(q.d_long);
-            (void)hipHostFree(q.h_rowptr);
-            (void)hipHostFree(q.h_blocks);
-            (void)hipHostFree(q.h_long);
-            (void)hipHostFree(q.h_y);
-            if (q.done) (void)hipEventDestroy(q.done);
-            if (q.s) (void)hipStreamDestroy(q.s);
-        }
-        (void)hipFree(d_x);
+        for (int qi = 0; qi < nstreams; ++qi)
+            if (slots[qi].s) (void)hipStreamSynchronize(slots[qi].s);
     }
     t_kernels_end = sblas_get_time();
     if (reg_col) (void)hipHostUnregister((void *)col);
@@ -233,12 +278,16 @@ extern "C" int sblas_spmv_ooc(int m, int n, long long nnz, double alpha, const l
     if (status.load() != SBLAS_OK) return status.load();
     for (int t = 0; t < T; ++t)
         if (chunks[t].cont) y[chunks[t].r0] += carry[t];
-    if (stats) {  // {seconds, H2D GB/s, chunks, devices}
+    if (stats) {  // {seconds, H2D GB/s of the streaming phase, chunks, devices, pin s, setup s}
         const double sec = t_kernels_end - t_start;
+        const double setup = (double)setup_ns.load() / 1e9 / std::max(ndev, 1);
+        const double stream_s = std::max(1e-9, sec - t_reg - setup);
         stats[0] = sec;
-        stats[1] = sec > 0 ? (double)h2d_bytes.load() / sec / 1e9 : 0.0;
+        stats[1] = (double)h2d_bytes.load() / stream_s / 1e9;
         stats[2] = T;
         stats[3] = ndev;
+        stats[4] = t_reg;
+        stats[5] = setup;
     }
     return SBLAS_OK;
 }

@@ -228,10 +228,11 @@ def spmv_ooc(m: int, n: int, rowptr, col, val, x, alpha: float, beta: float, y, 
     v = np.ascontiguousarray(val, np.float64)
     xx = np.ascontiguousarray(x, np.float64)
     assert y.dtype == np.float64 and y.flags.c_contiguous
-    st = np.zeros(4)
+    st = np.zeros(6)
     check(lib.sblas_spmv_ooc(m, n, int(rp[-1]), alpha, ptr(rp), ptr(ci), ptr(v), ptr(xx), beta,
                              ptr(y), ngpu, chunk_nnz, nstreams, ptr(st)), "spmv_ooc")
-    return {"seconds": st[0], "h2d_gbps": st[1], "chunks": int(st[2]), "devices": int(st[3])}
+    return {"seconds": st[0], "h2d_gbps": st[1], "chunks": int(st[2]), "devices": int(st[3]),
+            "pin_seconds": st[4], "setup_seconds": st[5]}
 
 
 def csr2csc_mgpu(m: int, n: int, rowptr, col, val, ngpu: int):

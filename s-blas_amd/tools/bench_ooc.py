@@ -46,6 +46,8 @@ def main():
             res.append({"chunk_nnz": ch, "streams": q, "ms": round(best["seconds"] * 1e3, 2),
                         "gflops": round(2.0 * nnz / best["seconds"] / 1e9, 2),
                         "h2d_gbps": round(best["h2d_gbps"], 1), "chunks": best["chunks"],
+                        "pin_ms": round(best["pin_seconds"] * 1e3, 2),
+                        "setup_ms": round(best["setup_seconds"] * 1e3, 2),
                         "bitwise_same_as_first": same})
     print(json.dumps({"metric": "out-of-core fp64 SpMV (host-resident config-2 matrix)", "nnz": nnz,
                       "n": n, "ngpu": args.ngpu, "runs": res}), flush=True)
