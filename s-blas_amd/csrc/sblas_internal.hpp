@@ -168,7 +168,7 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
                 int ldb, int b_layout, double beta, double *C, int ldc,
                 hipStream_t s);
 int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx,
-                     double *cval, hipStream_t s);
+                     double *cval, hipStream_t s, int *colidx = nullptr);
 void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
                      std::vector<int4> &longs, int &nslots);
 int launch_rowsplit_raw(const int *rowptr, const int *col, const double *val, const double *x,

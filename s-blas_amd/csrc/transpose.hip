@@ -227,7 +227,8 @@ struct TransposeScratch {
 };
 static thread_local TransposeScratch g_tscratch[64];
 
-int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cval, hipStream_t s)
+int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cval, hipStream_t s,
+                     int *colidx)
 {
     const long long nnz = A.nnz;
     const int n = A.n, m = A.m;
@@ -285,6 +286,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     }
     hipLaunchKernelGGL(k_colptr_sorted, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, kin, nnz, n,
                        colptr);
+    if (colidx)  // column of every CSC entry (the sorted keys)
+        SBLAS_HIP(hipMemcpyAsync(colidx, kin, sizeof(int) * (size_t)nnz, hipMemcpyDeviceToDevice, s));
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;
 }
@@ -293,8 +296,9 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
 // sptrans/sptrans_v1/src/sptrans_kernal.h:80-555) -------------------------
 // Rows are split into g nnz-balanced blocks of whole rows; block d is
 // transposed on device d % count by the single-device path above (stable:
-// rows ascend within a column).  The pieces then travel to device 0 (peer DMA
-// over xGMI) and one element-parallel kernel composes them: block d's column
+// rows ascend within a column; its sorted keys give every entry's column).
+// The pieces then travel to device 0 (peer DMA over xGMI) and one
+// element-parallel kernel composes them: block d's column
 // c lands after blocks 0..d-1's entries of c, so the result is the global
 // stable transpose, bit for bit.  (The reference's compose leaves row indices
 // block-local, a quirk not inherited.)
@@ -316,23 +320,17 @@ __global__ void k_compose_ptr(const int *__restrict__ ptrs, int g, int n, int *_
 
 __global__ void k_compose_val(const int *__restrict__ ptrs, const int *__restrict__ base,
                               const long long *__restrict__ start, const int *__restrict__ row0,
-                              int g, int n, long long nnz, const int *__restrict__ rid_cat,
-                              const double *__restrict__ val_cat, int *__restrict__ rowidx,
-                              double *__restrict__ cval)
+                              int g, int n, long long nnz, const int *__restrict__ key_cat,
+                              const int *__restrict__ rid_cat, const double *__restrict__ val_cat,
+                              int *__restrict__ rowidx, double *__restrict__ cval)
 {
     const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= nnz) return;
     int d = 0;
     while (d + 1 < g && start[d + 1] <= p) ++d;
     const int e = (int)(p - start[d]);
-    const int *cp = ptrs + (size_t)d * (n + 1);
-    int lo = 0, hi = n - 1;  // column c: cp[c] <= e < cp[c+1]
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (cp[mid] <= e) lo = mid;
-        else hi = mid - 1;
-    }
-    const int dst = base[(size_t)d * n + lo] + (e - cp[lo]);
+    const int c = key_cat[p];  // column of this entry (block-local CSC order)
+    const int dst = base[(size_t)d * n + c] + (e - ptrs[(size_t)d * (n + 1) + c]);
     rowidx[dst] = rid_cat[p] + row0[d];
     cval[dst] = val_cat[p];
 }
@@ -366,7 +364,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
     struct Blk {
         int phys = 0;
         sblas_csr_s A;
-        int *cp = nullptr, *ri = nullptr;
+        int *cp = nullptr, *ri = nullptr, *ck = nullptr;
         double *cv = nullptr;
         hipStream_t s = nullptr;
     };
@@ -375,7 +373,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
     // in order (they share that device's transpose scratch)
     std::vector<hipStream_t> streams((size_t)std::min(count, g), nullptr);
     int *h_ptrs = nullptr, *h_base = nullptr, *h_rid = nullptr, *h_row0 = nullptr, *h_cp = nullptr,
-        *h_ri = nullptr;
+        *h_ri = nullptr, *h_key = nullptr;
     double *h_val = nullptr, *h_cv = nullptr;
     long long *h_start = nullptr;
     hipStream_t s0 = nullptr;
@@ -388,6 +386,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
             (void)hipFree(b.cp);
             (void)hipFree(b.ri);
             (void)hipFree(b.cv);
+            (void)hipFree(b.ck);
         }
         for (size_t p = 0; p < streams.size(); ++p)
             if (streams[p]) {
@@ -396,7 +395,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
             }
         DeviceGuard gd(0);
         for (void *p : {(void *)h_ptrs, (void *)h_base, (void *)h_rid, (void *)h_row0, (void *)h_cp,
-                        (void *)h_ri, (void *)h_val, (void *)h_cv, (void *)h_start})
+                        (void *)h_ri, (void *)h_val, (void *)h_cv, (void *)h_start, (void *)h_key})
             (void)hipFree(p);
         if (s0) (void)hipStreamDestroy(s0);
     };
@@ -432,6 +431,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
         TG(hipMalloc(&b.cp, sizeof(int) * ((size_t)n + 1)));
         TG(hipMalloc(&b.ri, sizeof(int) * std::max(e1 - e0, 1)));
         TG(hipMalloc(&b.cv, sizeof(double) * std::max(e1 - e0, 1)));
+        TG(hipMalloc(&b.ck, sizeof(int) * std::max(e1 - e0, 1)));
         TG(hipMemcpy(b.A.rowptr, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
         if (e1 > e0) {
             TG(hipMemcpy(b.A.col, col + e0, sizeof(int) * (e1 - e0), hipMemcpyHostToDevice));
@@ -445,6 +445,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
         TG(hipMalloc(&h_base, sizeof(int) * std::max<size_t>((size_t)g * n, 1)));
         TG(hipMalloc(&h_rid, sizeof(int) * std::max(nnz, 1)));
         TG(hipMalloc(&h_val, sizeof(double) * std::max(nnz, 1)));
+        TG(hipMalloc(&h_key, sizeof(int) * std::max(nnz, 1)));
         TG(hipMalloc(&h_row0, sizeof(int) * g));
         TG(hipMalloc(&h_start, sizeof(long long) * (g + 1)));
         TG(hipMalloc(&h_cp, sizeof(int) * ((size_t)n + 1)));
@@ -462,7 +463,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
     for (int d = 0; d < g; ++d) {
         Blk &b = B[d];
         DeviceGuard gd(b.phys);
-        const int st = launch_transpose(b.A, b.cp, b.ri, b.cv, b.s);
+        const int st = launch_transpose(b.A, b.cp, b.ri, b.cv, b.s, b.ck);
         if (st != SBLAS_OK) {
             cleanup();
             return st;
@@ -482,6 +483,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
             TG(hipMemcpyPeerAsync(h_ptrs + (size_t)d * (n + 1), 0, b.cp, b.phys, sizeof(int) * ((size_t)n + 1), s0));
             if (k) {
                 TG(hipMemcpyPeerAsync(h_rid + start[d], 0, b.ri, b.phys, sizeof(int) * k, s0));
+                TG(hipMemcpyPeerAsync(h_key + start[d], 0, b.ck, b.phys, sizeof(int) * k, s0));
                 TG(hipMemcpyPeerAsync(h_val + start[d], 0, b.cv, b.phys, sizeof(double) * k, s0));
             }
         }
@@ -489,7 +491,7 @@ extern "C" int sblas_csr2csc_mgpu(int m, int n, int nnz, int ngpu, const int *ro
                            h_base);
         if (nnz && n > 0)
             hipLaunchKernelGGL(k_compose_val, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s0, h_ptrs,
-                               h_base, h_start, h_row0, g, n, (long long)nnz, h_rid, h_val, h_ri, h_cv);
+                               h_base, h_start, h_row0, g, n, (long long)nnz, h_key, h_rid, h_val, h_ri, h_cv);
         TG(hipGetLastError());
         TG(hipStreamSynchronize(s0));
     }
