@@ -7,14 +7,16 @@ distinct uniform-random sorted columns (seed 42), values U[0,1), x U[0,1)
 (seed 43), y0 = 0, alpha/beta = the test_spmv constants (glibc rand(),
 0.8401877172 / 0.3943829268).  One step = one y = alpha*A*x + beta*y over
 the whole matrix with every input already resident in HBM; at N > 1 the
-matrix is split by nnz over the ranks (x replicated) and a step also
-includes the RCCL allgather of the y slices plus their device-side merge
-(strong scaling: the same matrix at every N).  Timing is cold-cache by
-default: at N = 8 a rank's slice (~67 MB) would otherwise
-sit in the 256 MB Infinity Cache between back-to-back steps; the warm number
-is reported beside it.
+rows are dealt to the ranks in equal cyclic chunks (x replicated) and a step
+also includes the RCCL allgather of the y slices plus their device-side
+placement (strong scaling: the same matrix at every N).  Timing follows the
+bench contract (K back-to-back steps between barriers); the cold-cache
+number (a 1 GiB scrub before each step, so that at N = 8 a
+rank's ~67 MB slice cannot sit in the 256 MB Infinity Cache) is reported
+beside it under `cold`.
 
-  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5] [--cache cold|warm]
+  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5] [--cache warm|cold]
+                  [--partition cyclic|nnz]
 
 Default kernel: `panel` = the row-split kernel run over XCD-affine column
 panels (x slice ~4 MiB per panel, panel p's row blocks on workgroups with
@@ -114,11 +116,16 @@ def main() -> int:
     ap.add_argument("--check", action="store_true",
                     help="after timing, verify the assembled y of one fresh step against the "
                          "oracle (rank 0; small n only)")
-    ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
-                    help="cold (default, SURVEY M1-cache): a 1 GiB scrub before every timed step "
-                         "evicts the 256 MB Infinity Cache and the L2s, each step is bracketed "
-                         "by its own barrier + synchronize; warm: K back-to-back steps.  The other "
-                         "mode is always measured too and reported under `warm`/`cold`.")
+    ap.add_argument("--cache", choices=["cold", "warm"], default="warm",
+                    help="warm (default, the bench contract): K back-to-back steps bracketed by "
+                         "one barrier + synchronize on each side; cold (SURVEY M1-cache): a 1 GiB "
+                         "scrub before every timed step evicts the 256 MB Infinity Cache and the "
+                         "L2s, each step bracketed by its own barrier + synchronize.  The other "
+                         "mode is always measured too and reported under `cold`/`warm`.")
+    ap.add_argument("--partition", choices=["cyclic", "nnz"], default="cyclic",
+                    help="N > 1 row distribution: cyclic equal-row chunks (default; no padding, "
+                         "whole rows) or one nnz-balanced range per rank (spMV_mgpu_v1's split, "
+                         "with split-row carries; always used with --exchange allreduce)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -149,24 +156,38 @@ def main() -> int:
     n = args.nrows
     rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
     nnz = int(rowptr[-1])
-    plan = sblas_dist.make_plan(rowptr, n, world)
-    r0, r1, i0, i1, _ = plan.local(rank)
+    prefix = args.cols == "prefix"
     t_gen = time.perf_counter()
-    col_rows, val_rows = sblas.gen_synth_rows(n, rowptr, r0, r1, args.heavy, args.light,
-                                              prefix=args.cols == "prefix", seed=42)
-    off = i0 - int(rowptr[r0])
-    col = np.ascontiguousarray(col_rows[off:off + (i1 - i0)])
-    val = np.ascontiguousarray(val_rows[off:off + (i1 - i0)])
-    t_gen = time.perf_counter() - t_gen
+    if args.partition == "cyclic" and args.exchange == "allgather":
+        plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
+        lrp, col, val = sblas_dist.cyclic_local_csr(
+            rowptr, plan, rank,
+            lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, args.heavy, args.light,
+                                              prefix=prefix, seed=42))
+        t_gen = time.perf_counter() - t_gen
+        op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
+        local_nnz = int(lrp[-1])
+        partition = f"cyclic row chunks ({plan.chunk_rows} rows, {plan.nchunks} chunks)"
+    else:
+        plan = sblas_dist.make_plan(rowptr, n, world)
+        r0, r1, i0, i1, _ = plan.local(rank)
+        col_rows, val_rows = sblas.gen_synth_rows(n, rowptr, r0, r1, args.heavy, args.light,
+                                                  prefix=prefix, seed=42)
+        off = i0 - int(rowptr[r0])
+        col = np.ascontiguousarray(col_rows[off:off + (i1 - i0)])
+        val = np.ascontiguousarray(val_rows[off:off + (i1 - i0)])
+        t_gen = time.perf_counter() - t_gen
+        op = sblas_dist.DistSpMV(plan, rank, dev_idx, rowptr, col, val, algo, torch, dist,
+                                 args.exchange)
+        local_nnz = i1 - i0
+        partition = "nnz-balanced (spMV_mgpu_v1)"
     x_h = sblas.gen_vector(n, 43)
     x = torch.from_numpy(x_h).to(dev)
 
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
-    op = sblas_dist.DistSpMV(plan, rank, dev_idx, rowptr, col, val, algo, torch, dist,
-                             args.exchange)
     local_bytes = op.A.algorithmic_bytes(BETA != 0.0)
-    local_flops = 2.0 * (i1 - i0)
+    local_flops = 2.0 * local_nnz
     torch.cuda.synchronize()
 
     def step(ev=None):
@@ -277,7 +298,7 @@ def main() -> int:
                              f"nnz else {args.light}, {args.cols} sorted cols (seed 42), "
                              f"y=alpha*A*x+beta*y, {args.algo} kernel"),
                 "n": n, "nnz": nnz, "algo": args.algo,
-                "partition": "nnz-balanced (spMV_mgpu_v1)" if world > 1 else "single GPU",
+                "partition": partition if world > 1 else "single GPU",
                 "exchange": args.exchange if world > 1 else "none",
             },
             "roofline": {

@@ -190,6 +190,15 @@ int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
                           const int *d_meta, double *d_y, int self,
                           double *d_y_local, void *stream);
 
+/* y assembly for the cyclic row-chunk distribution (whole rows, no split
+ * rows): chunk j = rows [j*chunk_rows, ...) is held by partition j % g at its
+ * local rows (j / g)*chunk_rows + ..., partition r's slice starting at
+ * d_gathered + r*stride.  Writes all m rows of d_y.  Replaces the
+ * reference's host-side y copy-back (dspmv_mgpu_v1.cu:224-248) when the rows
+ * are dealt cyclically; stride must hold ceil(ceil(m/chunk_rows)/g) chunks. */
+int sblas_assemble_cyclic(const double *d_gathered, int g, long long stride,
+                          long long chunk_rows, long long m, double *d_y, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Host utilities (no GPU needed). */
 /* Matrix-Market: mode 0 = full mmio_data semantics (symmetric expansion,

@@ -43,9 +43,39 @@ __global__ void k_assemble_carry(const double *__restrict__ gathered, int g, lon
     }
 }
 
+// Cyclic row-chunk distribution (sblas_dist.CyclicPlan): chunk j = rows
+// [j*R, min((j+1)*R, m)) lives on rank j % g at local rows (j / g)*R + ...;
+// every rank owns whole rows, so there is nothing to carry.  One thread per
+// GLOBAL row: y is written in order and each chunk is read contiguously.
+__global__ void k_assemble_cyclic(const double *__restrict__ gathered, int g, long long stride,
+                                  long long R, long long m, double *__restrict__ y)
+{
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const long long j = r / R;
+    const int d = (int)(j % g);
+    const long long k = (j / g) * R + (r - j * R);
+    y[r] = gathered[(long long)d * stride + k];
+}
+
 }  // namespace sblas
 
 using namespace sblas;
+
+extern "C" int sblas_assemble_cyclic(const double *d_gathered, int g, long long stride,
+                                     long long chunk_rows, long long m, double *d_y, void *stream)
+{
+    if (g <= 0 || stride < 0 || chunk_rows <= 0 || m < 0 || !d_gathered || !d_y)
+        return SBLAS_ERR_INVALID;
+    // every rank's local rows must fit its slice: ceil(nchunks / g) chunks
+    const long long nchunks = (m + chunk_rows - 1) / chunk_rows;
+    if (((nchunks + g - 1) / g) * chunk_rows > stride) return SBLAS_ERR_INVALID;
+    if (m == 0) return SBLAS_OK;
+    hipLaunchKernelGGL(k_assemble_cyclic, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_gathered, g, stride, chunk_rows, m, d_y);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
 
 extern "C" int sblas_assemble_slices(const double *d_gathered, int g, long long stride,
                                      const int *d_meta, double *d_y, int self,

@@ -120,6 +120,53 @@ struct SpmmPlan {
     bool ready = false;
 };
 
+// Column-sorted XCD-group plan (algo 5, xsort.hip).  Columns are cut into
+// G = 8q groups of Wg <= 2^18 columns (XCD k serves groups [kq, (k+1)q)), rows
+// into ranges of <= kXsRows rows.  Block (range i, group g) holds the range's
+// entries of group g sorted by (column, row) as packed keys
+// (col - g*Wg) << 14 | (row - row0) plus values, so the lanes of one gather
+// instruction share x lines.  A narrow range is one work item (one
+// workgroup walks all groups, XCD-staggered, and writes y); a wide range is G
+// items, one per group, each writing an alpha-free partial that a reduce
+// pass adds in group order.
+struct XsRange {
+    int row0;
+    int nrows;
+    int wide;
+    int pad;
+    long long pbase;  // wide: offset of the range's [G][nrows] partials
+};
+
+struct XsArgs {
+    const XsRange *ranges;
+    const long long *blk;   // [nranges*G + 1] block offsets
+    const uint32_t *key;
+    const double *val;
+    const int *qitems;      // [8][qstride] items (range << 8 | group + 1; 0 = all)
+    int *qhead;             // [8] claim counters, zeroed per launch
+    double *partial;
+    int qlen[8];
+    int qstride;
+    int G, q, Wg;
+    int use_xcc;
+};
+
+struct XsPlan {
+    int G = 0, q = 0, Wg = 0;
+    int nranges = 0, nwide = 0, nitems = 0, grid = 0;
+    XsRange *ranges = nullptr;
+    int *wide = nullptr;         // [nwide] range ids
+    long long *blk = nullptr;
+    uint32_t *key = nullptr;
+    double *val = nullptr;
+    int *qitems = nullptr;
+    int *qhead = nullptr;
+    double *partial = nullptr;
+    int qlen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int qstride = 0;
+    bool ready = false;
+};
+
 struct RsPlan {
     int nblocks = 0;
     RowBlock *blocks = nullptr;
@@ -143,6 +190,7 @@ struct sblas_csr_s {
     sblas::Csr5Plan c5;
     sblas::PanelPlan pn;
     sblas::SpmmPlan mm;
+    sblas::XsPlan xs;
     std::vector<int> h_rowptr;  // host copy (analysis)
 };
 
@@ -161,6 +209,11 @@ int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x,
                       double beta, double *y, hipStream_t s);
 int build_panel_plan(sblas_csr_s &A, hipStream_t s);
 int scan_inclusive(int *a, long long len, int *scratch, hipStream_t s);
+
+int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x,
+                      double beta, double *y, hipStream_t s);
+int build_xsort_plan(sblas_csr_s &A, hipStream_t s);
+void free_xsort_plan(sblas_csr_s &A);
 
 int build_spmm_plan(sblas_csr_s &A, hipStream_t s);
 void free_spmm_plan(sblas_csr_s &A);

@@ -87,6 +87,7 @@ _sig("sblas_spmv_ooc", _i, _i, _i, _ll, _d, _p, _p, _p, _p, _d, _p, _i, _ll, _i,
 _sig("sblas_csr2csc_mgpu", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_sptrans", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_assemble_slices", _i, _p, _i, _ll, _p, _p, _i, _p, _p)
+_sig("sblas_assemble_cyclic", _i, _p, _i, _ll, _ll, _ll, _p, _p)
 _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
 _sig("sblas_csrbin_write", _i, C.c_char_p, _i, _i, _ll, _p, _p, _p)
 _sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)

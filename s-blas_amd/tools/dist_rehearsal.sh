@@ -5,15 +5,20 @@
 set -o pipefail
 O=gpurun_out; mkdir -p $O
 port=29611
-for np in 2 3 4; do for ex in allgather allreduce; do for algo in panel rowsplit csr5; do
+# (exchange, partition, algorithms): cyclic row chunks are the allgather default
+for np in 2 3 4; do for combo in "allgather cyclic panel rowsplit csr5" "allgather nnz panel" \
+    "allreduce nnz panel csr5"; do
+  set -- $combo; ex=$1; part=$2; shift 2
+  for algo in "$@"; do
   port=$((port+1))
+  L=$O/rehearsal_${np}_${ex}_${part}_${algo}.log
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
     --master-addr 127.0.0.1 --master-port $port bench.py --gpus $np --dist-backend gloo \
-    --nrows 200000 --steps 3 --warmup 1 --check --exchange $ex --algo $algo \
-    > $O/rehearsal_${np}_${ex}_${algo}.log 2>&1 || { echo "FAIL np=$np $ex $algo"; tail -20 $O/rehearsal_${np}_${ex}_${algo}.log; exit 1; }
-  grep -h '^{' $O/rehearsal_${np}_${ex}_${algo}.log | python3 -c "
+    --nrows 200000 --steps 3 --warmup 1 --check --exchange $ex --partition $part --algo $algo \
+    > $L 2>&1 || { echo "FAIL np=$np $ex $part $algo"; tail -20 $L; exit 1; }
+  grep -h '^{' $L | python3 -c "
 import sys,json
-d=json.loads(sys.stdin.read()); print('np=$np $ex $algo check=', d.get('check_vs_oracle'), d['value'])"
+d=json.loads(sys.stdin.read()); c=d.get('check_vs_oracle'); print('np=$np $ex $part $algo check=', c, d['value']); sys.exit(0 if c else 1)" || exit 1
 done; done; done
 # torchrun with one rank over RCCL (the driver's N=1 launch shape)
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \

@@ -85,6 +85,60 @@ def test_gloo_protocol(world):
     assert any(c for _, _, c in res)  # the split actually crossed a row
 
 
+def assemble_cyclic(gathered, world, stride, R, m):
+    """numpy restatement of k_assemble_cyclic (checker)."""
+    r = np.arange(m)
+    j = r // R
+    return gathered[(j % world) * stride + (j // world) * R + (r - j * R)]
+
+
+def _cyclic_worker(rank, world, port, n, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import orc
+    import sblas_dist
+    rp, col, val = orc.gen_synth(n, heavy=40, light=3)
+    x = orc.gen_vector(n, 43)
+    y0 = orc.gen_vector(n, 44)
+    a, b = orc.alpha_beta()
+    plan = sblas_dist.make_cyclic_plan(rp, n, world)
+    lrp, lcol, lval = sblas_dist.cyclic_local_csr(rp, plan, rank,
+                                                  lambda r0, r1: (col[rp[r0]:rp[r1]],
+                                                                  val[rp[r0]:rp[r1]]))
+    yl = np.concatenate([y0[r0:r1] for r0, r1 in plan.chunks(rank)] or [np.zeros(0)])
+    part = orc.csr_spmv(lrp, lcol, lval, x, a, b, yl)
+    buf = torch.zeros(plan.stride, dtype=torch.float64)
+    buf[:len(part)] = torch.from_numpy(part)
+    out = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf)
+    y = assemble_cyclic(torch.cat(out).numpy(), world, plan.stride, plan.chunk_rows, plan.m)
+    want = orc.csr_spmv(rp, col, val, x, a, b, y0)
+    ok = bool(np.all(np.abs(y - want) <= orc.spmv_bound(rp, col, val, x, a, b, y0)))
+    # every rank holds the same number of rows (up to the last chunk) and
+    # the heavy first eighth of the rows is spread over the ranks
+    rows = [plan.local_rows(d) for d in range(world)]
+    nnzs = [int(sum(rp[r1] - rp[r0] for r0, r1 in plan.chunks(d))) for d in range(world)]
+    balanced = max(rows) - min(rows) <= plan.chunk_rows and max(nnzs) <= 1.5 * (plan.nnz / world)
+    result_q.put((rank, ok and balanced and len(part) == plan.local_rows(rank)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_gloo_cyclic_protocol(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cyclic_worker, args=(r, world, port, 1003, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
+
+
 def _spmm_worker(rank, world, port, result_q):
     """SpMM row-block protocol: whole-row blocks by nnz, B
     replicated, each rank's C slice (ncols x stride, ld = stride) all-gathered
