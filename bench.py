@@ -104,7 +104,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel"], default="panel")
+    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel", "xsort"], default="panel")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
@@ -152,7 +152,8 @@ def main() -> int:
         else:
             dist.init_process_group("gloo")
 
-    algo = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL}[args.algo]
+    algo = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
+            "xsort": sblas.XSORT}[args.algo]
     n = args.nrows
     rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
     nnz = int(rowptr[-1])

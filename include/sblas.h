@@ -40,7 +40,9 @@ typedef enum {
     SBLAS_SPMV_ROWSPLIT = 1, /* CSR-adaptive row blocks, wave64, LDS stream */
     SBLAS_SPMV_CSR5 = 2,     /* wave64 CSR5-style tiles, segmented sum */
     SBLAS_SPMV_CSR5_ALT = 3, /* same kernel as 2 */
-    SBLAS_SPMV_PANEL = 4     /* XCD-affine column panels of the row-split kernel */
+    SBLAS_SPMV_PANEL = 4,    /* XCD-affine column panels of the row-split kernel */
+    SBLAS_SPMV_XSORT = 5     /* column-sorted XCD groups, LDS row accumulators
+                                (within the fp64 bound, not bitwise repeatable) */
 } sblas_spmv_algo;
 
 const char *sblas_status_string(int status);

@@ -192,6 +192,7 @@ int sblas_csr_analyse(sblas_csr A, int algo, void *stream)
     case SBLAS_SPMV_CSR5:
     case SBLAS_SPMV_CSR5_ALT: return build_csr5_plan(*A, s);
     case SBLAS_SPMV_PANEL: return build_panel_plan(*A, s);
+    case SBLAS_SPMV_XSORT: return build_xsort_plan(*A, s);
     default: return SBLAS_ERR_INVALID;
     }
 }
@@ -213,6 +214,9 @@ int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x, double be
     case SBLAS_SPMV_PANEL:
         if (!A->pn.ready) SBLAS_TRY(build_panel_plan(*A, s));
         return launch_spmv_panel(*A, alpha, d_x, beta, d_y, s);
+    case SBLAS_SPMV_XSORT:
+        if (!A->xs.ready) SBLAS_TRY(build_xsort_plan(*A, s));
+        return launch_spmv_xsort(*A, alpha, d_x, beta, d_y, s);
     default: return SBLAS_ERR_INVALID;
     }
 }

@@ -149,11 +149,12 @@ struct XsArgs {
     int qstride;
     int G, q, Wg;
     int use_xcc;
+    long long *trace;       // debugging aid (SBLAS_XS_TRACE), else null
 };
 
 struct XsPlan {
     int G = 0, q = 0, Wg = 0;
-    int nranges = 0, nwide = 0, nitems = 0, grid = 0;
+    int nranges = 0, nwide = 0, nitems = 0, grid = 0, nt = 0;
     XsRange *ranges = nullptr;
     int *wide = nullptr;         // [nwide] range ids
     long long *blk = nullptr;

@@ -788,6 +788,7 @@ void free_plans(sblas_csr_s &A)
     (void)hipFree(Q.partial);
     (void)hipFree(Q.long_rows);
     A.pn = PanelPlan{};
+    free_xsort_plan(A);
     free_spmm_plan(A);
 }
 

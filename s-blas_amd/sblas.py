@@ -23,6 +23,7 @@ LIB_PATH = os.path.join(_HERE, "libsblas.so")
 ROWSPLIT = 1  # test_spmv kernel 1 (csrmv)
 CSR5 = 2      # test_spmv kernel 2/3 (csrmv_mp / CSR5)
 PANEL = 4     # XCD-affine column panels (row-split per panel + reduce)
+XSORT = 5     # column-sorted XCD groups (LDS row accumulators)
 
 _STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error",
            3: "insufficient device memory", 4: "no device", 5: "unsupported",

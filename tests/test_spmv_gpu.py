@@ -14,18 +14,24 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-# (algorithm, forced panel count).  The panel algorithm (4) picks ~4 MiB of x
+# (algorithm, plan environment).  The panel algorithm (4) picks ~4 MiB of x
 # per panel, i.e. one panel for these small matrices; 3 and 8 panels are
 # forced too so the multi-panel path (interleaved grid + partial reduce) runs.
-ALGOS = [(1, None), (2, None), (4, None), (4, 3), (4, 8)]
-ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8"]
+# The column-sorted algorithm (5) makes few, narrow ranges for small
+# matrices; a tiny work target forces many ranges, most of them wide (one
+# item per column group + the partial reduce), and ALLWIDE forces every range
+# with entries through the wide path.
+ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
+         (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"})]
+ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
+            "xsort_allwide"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
 def algo(request, monkeypatch):
-    a, panels = request.param
-    if panels is not None:
-        monkeypatch.setenv("SBLAS_PANELS", str(panels))
+    a, env = request.param
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     return a
 
 
