@@ -124,11 +124,12 @@ struct SpmmPlan {
 // G = 8q groups of Wg <= 2^18 columns (XCD k serves groups [kq, (k+1)q)), rows
 // into ranges of <= kXsRows rows.  Block (range i, group g) holds the range's
 // entries of group g sorted by (column, row) as packed keys
-// (col - g*Wg) << 14 | (row - row0) plus values, so the lanes of one gather
-// instruction share x lines.  A narrow range is one work item (one
-// workgroup walks all groups, XCD-staggered, and writes y); a wide range is G
-// items, one per group, each writing an alpha-free partial that a reduce
-// pass adds in group order.
+// (col - g*Wg) << 14 | (row - row0) plus values, padded to whole 256-entry
+// chunks stored lane-transposed, so the lanes of one gather instruction share
+// x lines.  A narrow range is one sub-item (walks all groups, XCD-staggered,
+// and writes y); a wide range is 8 sub-items, one per XCD, each writing an
+// alpha-free partial that a reduce pass adds in XCD order.  A work item pairs
+// two sub-items (one per half of the workgroup).
 struct XsRange {
     int row0;
     int nrows;
@@ -142,7 +143,7 @@ struct XsArgs {
     const long long *blk;   // [nranges*G + 1] block offsets
     const uint32_t *key;
     const double *val;
-    const int *qitems;      // [8][qstride] items (range << 8 | group + 1; 0 = all)
+    const int *qitems;      // [8][qstride][2] sub-item pairs (range << 8 | XCD + 1, 0 = narrow; -1 = none)
     int *qhead;             // [8] claim counters, zeroed per launch
     double *partial;
     int qlen[8];
@@ -165,6 +166,8 @@ struct XsPlan {
     double *partial = nullptr;
     int qlen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int qstride = 0;
+    long long nchunks = 0;       // 256-entry chunks (blocks padded to whole chunks)
+    bool pair = true;            // items pair two sub-items (two 512-thread teams)
     bool ready = false;
 };
 

@@ -8,28 +8,40 @@
 // MI355X such divergent gathers run at ~265 G/s even when every line hits L2
 // (profiles/r01_exp_gather.txt), i.e. ~150 us for config 2's 39.75M nonzeros,
 // and at ~82 G/s when x (16 MB) misses L2.  Two changes attack both limits:
-//  * columns are cut into G = 8q groups of <= 2^18 columns; XCD k serves groups
-//    [kq, (k+1)q) (x slice <= 2 MiB, L2-resident);
-//  * inside a block (row range x group) the entries are sorted by column, and
-//    lanes read consecutive entries, so the lanes of one gather instruction
-//    land on few x lines (the TA merges them) -- measured 2x on the gather.
+//  * columns are cut into G = 8q groups of < 2^18 columns (~1 MiB of x); XCD
+//    k serves groups [kq, (k+1)q), so its gathers stay in its own L2;
+//  * inside a block (row range x group) the entries are sorted by column and
+//    the lanes of one gather instruction take CONSECUTIVE entries, so they
+//    land on few x lines (the TA merges them): 2x on the gather in the
+//    microbenchmark.
 // Row sums then arrive in column order, so they accumulate into per-row LDS
 // slots with ds_add_f64.  The summation ORDER within a row therefore depends
 // on wave timing: results are within the fp64 error bound of the sequential
 // row sum (tests) but not bitwise reproducible from run to run, unlike the
 // row-split/CSR5/panel kernels.
 //
-// Work items: a narrow range (few nonzeros) is one item -- one workgroup walks
-// all G groups, starting at its XCD's first group, and writes y; a wide range
-// is G items, one per group, each writing a partial for its rows, which a
-// reduce pass adds in group order.  Items sit in one queue per XCD; a
-// persistent grid claims from its own XCD's queue (XCC_ID hardware register)
-// and steals from the others when it runs dry.
+// Storage: each block is padded to whole 256-entry chunks (one wave, 4 entries
+// per lane) and every chunk is stored lane-transposed: lane l's 16-byte key
+// load holds entries {l, 64+l, 128+l, 192+l} and its two 16-byte value loads
+// {l, 64+l} and {128+l, 192+l}.  Streaming therefore runs at the 16-B/lane
+// rate while gather j of a wave covers the 64 consecutive entries 64j..64j+63.
+// Keys pack (col - g*Wg) << 14 | (row - row0); a padding key has the column
+// field all ones (no real column reaches it) and row 0.
+//
+// Work: a narrow range (short rows) is one sub-item -- it walks all G groups,
+// starting at its XCD's first group and wrapping, and writes y; a wide range
+// (rows >= 16 entries on average) is 8 sub-items, one per XCD over that XCD's
+// q groups, each writing a partial that a reduce pass adds in XCD order.
+// Narrow sub-items are bound by gather requests, wide ones by the entry
+// stream, so by default every work item PAIRS one of each: the two halves of
+// the 1024-thread workgroup (8 waves and 8192 LDS rows each) run them side by
+// side and every CU mixes both kinds of traffic.  Items sit in one queue per
+// XCD; a persistent grid claims from its own XCD's queue (XCC_ID hardware
+// register) and steals when it runs dry.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <numeric>
 #include <utility>
 #include <vector>
 
@@ -37,13 +49,20 @@
 
 namespace sblas {
 
-constexpr int kXsThreads = 1024;  // default workgroup (SBLAS_XS_THREADS=512 for experiments)
+constexpr int kXsThreads = 1024;
 constexpr int kXsRows = 16384;     // LDS row accumulators per workgroup (128 KiB)
+constexpr int kXsHalfRows = kXsRows / 2;
 constexpr int kXsRowBits = 14;     // packed key: local row in the low 14 bits
 constexpr int kXsColBits = 18;     //             group-local column above
-constexpr int kXsUnroll = 8;       // entries per lane in flight
+constexpr int kXsChunk = 256;      // entries per chunk: one wave, 4 per lane
+constexpr int kXsUnroll = 2;       // chunks per wave per pipeline stage
+constexpr uint32_t kXsPad = ((1u << kXsColBits) - 1) << kXsRowBits;  // column all ones, row 0
+constexpr int kXsTrace = 6;        // longs per trace row
 static_assert(kXsRowBits + kXsColBits == 32, "packed key is 32 bits");
 static_assert(kXsRows <= (1 << kXsRowBits), "local row must fit the key");
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
 
 // XCC_ID hardware register (gfx940+: HW_REG_XCC_ID = 20, bits [3:0]).
 __device__ __forceinline__ int xs_xcc_id()
@@ -51,6 +70,8 @@ __device__ __forceinline__ int xs_xcc_id()
     return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7;
 }
 
+// Claims a work item: returns its slot in qitems (queue * qstride + index),
+// own XCD's queue first, or -1 when every queue is empty.
 __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 {
     for (int k = 0; k < 8; ++k) {
@@ -58,111 +79,159 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
         if (__hip_atomic_load(&a.qhead[qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qlen[qq])
             continue;
         const int idx = atomicAdd(&a.qhead[qq], 1);
-        if (idx < a.qlen[qq]) return a.qitems[qq * a.qstride + idx];
+        if (idx < a.qlen[qq]) return qq * a.qstride + idx;
     }
     return -1;
 }
 
-// One work item's entries [s0, s1): consecutive column-group blocks whose
-// offsets are bnd[0..ng] (bnd[0] = s0, bnd[ng] = s1) for groups gb, gb+1, ...
-// (a wide item is one block, a narrow item all G blocks of its range, walked
-// as ONE stream so the pipeline never drains between groups).  Lanes read
-// consecutive entries; each lane tracks the group of its (increasing)
-// entries and turns it into the x offset of the group.
-// Software pipeline with ping-pong registers and an even, workgroup-uniform
-// trip count (no mid-loop exit, so nothing can be sunk below the adds):
+// One stream of chunks [c0, c1): consecutive column-group blocks whose chunk
+// offsets are bnd[0..ng] (bnd[0] = c0) for groups gb, gb+1, ...  The S waves
+// of a team take chunks c0 + w, c0 + w + S, ...; a wave's chunk (hence its
+// group) is wave-uniform.
+// Software pipeline with ping-pong registers and an even, team-uniform trip
+// count (no mid-loop exit, so nothing can be sunk below the adds):
 //   gathers(A) | loads(B) | adds(A) | gathers(B) | loads(A') | adds(B)
 // sched_barrier pins that issue order; waiting for the gathers (vmcnt counts
-// in order) then leaves the next batch's key/value loads in flight.  Lanes
-// past s1 load the last entry (one line per wave) and add an exact +0.0
-// (a select, not a product: the clamped x may be inf/nan).
+// in order) then leaves the next stage's key/value loads in flight.  A wave
+// past c1 loads one line (every lane the same address) and adds exact +0.0;
+// padding entries add +0.0 too (a select, not a product: x may be inf/nan).
 // kMode (timing experiments only, SBLAS_XS_MODE): 0 = the product kernel,
 // bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0].
-template <int kMode, int NT>
-__device__ __forceinline__ void xs_stream(const uint32_t *__restrict__ key,
-                                          const double *__restrict__ val, long long s0,
-                                          long long s1, const long long *bnd, int gb, int Wg,
-                                          const double *__restrict__ x, double *acc)
+template <int kMode, int S>
+__device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
+                                          const v2d *__restrict__ val2, long long c0,
+                                          long long c1, const long long *bnd, int gb, int Wg,
+                                          const double *__restrict__ x, double *acc, int wave)
 {
-    if (s1 <= s0) return;  // workgroup-uniform
+    if (c1 <= c0) return;  // team-uniform
     constexpr int U = kXsUnroll;
-    constexpr long long S = (long long)U * NT;
-    int gi = 0;              // lane's current group (relative to gb)
+    const int lane = threadIdx.x & 63;
+    int gi = 0;              // the wave's current group (relative to gb)
     long long nb = bnd[1];   // its end
-    auto load = [&](long long eb, uint32_t *kk, double *vv, int *xo) {
+    auto load = [&](long long t, v4u *kk, v2d *va, v2d *vb, int *xo) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const long long eu = eb + (long long)u * NT;
-            const long long ei = eu < s1 ? eu : s1 - 1;
-            kk[u] = __builtin_nontemporal_load(key + ei);
-            vv[u] = __builtin_nontemporal_load(val + ei);
-            while (ei >= nb) nb = bnd[++gi + 1];
+            const long long c = c0 + wave + (t * U + u) * S;
+            const bool live = c < c1;
+            const long long ci = live ? c : c1 - 1;
+            kk[u] = __builtin_nontemporal_load(key4 + ci * 64 + (live ? lane : 0));
+            va[u] = __builtin_nontemporal_load(val2 + ci * 128 + (live ? lane : 0));
+            vb[u] = __builtin_nontemporal_load(val2 + ci * 128 + 64 + (live ? lane : 0));
+            while (ci >= nb) nb = bnd[++gi + 1];
             xo[u] = (gb + gi) * Wg;
         }
     };
-    auto gather = [&](const uint32_t *kk, const int *xo, double *xx) {
+    auto gather = [&](const v4u *kk, const int *xo, double (*xx)[4]) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) xx[u] = x[(kMode & 2) ? 0 : xo[u] + (int)(kk[u] >> kXsRowBits)];
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                const int idx = k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits);
+                xx[u][j] = x[(kMode & 2) ? 0 : idx];
+            }
     };
-    auto accumulate = [&](long long eb, const uint32_t *kk, const double *vv, const double *xx) {
+    auto accumulate = [&](long long t, const v4u *kk, const v2d *va, const v2d *vb,
+                          double (*xx)[4]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double p = eb + (long long)u * NT < s1 ? vv[u] * xx[u] : 0.0;
-            if (kMode & 1) acc[kk[u] & ((1u << kXsRowBits) - 1)] = p;
-            else atomicAdd(&acc[kk[u] & ((1u << kXsRowBits) - 1)], p);
+            const bool live = c0 + wave + (t * U + u) * S < c1;
+            const double v[4] = {va[u].x, va[u].y, vb[u].x, vb[u].y};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                const double p = (live && k != kXsPad) ? v[j] * xx[u][j] : 0.0;
+                double *slot = &acc[k & ((1u << kXsRowBits) - 1)];
+                if (kMode & 1) *slot = p;
+                else atomicAdd(slot, p);
+            }
         }
     };
-    uint32_t ka[U], kb[U];
-    double va[U], vb[U], xa[U], xb[U];
+    v4u ka[U], kb[U];
+    v2d vaa[U], vab[U], vba[U], vbb[U];
+    double xa[U][4], xb[U][4];
     int oa[U], ob[U];
-    const long long nit = (s1 - s0 + S - 1) / S;
-    long long e = s0 + threadIdx.x;
-    load(e, ka, va, oa);
-    for (long long it = 0; it < nit; it += 2) {
+    const long long T = (c1 - c0 + (long long)S * U - 1) / ((long long)S * U);
+    load(0, ka, vaa, vab, oa);
+    for (long long t = 0; t < T; t += 2) {
         gather(ka, oa, xa);
         __builtin_amdgcn_sched_barrier(0);
-        load(e + S, kb, vb, ob);
+        load(t + 1, kb, vba, vbb, ob);
         __builtin_amdgcn_sched_barrier(0);
-        accumulate(e, ka, va, xa);
+        accumulate(t, ka, vaa, vab, xa);
         __builtin_amdgcn_sched_barrier(0);
         gather(kb, ob, xb);
         __builtin_amdgcn_sched_barrier(0);
-        load(e + 2 * S, ka, va, oa);
+        load(t + 2, ka, vaa, vab, oa);
         __builtin_amdgcn_sched_barrier(0);
-        accumulate(e + S, kb, vb, xb);
-        e += 2 * S;
+        accumulate(t + 1, kb, vba, vbb, xb);
     }
 }
 
-template <bool kBeta, int kMode, int NT>
-__global__ __launch_bounds__(NT) void k_spmv_xsort(const XsArgs a, const double *__restrict__ x,
-                                                   double alpha, double beta,
-                                                   double *__restrict__ y)
+// kWG threads per workgroup: 1024 (16384 LDS rows, one workgroup per CU) or
+// 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
+// two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
+// the item's two sub-items side by side; otherwise all waves run sub-item 0.
+template <bool kBeta, int kMode, int kWG, bool kPair>
+__global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
+                                                    const double *__restrict__ x,
+                                                    double alpha, double beta,
+                                                    double *__restrict__ y)
 {
-    __shared__ double acc[kXsRows];
-    __shared__ long long s_bnd[256];
+    static_assert(kWG == 1024 || (kWG == 512 && !kPair), "workgroup shapes");
+    __shared__ double acc_all[kWG == 1024 ? kXsRows : kXsHalfRows];
+    __shared__ long long s_bnd_all[2][256];
+    __shared__ unsigned long long s_tend[2];
     __shared__ int s_item;
+    constexpr int NT = kPair ? kWG / 2 : kWG;                // threads per team
+    constexpr int S = NT / 64;                               // waves per team
+    const int half = kPair ? (int)(threadIdx.x >= (unsigned)NT) : 0;
+    const int ht = (int)threadIdx.x - half * NT;
+    const int hwave = __builtin_amdgcn_readfirstlane(ht >> 6);
+    double *acc = acc_all + (kPair ? half * kXsHalfRows : 0);
+    long long *s_bnd = s_bnd_all[half];
+    const v4u *key4 = reinterpret_cast<const v4u *>(a.key);
+    const v2d *val2 = reinterpret_cast<const v2d *>(a.val);
     const int xcc = a.use_xcc ? xs_xcc_id() : (int)(blockIdx.x & 7);
+    const long long t_entry = a.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     if (threadIdx.x == 0) s_item = xs_claim(a, xcc);
     for (;;) {
         __syncthreads();
-        const int item = s_item;
-        if (item < 0) return;  // workgroup-uniform
-        // item = range << 8 | slot: slot k+1 = wide item of XCD k (its q
-        // groups [kq, kq+q), partial slot k); slot 0 = narrow item (all G
-        // groups, starting at this XCD's first group and wrapping)
-        const int ri = item >> 8, k1 = item & 255;
-        const XsRange R = a.ranges[ri];
-        const long long *bo = a.blk + (long long)ri * a.G;
-        const int g0 = k1 ? (k1 - 1) * a.q : xcc * a.q;
-        const int ng = k1 ? a.q : a.G;
-        for (int r = threadIdx.x; r < R.nrows; r += NT) acc[r] = 0.0;
-        // s_bnd[j] = start of group (g0 + j) % G in a wrapped walk: segment 1
-        // is groups [g0, G) (bounds s_bnd[0..G-g0]), segment 2 groups [0, g0)
-        const int n1 = k1 ? ng : a.G - g0;
-        for (int j = threadIdx.x; j <= n1; j += NT) s_bnd[j] = bo[g0 + j];
-        if (!k1)
-            for (int j = threadIdx.x; j <= g0; j += NT) s_bnd[128 + j] = bo[j];
+        const int slot = s_item;
+        if (slot < 0) {  // workgroup-uniform
+            if (a.trace && threadIdx.x == 0) {  // per-workgroup row: entry .. exit
+                const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
+                a.trace[ts] = -2;
+                a.trace[ts + 1] = -2;
+                a.trace[ts + 2] = ((long long)blockIdx.x << 4) | xcc;
+                a.trace[ts + 3] = t_entry;
+                a.trace[ts + 4] = (long long)__builtin_amdgcn_s_memrealtime();
+                a.trace[ts + 5] = 0;
+            }
+            return;
+        }
+        // sub = range << 8 | k: k+1 = wide sub-item of XCD k (its q groups
+        // [kq, kq+q), partial slot k); 0 = narrow (all G groups, starting at
+        // this XCD's first group and wrapping); -1 = nothing for this team
+        const int sub = a.qitems[2 * slot + half];
+        XsRange R{};
+        int k1 = 0, g0 = 0, n1 = 0;
+        if (sub >= 0) {  // team-uniform
+            const int ri = sub >> 8;
+            k1 = sub & 255;
+            R = a.ranges[ri];
+            const long long *bo = a.blk + (long long)ri * a.G;
+            g0 = k1 ? (k1 - 1) * a.q : xcc * a.q;
+            // s_bnd[j] = first chunk of group g0 + j: segment 1 is groups
+            // [g0, g0+n1); a narrow sub-item's segment 2 is groups [0, g0)
+            // at s_bnd + 128
+            n1 = k1 ? a.q : a.G - g0;
+            for (int r = ht; r < R.nrows; r += NT) acc[r] = 0.0;
+            for (int j = ht; j <= n1; j += NT) s_bnd[j] = bo[g0 + j];
+            if (!k1)
+                for (int j = ht; j <= g0; j += NT) s_bnd[128 + j] = bo[j];
+        }
+        if (a.trace && ht == 0) s_tend[half] = 0;
         __syncthreads();
         // claim the next item now; its result is consumed after the stream,
         // so the atomic's latency hides behind the stream's own loads
@@ -172,40 +241,45 @@ __global__ __launch_bounds__(NT) void k_spmv_xsort(const XsArgs a, const double 
             pre = atomicAdd(&a.qhead[xcc], 1);
             if (a.trace) t0 = (long long)__builtin_amdgcn_s_memrealtime();
         }
-        xs_stream<kMode, NT>(a.key, a.val, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc);
-        if (!k1 && g0 > 0)
-            xs_stream<kMode, NT>(a.key, a.val, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0, a.Wg, x,
-                                 acc);
-        if (threadIdx.x == 0) {
-            if (a.trace) {  // debugging aid (SBLAS_XS_TRACE): per-item timeline
-                const long long t1 = (long long)__builtin_amdgcn_s_memrealtime();
-                const long long slot = 1 + 4LL * atomicAdd((unsigned long long *)a.trace, 1ULL);
-                a.trace[slot] = item;
-                const long long cnt = k1 ? s_bnd[n1] - s_bnd[0] : bo[a.G] - bo[0];
-                a.trace[slot + 1] = (cnt << 20) | ((long long)blockIdx.x << 4) | xcc;
-                a.trace[slot + 2] = t0;
-                a.trace[slot + 3] = t1;
-            }
-            s_item = pre < a.qlen[xcc] ? a.qitems[xcc * a.qstride + pre] : xs_claim(a, xcc);
+        if (sub >= 0) {
+            xs_stream<kMode, S>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
+            if (!k1 && g0 > 0)
+                xs_stream<kMode, S>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0, a.Wg,
+                                    x, acc, hwave);
         }
+        if (a.trace && (threadIdx.x & 63) == 0)  // debugging aid: this team's last wave
+            atomicMax(&s_tend[half], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0)
+            s_item = pre < a.qlen[xcc] ? xcc * a.qstride + pre : xs_claim(a, xcc);
         __syncthreads();
-        if (k1) {
-            double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
-            for (int r = threadIdx.x; r < R.nrows; r += NT) out[r] = acc[r];
-        } else {
-            double *yr = y + R.row0;
-            for (int r = threadIdx.x; r < R.nrows; r += NT)
-                yr[r] = kBeta ? alpha * acc[r] + beta * yr[r] : alpha * acc[r];
+        if (a.trace && threadIdx.x == 0) {  // debugging aid (SBLAS_XS_TRACE): item timeline
+            const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
+            a.trace[ts] = a.qitems[2 * slot];
+            a.trace[ts + 1] = kPair ? a.qitems[2 * slot + 1] : -1;
+            a.trace[ts + 2] = ((long long)blockIdx.x << 4) | xcc;
+            a.trace[ts + 3] = t0;
+            a.trace[ts + 4] = (long long)s_tend[0];
+            a.trace[ts + 5] = (long long)s_tend[1];
+        }
+        if (sub >= 0) {
+            if (k1) {
+                double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
+                for (int r = ht; r < R.nrows; r += NT) out[r] = acc[r];
+            } else {
+                double *yr = y + R.row0;
+                for (int r = ht; r < R.nrows; r += NT)
+                    yr[r] = kBeta ? alpha * acc[r] + beta * yr[r] : alpha * acc[r];
+            }
         }
         // (the barrier at the loop top orders these reads of acc before the
-        // next item's zeroing)
+        // next item's zeroing, and s_bnd's reuse)
     }
 }
 
 // Wide ranges: y = alpha * sum_k partial[k] (+ beta*y), XCD slots in order.
 template <bool kBeta>
 __global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict__ ranges,
-                                                      const int *__restrict__ wide, int G,
+                                                      const int *__restrict__ wide,
                                                       const double *__restrict__ partial,
                                                       double alpha, double beta,
                                                       double *__restrict__ y)
@@ -214,7 +288,8 @@ __global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict_
     for (int r = blockIdx.x * 256 + threadIdx.x; r < R.nrows; r += gridDim.x * 256) {
         const double *p = partial + R.pbase + r;
         double s = 0.0;
-        for (int g = 0; g < G; ++g) s += p[(long long)g * R.nrows];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += p[(long long)k * R.nrows];
         double *yr = y + R.row0 + r;
         *yr = kBeta ? alpha * s + beta * *yr : alpha * s;
     }
@@ -243,12 +318,14 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     const long long nnz = A.nnz;
     const std::vector<int> &rp = A.h_rowptr;
 
-    // column groups: G = 8q groups of Wg <= 2^18 columns and ~1 MiB of x
-    // (an XCD's current group plus the A stream must fit its 4 MiB L2)
-    const long long ng = ((long long)std::max(n, 1) + (1LL << kXsColBits) - 1) >> kXsColBits;
+    // column groups: G = 8q groups of Wg < 2^18 columns (the all-ones column
+    // field is the padding key) and ~1 MiB of x (an XCD's current group plus
+    // the entry stream must fit its 4 MiB L2)
+    const long long wmax = (1LL << kXsColBits) - 1;
+    const long long ng = ((long long)std::max(n, 1) + wmax - 1) / wmax;
     const long long nmib = ((long long)std::max(n, 1) * 8 + (1LL << 20) - 1) >> 20;
     P.q = (int)std::max<long long>({1LL, (ng + 7) / 8, (nmib + 7) / 8});
-    if (const char *e = getenv("SBLAS_XS_Q"))  // experiments: override, >= the 2^18 bound
+    if (const char *e = getenv("SBLAS_XS_Q"))  // experiments: override, >= the width bound
         P.q = (int)std::max<long long>({1LL, (ng + 7) / 8, (long long)atoi(e)});
     P.G = 8 * P.q;
     if (P.G > 127) {
@@ -258,39 +335,38 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     P.Wg = (int)std::max<long long>(1, ((long long)std::max(n, 1) + P.G - 1) / P.G);
     const int G = P.G, Wg = P.Wg;
 
-    // resident workgroups -> work per item
+    // workgroup shape (SBLAS_XS_WG / SBLAS_XS_PAIR select the experiments'
+    // alternatives); resident workgroups = item slots, a paired item holds
+    // two sub-items
+    P.nt = kXsThreads;
+    if (const char *e = getenv("SBLAS_XS_WG")) P.nt = atoi(e) == 512 ? 512 : kXsThreads;
+    P.pair = P.nt == kXsThreads && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
     int dev = 0, ncu = 0, per_cu = 0;
     SBLAS_HIP(hipGetDevice(&dev));
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    P.nt = getenv("SBLAS_XS_THREADS") && atoi(getenv("SBLAS_XS_THREADS")) == 512 ? 512 : kXsThreads;
     if (P.nt == 512)
-        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_xsort<true, 0, 512>, 512, 0));
+        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, k_spmv_xsort<true, 0, 512, false>, 512, 0));
     else
-        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_spmv_xsort<true, 0, kXsThreads>,
-                                                                kXsThreads, 0));
+        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, k_spmv_xsort<true, 0, kXsThreads, true>, kXsThreads, 0));
     const int resident = std::max(1, ncu * std::max(per_cu, 1));
-    // about kper items per resident workgroup (claimed dynamically)
     int kper = 1;
     if (const char *e = getenv("SBLAS_XS_K")) kper = std::max(1, atoi(e));
-    long long wstar = std::max<long long>(1, (nnz + (long long)resident * kper - 1) / ((long long)resident * kper));
-    if (const char *e = getenv("SBLAS_XS_WSTAR")) wstar = std::max(1LL, atoll(e));
+    const long long slots = (long long)resident * kper * (P.pair ? 2 : 1);  // sub-items
     const bool all_wide = getenv("SBLAS_XS_ALLWIDE") && atoi(getenv("SBLAS_XS_ALLWIDE")) != 0;
     const bool nosort = getenv("SBLAS_XS_NOSORT") && atoi(getenv("SBLAS_XS_NOSORT")) != 0;
-    int rows_cap = kXsRows;
-    if (const char *e = getenv("SBLAS_XS_ROWS")) rows_cap = std::max(1, std::min(kXsRows, atoi(e)));
+    int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsRows;
+    if (const char *e = getenv("SBLAS_XS_ROWS")) rows_cap = std::max(1, std::min(rows_cap, atoi(e)));
 
-    // Row ranges: a candidate range takes <= rows_cap rows while one of its
-    // 8 wide items costs <= cap; it becomes wide or is re-cut into narrow
-    // ranges of cost <= cap (below).
-    std::vector<XsRange> ranges;
-    // Cost model (work units ~ one streamed entry): an item's time is its
-    // entries plus lambda per distinct x line its gathers touch; with
-    // uniform columns a block of c entries over L lines touches
-    // L*(1 - exp(-c/L)) lines.  A narrow item spreads its entries over all of
-    // x (G*Lg lines), a wide item's 1/8 share over its XCD's q groups.
-    // lambda = 1.7 was fitted on config 2's item timeline (SBLAS_XS_TRACE:
-    // narrow items ran at 0.58x the entries/us of wide ones).
-    double lam = 1.7;
+    // Cost model (work units ~ one streamed entry): a sub-item's time is its
+    // entries plus lambda per distinct x line its gathers touch; with uniform
+    // columns a block of c entries over L lines touches L*(1 - exp(-c/L))
+    // lines.  A narrow sub-item spreads its entries over all of x (G*Lg
+    // lines), a wide one its 1/8 share over its XCD's q groups.  lambda = 1.0
+    // is the best of a sweep (0.3 .. 1.7) on config 2 with the paired,
+    // chunked kernel.
+    double lam = 1.0;
     if (const char *e = getenv("SBLAS_XS_LAMBDA")) lam = atof(e);
     const double Lg = std::max(1.0, Wg / 16.0);  // 128-B lines of one group's x slice
     auto narrow_cost = [&](double c) { return c + lam * G * Lg * (1.0 - std::exp(-c / (G * Lg))); };
@@ -298,13 +374,18 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         const double ci = c / 8.0;
         return ci + lam * P.q * Lg * (1.0 - std::exp(-ci / (P.q * Lg)));
     };
+    // Row ranges: from row r, a wide candidate takes <= rows_cap rows while
+    // one of its 8 sub-items costs <= cap.  It is WIDE (8 sub-items + 8
+    // partials per row) when it holds more than one narrow sub-item's work and
+    // its rows average >= 16 entries (the partials then cost <= 8 B per
+    // entry); otherwise a narrow range of cost <= cap is cut afresh from r.
+    std::vector<XsRange> ranges;
     auto build_ranges = [&](double cap) {
         ranges.clear();
-        // extend [r, ...) while cost(entries) <= cap and rows <= rows_cap
-        auto cut = [&](int r, int rend, bool wide, long long &cnt) {
+        auto cut = [&](int r, bool wide, long long &cnt) {
             const int start = r;
             cnt = 0;
-            while (r < rend && r - start < rows_cap) {
+            while (r < m && r - start < rows_cap) {
                 const long long len = rp[r + 1] - rp[r];
                 const double c = (double)(cnt + len);
                 if (r > start && (wide ? wide_cost(c) : narrow_cost(c)) > cap) break;
@@ -316,46 +397,30 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         int r = 0;
         while (r < m) {
             long long cnt;
-            const int e = cut(r, m, true, cnt);
-            // WIDE (8 items, one per XCD, + 8 partials per row) when it holds
-            // more than one narrow item's work and its rows average >= 16
-            // entries (the partials then cost <= 8 B per entry)
+            int e = cut(r, true, cnt);
             const bool wide = cnt > 0 && (all_wide || (narrow_cost((double)cnt) > cap &&
                                                        cnt >= 16LL * (e - r)));
-            if (wide) {
-                XsRange R{};
-                R.row0 = r;
-                R.nrows = e - r;
-                R.wide = 1;
-                ranges.push_back(R);
-            } else {
-                for (int q0 = r; q0 < e;) {
-                    long long c2;
-                    const int q1 = cut(q0, e, false, c2);
-                    XsRange R{};
-                    R.row0 = q0;
-                    R.nrows = q1 - q0;
-                    R.wide = 0;
-                    ranges.push_back(R);
-                    q0 = q1;
-                }
-            }
+            if (!wide) e = cut(r, false, cnt);
+            XsRange R{};
+            R.row0 = r;
+            R.nrows = e - r;
+            R.wide = wide ? 1 : 0;
+            ranges.push_back(R);
             r = e;
         }
     };
-    auto count_items = [&]() {
+    auto count_subs = [&]() {
         long long c = 0;
         for (const XsRange &R : ranges) c += R.wide ? 8 : 1;
         return c;
     };
-    // grow the item cost until the items fit the resident grid (a second
-    // round for a few items would double the kernel's tail)
-    const long long slots = (long long)resident * kper;
-    double cap = (double)wstar;
-    if (!getenv("SBLAS_XS_WSTAR")) cap = narrow_cost((double)nnz) / (double)slots;
-    for (int it = 0; it < 200; ++it) {
+    // grow the sub-item cost until the sub-items fit the resident grid (a
+    // second round for a few items would double the kernel's tail)
+    double cap = narrow_cost((double)nnz) / (double)slots;
+    if (const char *e = getenv("SBLAS_XS_WSTAR")) cap = std::max(1.0, atof(e));
+    for (int it = 0; it < 400; ++it) {
         build_ranges(cap);
-        if (count_items() <= slots || getenv("SBLAS_XS_WSTAR")) break;
+        if (count_subs() <= slots || getenv("SBLAS_XS_WSTAR")) break;
         cap *= 1.02;
     }
     const int I = (int)ranges.size();
@@ -372,49 +437,62 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMemcpy(hval.data(), A.val, sizeof(double) * nnz, hipMemcpyDeviceToHost));
     }
 
-    // pass 1: entries per (range, group)
-    std::vector<long long> blk((size_t)I * G + 1, 0);
+    // pass 1: entries per (range, group) -> whole chunks per block
+    std::vector<long long> cnt((size_t)I * G, 0);
 #pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < I; ++i) {
-        long long *c = blk.data() + (size_t)i * G + 1;
-        for (int e = rp[ranges[i].row0]; e < rp[ranges[i].row0 + ranges[i].nrows]; ++e)
-            ++c[hcol[e] / Wg];
+        long long *c = cnt.data() + (size_t)i * G;
+        for (int e = rp[ranges[i].row0]; e < rp[ranges[i].row0 + ranges[i].nrows]; ++e) {
+            const int col = hcol[e];
+            if (col >= 0 && col < n) ++c[col / Wg];
+        }
     }
-    for (size_t k = 1; k < blk.size(); ++k) blk[k] += blk[k - 1];
+    std::vector<long long> blk((size_t)I * G + 1, 0);  // chunk offsets
+    for (size_t k = 0; k < cnt.size(); ++k) blk[k + 1] = blk[k] + (cnt[k] + kXsChunk - 1) / kXsChunk;
+    const long long nchunks = blk.back();
 
-    // pass 2: fill each block and sort it by (column, row)
-    std::vector<uint32_t> hkey((size_t)nnz);
-    std::vector<double> hv((size_t)nnz);
+    // pass 2: fill each block, sort it by (column, row), pad it to whole
+    // chunks and store every chunk lane-transposed (header comment)
+    std::vector<uint32_t> hkey((size_t)nchunks * kXsChunk);
+    std::vector<double> hv((size_t)nchunks * kXsChunk);
     bool bad = false;
 #pragma omp parallel
     {
-        std::vector<long long> pos(G);
-        std::vector<std::pair<uint32_t, double>> tmp;
+        std::vector<std::vector<std::pair<uint32_t, double>>> bucket(G);
 #pragma omp for schedule(dynamic, 16) reduction(|| : bad)
         for (int i = 0; i < I; ++i) {
             const XsRange &R = ranges[i];
-            for (int g = 0; g < G; ++g) pos[g] = blk[(size_t)i * G + g];
+            for (int g = 0; g < G; ++g) bucket[g].clear();
             for (int r = R.row0; r < R.row0 + R.nrows; ++r) {
                 for (int e = rp[r]; e < rp[r + 1]; ++e) {
                     const int c = hcol[e];
+                    if (c < 0 || c >= n) {
+                        bad = true;
+                        continue;
+                    }
                     const int g = c / Wg;
                     const uint32_t cp = (uint32_t)(c - g * Wg), lr = (uint32_t)(r - R.row0);
-                    if (c < 0 || c >= n || cp >= (1u << kXsColBits) || lr >= (uint32_t)kXsRows) bad = true;
-                    const long long o = pos[g]++;
-                    hkey[o] = (cp << kXsRowBits) | lr;
-                    hv[o] = hval[e];
+                    if ((long long)cp >= wmax || lr >= (uint32_t)rows_cap) bad = true;
+                    bucket[g].push_back({(cp << kXsRowBits) | lr, hval[e]});
                 }
             }
             for (int g = 0; g < G; ++g) {
-                const long long b0 = blk[(size_t)i * G + g], b1 = blk[(size_t)i * G + g + 1];
-                tmp.resize((size_t)(b1 - b0));
-                for (long long o = b0; o < b1; ++o) tmp[o - b0] = {hkey[o], hv[o]};
-                if (!nosort) std::stable_sort(tmp.begin(), tmp.end(),
-                                 [](const std::pair<uint32_t, double> &a,
-                                    const std::pair<uint32_t, double> &b) { return a.first < b.first; });
-                for (long long o = b0; o < b1; ++o) {
-                    hkey[o] = tmp[o - b0].first;
-                    hv[o] = tmp[o - b0].second;
+                auto &b = bucket[g];
+                if (!nosort)
+                    std::stable_sort(b.begin(), b.end(),
+                                     [](const std::pair<uint32_t, double> &u,
+                                        const std::pair<uint32_t, double> &v) { return u.first < v.first; });
+                const long long c0 = blk[(size_t)i * G + g], c1 = blk[(size_t)i * G + g + 1];
+                for (long long c = c0; c < c1; ++c) {
+                    uint32_t *kc = hkey.data() + c * kXsChunk;
+                    double *vc = hv.data() + c * kXsChunk;
+                    for (int p = 0; p < kXsChunk; ++p) {
+                        const long long src = (c - c0) * kXsChunk + p;
+                        const bool in = src < (long long)b.size();
+                        const int l = p & 63, j = p >> 6;
+                        kc[4 * l + j] = in ? b[src].first : kXsPad;
+                        vc[(j < 2 ? 0 : 128) + 2 * l + (j & 1)] = in ? b[src].second : 0.0;
+                    }
                 }
             }
         }
@@ -424,24 +502,65 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         return SBLAS_ERR_INVALID;
     }
 
-    // items, wide partial slots, XCD queues
-    std::vector<int> wide;
-    std::vector<std::vector<int>> q(8);
+    // sub-items, wide partial slots, then items (pairs) in XCD queues
+    std::vector<int> wide, nsub;
+    std::vector<std::vector<int>> wsub(8);
     long long pbase = 0;
-    int nnarrow = 0;
     for (int i = 0; i < I; ++i) {
         XsRange &R = ranges[i];
         if (R.wide) {
             R.pbase = pbase;
             pbase += 8LL * R.nrows;
             wide.push_back(i);
-            for (int k = 0; k < 8; ++k) q[k].push_back((i << 8) | (k + 1));
+            for (int k = 0; k < 8; ++k) wsub[k].push_back((i << 8) | (k + 1));
         } else {
-            q[nnarrow++ % 8].push_back(i << 8);
+            nsub.push_back(i << 8);
+        }
+    }
+    std::vector<std::vector<std::pair<int, int>>> q(8);
+    if (!P.pair) {
+        for (int k = 0; k < 8; ++k)
+            for (int w : wsub[k]) q[k].push_back({w, -1});
+        for (size_t j = 0; j < nsub.size(); ++j) q[j % 8].push_back({nsub[j], -1});
+        // longest first (estimated cost): the dynamic claims then end evenly
+        auto cost = [&](int sub) {
+            const XsRange &R = ranges[sub >> 8];
+            const double c = (double)(rp[R.row0 + R.nrows] - rp[R.row0]);
+            return (sub & 255) ? wide_cost(c) : narrow_cost(c);
+        };
+        for (int k = 0; k < 8; ++k)
+            std::stable_sort(q[k].begin(), q[k].end(),
+                             [&](const std::pair<int, int> &u, const std::pair<int, int> &v) {
+                                 return cost(u.first) > cost(v.first);
+                             });
+    } else {
+        // a narrow (gather-bound) with a wide (stream-bound) sub-item where
+        // possible, the XCDs interleaved so the narrow ones spread evenly;
+        // leftovers pair among themselves (wide ones within their XCD)
+        size_t ni = 0;
+        std::vector<std::vector<int>> wleft(8);
+        for (size_t j = 0;; ++j) {
+            bool any = false;
+            for (int k = 0; k < 8; ++k) {
+                if (j >= wsub[k].size()) continue;
+                any = true;
+                if (ni < nsub.size()) q[k].push_back({nsub[ni++], wsub[k][j]});
+                else wleft[k].push_back(wsub[k][j]);
+            }
+            if (!any) break;
+        }
+        for (int k = 0; k < 8; ++k)
+            for (size_t j = 0; j < wleft[k].size(); j += 2)
+                q[k].push_back({wleft[k][j], j + 1 < wleft[k].size() ? wleft[k][j + 1] : -1});
+        for (int t = 0; ni < nsub.size(); ++t) {
+            const int a0 = nsub[ni++];
+            const int a1 = ni < nsub.size() ? nsub[ni++] : -1;
+            q[t % 8].push_back({a0, a1});
         }
     }
     P.nranges = I;
     P.nwide = (int)wide.size();
+    P.nchunks = nchunks;
     P.qstride = 1;
     P.nitems = 0;
     for (int k = 0; k < 8; ++k) {
@@ -450,14 +569,19 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         P.nitems += P.qlen[k];
     }
     P.grid = std::min(P.nitems, resident);
-    std::vector<int> qflat((size_t)8 * P.qstride, -1);
-    for (int k = 0; k < 8; ++k) std::copy(q[k].begin(), q[k].end(), qflat.begin() + (size_t)k * P.qstride);
+    std::vector<int> qflat((size_t)16 * P.qstride, -1);
+    for (int k = 0; k < 8; ++k)
+        for (size_t j = 0; j < q[k].size(); ++j) {
+            qflat[2 * ((size_t)k * P.qstride + j)] = q[k][j].first;
+            qflat[2 * ((size_t)k * P.qstride + j) + 1] = q[k][j].second;
+        }
 
+    const size_t ne = (size_t)std::max<long long>(nchunks, 1) * kXsChunk;
     SBLAS_HIP(hipMalloc(&P.ranges, sizeof(XsRange) * std::max(I, 1)));
     SBLAS_HIP(hipMalloc(&P.wide, sizeof(int) * std::max<size_t>(wide.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.blk, sizeof(long long) * blk.size()));
-    SBLAS_HIP(hipMalloc(&P.key, sizeof(uint32_t) * std::max<long long>(nnz, 1)));
-    SBLAS_HIP(hipMalloc(&P.val, sizeof(double) * std::max<long long>(nnz, 1)));
+    SBLAS_HIP(hipMalloc(&P.key, sizeof(uint32_t) * ne));
+    SBLAS_HIP(hipMalloc(&P.val, sizeof(double) * ne));
     SBLAS_HIP(hipMalloc(&P.qitems, sizeof(int) * qflat.size()));
     SBLAS_HIP(hipMalloc(&P.qhead, sizeof(int) * 8));
     SBLAS_HIP(hipMalloc(&P.partial, sizeof(double) * std::max<long long>(pbase, 1)));
@@ -465,9 +589,9 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     if (!wide.empty())
         SBLAS_HIP(hipMemcpy(P.wide, wide.data(), sizeof(int) * wide.size(), hipMemcpyHostToDevice));
     SBLAS_HIP(hipMemcpy(P.blk, blk.data(), sizeof(long long) * blk.size(), hipMemcpyHostToDevice));
-    if (nnz) {
-        SBLAS_HIP(hipMemcpy(P.key, hkey.data(), sizeof(uint32_t) * nnz, hipMemcpyHostToDevice));
-        SBLAS_HIP(hipMemcpy(P.val, hv.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    if (nchunks) {
+        SBLAS_HIP(hipMemcpy(P.key, hkey.data(), sizeof(uint32_t) * hkey.size(), hipMemcpyHostToDevice));
+        SBLAS_HIP(hipMemcpy(P.val, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
     }
     SBLAS_HIP(hipMemcpy(P.qitems, qflat.data(), sizeof(int) * qflat.size(), hipMemcpyHostToDevice));
     P.ready = true;
@@ -484,6 +608,10 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         const char *e = getenv("SBLAS_XS_XCC");
         return e ? atoi(e) : 1;
     }();
+    static const int mode = [] {
+        const char *e = getenv("SBLAS_XS_MODE");
+        return e ? atoi(e) : 0;
+    }();
     XsArgs a{};
     a.ranges = P.ranges;
     a.blk = P.blk;
@@ -498,52 +626,54 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.q = P.q;
     a.Wg = P.Wg;
     a.use_xcc = use_xcc;
-    static const int mode = [] {
-        const char *e = getenv("SBLAS_XS_MODE");
-        return e ? atoi(e) : 0;
-    }();
     SBLAS_HIP(hipMemsetAsync(P.qhead, 0, sizeof(int) * 8, s));
     using K = void (*)(const XsArgs, const double *, double, double, double *);
     K kern;
-    if (P.nt == 512)
-        kern = beta != 0.0 ? k_spmv_xsort<true, 0, 512> : k_spmv_xsort<false, 0, 512>;
-    else if (mode == 1)
-        kern = beta != 0.0 ? k_spmv_xsort<true, 1, kXsThreads> : k_spmv_xsort<false, 1, kXsThreads>;
-    else if (mode == 2)
-        kern = beta != 0.0 ? k_spmv_xsort<true, 2, kXsThreads> : k_spmv_xsort<false, 2, kXsThreads>;
-    else if (mode == 3)
-        kern = beta != 0.0 ? k_spmv_xsort<true, 3, kXsThreads> : k_spmv_xsort<false, 3, kXsThreads>;
-    else
-        kern = beta != 0.0 ? k_spmv_xsort<true, 0, kXsThreads> : k_spmv_xsort<false, 0, kXsThreads>;
+    const bool b = beta != 0.0;
+    constexpr int W = kXsThreads;
+    if (P.nt == 512) {
+        if (mode == 1) kern = b ? k_spmv_xsort<true, 1, 512, false> : k_spmv_xsort<false, 1, 512, false>;
+        else if (mode == 2) kern = b ? k_spmv_xsort<true, 2, 512, false> : k_spmv_xsort<false, 2, 512, false>;
+        else if (mode == 3) kern = b ? k_spmv_xsort<true, 3, 512, false> : k_spmv_xsort<false, 3, 512, false>;
+        else kern = b ? k_spmv_xsort<true, 0, 512, false> : k_spmv_xsort<false, 0, 512, false>;
+    } else if (P.pair) {
+        if (mode == 1) kern = b ? k_spmv_xsort<true, 1, W, true> : k_spmv_xsort<false, 1, W, true>;
+        else if (mode == 2) kern = b ? k_spmv_xsort<true, 2, W, true> : k_spmv_xsort<false, 2, W, true>;
+        else if (mode == 3) kern = b ? k_spmv_xsort<true, 3, W, true> : k_spmv_xsort<false, 3, W, true>;
+        else kern = b ? k_spmv_xsort<true, 0, W, true> : k_spmv_xsort<false, 0, W, true>;
+    } else {
+        kern = b ? k_spmv_xsort<true, 0, W, false> : k_spmv_xsort<false, 0, W, false>;
+    }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
     std::vector<long long> htrace;
     if (trace_path) {
-        const size_t len = 1 + 4 * (size_t)P.nitems;
+        const size_t len = 1 + (size_t)kXsTrace * (P.nitems + P.grid);
         SBLAS_HIP(hipMalloc(&a.trace, sizeof(long long) * len));
         SBLAS_HIP(hipMemsetAsync(a.trace, 0, sizeof(long long) * len, s));
         htrace.resize(len);
     }
     hipLaunchKernelGGL(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
-    if (trace_path) {  // debugging aid: append {item, block<<8|xcc, t0, t1} rows
+    if (trace_path) {  // debugging aid: rows {subA, subB, block<<4|xcc, t0, endA, endB}
         SBLAS_HIP(hipMemcpyAsync(htrace.data(), a.trace, sizeof(long long) * htrace.size(),
                                  hipMemcpyDeviceToHost, s));
         SBLAS_HIP(hipStreamSynchronize(s));
         (void)hipFree(a.trace);
         if (FILE *f = fopen(trace_path, "a")) {
-            fprintf(f, "# launch items=%d grid=%d\n", P.nitems, P.grid);
-            for (long long i = 0; i < htrace[0]; ++i)
-                fprintf(f, "%lld %lld %lld %lld\n", htrace[1 + 4 * i], htrace[2 + 4 * i],
-                        htrace[3 + 4 * i], htrace[4 + 4 * i]);
+            fprintf(f, "# launch items=%d grid=%d pair=%d\n", P.nitems, P.grid, (int)P.pair);
+            for (long long i = 0; i < htrace[0]; ++i) {
+                const long long *r = htrace.data() + 1 + kXsTrace * i;
+                fprintf(f, "%lld %lld %lld %lld %lld %lld\n", r[0], r[1], r[2], r[3], r[4], r[5]);
+            }
             fclose(f);
         }
     }
     if (P.nwide) {
-        const dim3 grid((kXsRows + 255) / 256, (unsigned)P.nwide);
-        if (beta != 0.0)
-            hipLaunchKernelGGL(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide, 8,
+        const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
+        if (b)
+            hipLaunchKernelGGL(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide,
                                P.partial, alpha, beta, y);
         else
-            hipLaunchKernelGGL(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.ranges, P.wide, 8,
+            hipLaunchKernelGGL(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.ranges, P.wide,
                                P.partial, alpha, beta, y);
     }
     SBLAS_HIP(hipGetLastError());

@@ -19,12 +19,15 @@ pytestmark = pytest.mark.gpu
 # forced too so the multi-panel path (interleaved grid + partial reduce) runs.
 # The column-sorted algorithm (5) makes few, narrow ranges for small
 # matrices; a tiny work target forces many ranges, most of them wide (one
-# item per column group + the partial reduce), and ALLWIDE forces every range
-# with entries through the wide path.
+# sub-item per XCD + the partial reduce) and paired with narrow ones, ALLWIDE
+# forces every range with entries through the wide path (wide sub-items paired
+# with each other), and PAIR=0 runs one sub-item per workgroup.
 ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
-         (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"})]
+         (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
+         (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"})]
 ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide"]
+            "xsort_allwide", "xsort_unpaired", "xsort_wg512"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
