@@ -9,19 +9,22 @@ distinct uniform-random sorted columns (seed 42), values U[0,1), x U[0,1)
 the whole matrix with every input already resident in HBM; at N > 1 the
 rows are dealt to the ranks in equal cyclic chunks (x replicated) and a step
 also includes the RCCL allgather of the y slices plus their device-side
-placement (strong scaling: the same matrix at every N).  Timing follows the
-bench contract (K back-to-back steps between barriers); the cold-cache
-number (a 1 GiB scrub before each step, so that at N = 8 a
-rank's ~67 MB slice cannot sit in the 256 MB Infinity Cache) is reported
-beside it under `cold`.
+placement (strong scaling: the same matrix at every N).  The headline is
+cold-cache (a 1 GiB scrub before each of the K
+timed steps, so that at N = 8 a rank's ~67 MB slice cannot sit in the 256 MB
+Infinity Cache; each step between its own barrier + synchronize pair, the
+scrub outside the timed region); the warm number (K back-to-back steps
+between one barrier pair) is reported beside it under `warm`.
 
-  python bench.py [--gpus N --steps K --warmup W] [--algo panel|rowsplit|csr5] [--cache warm|cold]
-                  [--partition cyclic|nnz]
+  python bench.py [--gpus N --steps K --warmup W] [--algo xsort|panel|rowsplit|csr5]
+                  [--cache cold|warm] [--partition cyclic|nnz]
 
-Default kernel: `panel` = the row-split kernel run over XCD-affine column
-panels (x slice ~4 MiB per panel, panel p's row blocks on workgroups with
-blockIdx % P == p) plus a partial-y reduce; with a single non-empty panel it
-is exactly the plain row-split kernel.
+Default kernel: `xsort` (csrc/xsort.hip) = entries sorted by column inside
+(row range x column group) blocks, column groups dealt to the XCDs so every
+x gather stays in the XCD's own L2, lane-consecutive gathers, LDS fp64 row
+accumulators.  Within the fp64 error bound of the sequential row sum but not
+bitwise repeatable (LDS atomics); `--algo panel` (XCD-affine column panels of
+the row-split kernel) is the fastest bitwise-deterministic kernel.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
@@ -104,7 +107,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel", "xsort"], default="panel")
+    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel", "xsort"], default="xsort")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
@@ -116,12 +119,13 @@ def main() -> int:
     ap.add_argument("--check", action="store_true",
                     help="after timing, verify the assembled y of one fresh step against the "
                          "oracle (rank 0; small n only)")
-    ap.add_argument("--cache", choices=["cold", "warm"], default="warm",
-                    help="warm (default, the bench contract): K back-to-back steps bracketed by "
-                         "one barrier + synchronize on each side; cold (SURVEY M1-cache): a 1 GiB "
-                         "scrub before every timed step evicts the 256 MB Infinity Cache and the "
-                         "L2s, each step bracketed by its own barrier + synchronize.  The other "
-                         "mode is always measured too and reported under `cold`/`warm`.")
+    ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
+                    help="cold (default; SURVEY M1-cache / BASELINE.md: the headline uses cold "
+                         "timing): a 1 GiB scrub before every timed step evicts the 256 MB "
+                         "Infinity Cache and the L2s, each of the K steps bracketed by its own "
+                         "barrier + synchronize; warm: K back-to-back steps bracketed by one "
+                         "barrier + synchronize on each side.  The other mode is always measured "
+                         "too and reported under `warm`/`cold`.")
     ap.add_argument("--partition", choices=["cyclic", "nnz"], default="cyclic",
                     help="N > 1 row distribution: cyclic equal-row chunks (default; no padding, "
                          "whole rows) or one nnz-balanced range per rank (spMV_mgpu_v1's split, "

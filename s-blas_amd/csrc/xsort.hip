@@ -355,6 +355,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     if (const char *e = getenv("SBLAS_XS_K")) kper = std::max(1, atoi(e));
     const long long slots = (long long)resident * kper * (P.pair ? 2 : 1);  // sub-items
     const bool all_wide = getenv("SBLAS_XS_ALLWIDE") && atoi(getenv("SBLAS_XS_ALLWIDE")) != 0;
+    const bool no_wide = getenv("SBLAS_XS_NOWIDE") && atoi(getenv("SBLAS_XS_NOWIDE")) != 0;
     const bool nosort = getenv("SBLAS_XS_NOSORT") && atoi(getenv("SBLAS_XS_NOSORT")) != 0;
     int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsRows;
     if (const char *e = getenv("SBLAS_XS_ROWS")) rows_cap = std::max(1, std::min(rows_cap, atoi(e)));
@@ -398,8 +399,8 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         while (r < m) {
             long long cnt;
             int e = cut(r, true, cnt);
-            const bool wide = cnt > 0 && (all_wide || (narrow_cost((double)cnt) > cap &&
-                                                       cnt >= 16LL * (e - r)));
+            const bool wide = cnt > 0 && !no_wide &&
+                              (all_wide || (narrow_cost((double)cnt) > cap && cnt >= 16LL * (e - r)));
             if (!wide) e = cut(r, false, cnt);
             XsRange R{};
             R.row0 = r;
