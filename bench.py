@@ -16,10 +16,11 @@ Infinity Cache; each step between its own barrier + synchronize pair, the
 scrub outside the timed region); the warm number (K back-to-back steps
 between one barrier pair) is reported beside it under `warm`.
 
-  python bench.py [--gpus N --steps K --warmup W] [--algo xsort|panel|rowsplit|csr5]
+  python bench.py [--gpus N --steps K --warmup W] [--algo auto|xsort|panel|rowsplit|csr5]
                   [--cache cold|warm] [--partition cyclic|nnz]
 
-Default kernel: `xsort` (csrc/xsort.hip) = entries sorted by column inside
+Default kernel (`auto`): `xsort` while a rank holds >= 12M nonzeros (N <= 2
+for config 2), else `panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
 (row range x column group) blocks, column groups dealt to the XCDs so every
 x gather stays in the XCD's own L2, lane-consecutive gathers, LDS fp64 row
 accumulators.  Within the fp64 error bound of the sequential row sum but not
@@ -107,7 +108,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--algo", choices=["rowsplit", "csr5", "panel", "xsort"], default="xsort")
+    ap.add_argument("--algo", choices=["auto", "rowsplit", "csr5", "panel", "xsort"], default="auto",
+                    help="auto (default): xsort when a rank holds >= 12M nonzeros, else panel "
+                         "(s-blas_amd/tools/bench_slice.py: per-rank kernel times at N = 1..8)")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
@@ -156,13 +159,19 @@ def main() -> int:
         else:
             dist.init_process_group("gloo")
 
-    algo = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
-            "xsort": sblas.XSORT}[args.algo]
+    algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
+                "xsort": sblas.XSORT}
     n = args.nrows
     rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
     nnz = int(rowptr[-1])
     prefix = args.cols == "prefix"
     t_gen = time.perf_counter()
+    if args.algo == "auto":
+        # the column-sorted kernel's per-item costs (padding to 256-entry
+        # chunks, item set-up) pay off on large slices; the XCD-panel row
+        # split wins below ~12M nonzeros per rank
+        args.algo = "xsort" if nnz / world >= 12e6 else "panel"
+    algo = algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
         lrp, col, val = sblas_dist.cyclic_local_csr(

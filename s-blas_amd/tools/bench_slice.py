@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-GPU SpMV kernel time of ONE rank's share of config 2 at N ranks.
+
+bench.py at N > 1 deals the rows to the ranks in cyclic chunks
+(sblas_dist.make_cyclic_plan); this tool builds rank 0's local CSR for N in
+--worlds on the single GPU of the box and times each kernel on it alone
+(warm back-to-back and cold after a 1 GiB scrub, HIP events on the launch
+stream), so the kernel choice per N can be made without an 8-GPU node.
+Prints one JSON line per (N, algo).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "s-blas_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--algos", default="xsort,panel,rowsplit")
+    ap.add_argument("--nrows", type=int, default=2_000_000)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+
+    import torch
+    import sblas
+    import sblas_dist
+
+    dev = torch.device("cuda", 0)
+    n = args.nrows
+    rowptr = sblas.gen_synth_rowptr(n, 96, 9)
+    x = torch.from_numpy(sblas.gen_vector(n, 43)).to(dev)
+    scrub = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    algos = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
+             "xsort": sblas.XSORT}
+    for world in [int(w) for w in args.worlds.split(",")]:
+        plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
+        lrp, col, val = sblas_dist.cyclic_local_csr(
+            rowptr, plan, 0, lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, 96, 9, seed=42))
+        for name in args.algos.split(","):
+            A = sblas.DeviceCSR.upload(0, n, lrp, col, val)
+            A.analyse(algos[name])
+            y = torch.zeros(len(lrp) - 1, dtype=torch.float64, device=dev)
+            out = {}
+            with torch.cuda.stream(stream):
+                for mode in ("warm", "cold"):
+                    ts = []
+                    for k in range(args.reps + 2):
+                        if mode == "cold":
+                            scrub.add_(1)
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record(stream)
+                        A.spmv(algos[name], 1.0, x.data_ptr(), 0.5, y.data_ptr(), stream.cuda_stream)
+                        e1.record(stream)
+                        if mode == "cold":
+                            torch.cuda.synchronize()
+                        ts.append((e0, e1))
+                    torch.cuda.synchronize()
+                    out[mode + "_us"] = round(float(np.median([a.elapsed_time(b) for a, b in ts[2:]])) * 1e3, 1)
+            A.close()
+            print(json.dumps({"world": world, "algo": name, "local_rows": int(len(lrp) - 1),
+                              "local_nnz": int(lrp[-1]), **out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

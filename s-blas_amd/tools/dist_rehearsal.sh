@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out; mkdir -p $O
 port=29611
 # (exchange, partition, algorithms): cyclic row chunks are the allgather default
-for np in 2 3 4; do for combo in "allgather cyclic panel rowsplit csr5" "allgather nnz panel" \
+for np in 2 3 4; do for combo in "allgather cyclic xsort panel rowsplit csr5" "allgather nnz xsort panel" \
     "allreduce nnz panel csr5"; do
   set -- $combo; ex=$1; part=$2; shift 2
   for algo in "$@"; do
