@@ -144,7 +144,7 @@ struct XsArgs {
     const uint32_t *key;
     const double *val;
     const int *qitems;      // [8][qstride][2] sub-item pairs (range << 8 | XCD + 1, 0 = narrow; -1 = none)
-    int *qhead;             // [8] claim counters, zeroed per launch
+    int *qhead;             // [8] claim counters + [8] exit count; the last workgroup re-zeroes them
     double *partial;
     int qlen[8];
     int qstride;
@@ -167,7 +167,8 @@ struct XsPlan {
     int qlen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int qstride = 0;
     long long nchunks = 0;       // 256-entry chunks (blocks padded to whole chunks)
-    bool pair = true;            // items pair two sub-items (two 512-thread teams)
+    bool pair = true;            // items pair two sub-items (two teams of waves)
+    int split = 8;               // waves of a pair's first team (of 16)
     bool ready = false;
 };
 

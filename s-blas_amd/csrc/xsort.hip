@@ -172,7 +172,7 @@ __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
 // 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
 // two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
 // the item's two sub-items side by side; otherwise all waves run sub-item 0.
-template <bool kBeta, int kMode, int kWG, bool kPair>
+template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false>
 __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     const double *__restrict__ x,
                                                     double alpha, double beta,
@@ -183,23 +183,38 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     __shared__ long long s_bnd_all[2][256];
     __shared__ unsigned long long s_tend[2];
     __shared__ int s_item;
-    constexpr int NT = kPair ? kWG / 2 : kWG;                // threads per team
-    constexpr int S = NT / 64;                               // waves per team
-    const int half = kPair ? (int)(threadIdx.x >= (unsigned)NT) : 0;
-    const int ht = (int)threadIdx.x - half * NT;
+    // waves per team: team 0 (the pair's first, normally narrow, sub-item)
+    // gets kWA waves, team 1 the rest
+    constexpr int SA = kPair ? kWA : kWG / 64;
+    constexpr int SB = kPair ? kWG / 64 - kWA : 0;
+    static_assert(!kPair || (kWA >= 1 && kWA < kWG / 64), "team split");
+    const int half = kPair ? (int)(threadIdx.x >= (unsigned)(SA * 64)) : 0;
+    const int NT = half ? SB * 64 : SA * 64;                 // threads in this team
+    const int ht = (int)threadIdx.x - half * SA * 64;
     const int hwave = __builtin_amdgcn_readfirstlane(ht >> 6);
     double *acc = acc_all + (kPair ? half * kXsHalfRows : 0);
     long long *s_bnd = s_bnd_all[half];
     const v4u *key4 = reinterpret_cast<const v4u *>(a.key);
     const v2d *val2 = reinterpret_cast<const v2d *>(a.val);
     const int xcc = a.use_xcc ? xs_xcc_id() : (int)(blockIdx.x & 7);
-    const long long t_entry = a.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    const long long t_entry = kTrace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     if (threadIdx.x == 0) s_item = xs_claim(a, xcc);
     for (;;) {
         __syncthreads();
         const int slot = s_item;
         if (slot < 0) {  // workgroup-uniform
-            if (a.trace && threadIdx.x == 0) {  // per-workgroup row: entry .. exit
+            // the last workgroup out re-arms the queues for the next launch
+            // (every claim has returned before its workgroup counts itself
+            // out), so no memset precedes the kernel; launches of one plan
+            // are serialised by their stream
+            if (threadIdx.x == 0) {
+                __threadfence();
+                if (atomicAdd(&a.qhead[8], 1) == (int)gridDim.x - 1) {
+                    for (int k = 0; k < 8; ++k) atomicExch(&a.qhead[k], 0);
+                    atomicExch(&a.qhead[8], 0);
+                }
+            }
+            if (kTrace && threadIdx.x == 0) {  // per-workgroup row: entry .. exit
                 const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
                 a.trace[ts] = -2;
                 a.trace[ts + 1] = -2;
@@ -231,7 +246,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             if (!k1)
                 for (int j = ht; j <= g0; j += NT) s_bnd[128 + j] = bo[j];
         }
-        if (a.trace && ht == 0) s_tend[half] = 0;
+        if (kTrace && ht == 0) s_tend[half] = 0;
         __syncthreads();
         // claim the next item now; its result is consumed after the stream,
         // so the atomic's latency hides behind the stream's own loads
@@ -239,20 +254,27 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
         long long t0 = 0;
         if (threadIdx.x == 0) {
             pre = atomicAdd(&a.qhead[xcc], 1);
-            if (a.trace) t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            if (kTrace) t0 = (long long)__builtin_amdgcn_s_memrealtime();
         }
         if (sub >= 0) {
-            xs_stream<kMode, S>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
-            if (!k1 && g0 > 0)
-                xs_stream<kMode, S>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0, a.Wg,
-                                    x, acc, hwave);
+            if (SA == SB || half == 0) {  // one inlined copy when the teams are equal
+                xs_stream<kMode, SA>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
+                if (!k1 && g0 > 0)
+                    xs_stream<kMode, SA>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
+                                         a.Wg, x, acc, hwave);
+            } else if constexpr (kPair && SA != SB) {
+                xs_stream<kMode, SB>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
+                if (!k1 && g0 > 0)
+                    xs_stream<kMode, SB>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
+                                         a.Wg, x, acc, hwave);
+            }
         }
-        if (a.trace && (threadIdx.x & 63) == 0)  // debugging aid: this team's last wave
+        if (kTrace && (threadIdx.x & 63) == 0)  // debugging aid: this team's last wave
             atomicMax(&s_tend[half], (unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (threadIdx.x == 0)
             s_item = pre < a.qlen[xcc] ? xcc * a.qstride + pre : xs_claim(a, xcc);
         __syncthreads();
-        if (a.trace && threadIdx.x == 0) {  // debugging aid (SBLAS_XS_TRACE): item timeline
+        if (kTrace && threadIdx.x == 0) {  // debugging aid (SBLAS_XS_TRACE): item timeline
             const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
             a.trace[ts] = a.qitems[2 * slot];
             a.trace[ts + 1] = kPair ? a.qitems[2 * slot + 1] : -1;
@@ -341,6 +363,8 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     P.nt = kXsThreads;
     if (const char *e = getenv("SBLAS_XS_WG")) P.nt = atoi(e) == 512 ? 512 : kXsThreads;
     P.pair = P.nt == kXsThreads && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
+    P.split = 8;  // waves of the first (narrow) team of a pair: 5, 6, 7 or 8
+    if (const char *e = getenv("SBLAS_XS_SPLIT")) P.split = std::min(8, std::max(5, atoi(e)));
     int dev = 0, ncu = 0, per_cu = 0;
     SBLAS_HIP(hipGetDevice(&dev));
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -369,6 +393,11 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // chunked kernel.
     double lam = 1.0;
     if (const char *e = getenv("SBLAS_XS_LAMBDA")) lam = atof(e);
+    // at most this fraction of the entries goes to wide ranges (the rest of
+    // the heavy rows is cut into narrow ranges), so that a paired item's two
+    // halves carry similar work
+    double wbudget = 1.0;
+    if (const char *e = getenv("SBLAS_XS_WBUDGET")) wbudget = atof(e);
     const double Lg = std::max(1.0, Wg / 16.0);  // 128-B lines of one group's x slice
     auto narrow_cost = [&](double c) { return c + lam * G * Lg * (1.0 - std::exp(-c / (G * Lg))); };
     auto wide_cost = [&](double c) {
@@ -396,11 +425,14 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             return r;
         };
         int r = 0;
+        long long wide_entries = 0;
         while (r < m) {
             long long cnt;
             int e = cut(r, true, cnt);
             const bool wide = cnt > 0 && !no_wide &&
-                              (all_wide || (narrow_cost((double)cnt) > cap && cnt >= 16LL * (e - r)));
+                              (all_wide || (narrow_cost((double)cnt) > cap && cnt >= 16LL * (e - r) &&
+                                            (double)(wide_entries + cnt) <= wbudget * (double)nnz));
+            if (wide) wide_entries += cnt;
             if (!wide) e = cut(r, false, cnt);
             XsRange R{};
             R.row0 = r;
@@ -584,7 +616,8 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     SBLAS_HIP(hipMalloc(&P.key, sizeof(uint32_t) * ne));
     SBLAS_HIP(hipMalloc(&P.val, sizeof(double) * ne));
     SBLAS_HIP(hipMalloc(&P.qitems, sizeof(int) * qflat.size()));
-    SBLAS_HIP(hipMalloc(&P.qhead, sizeof(int) * 8));
+    SBLAS_HIP(hipMalloc(&P.qhead, sizeof(int) * 16));  // [8] claim heads, [8] exit count
+    SBLAS_HIP(hipMemset(P.qhead, 0, sizeof(int) * 16));
     SBLAS_HIP(hipMalloc(&P.partial, sizeof(double) * std::max<long long>(pbase, 1)));
     if (I) SBLAS_HIP(hipMemcpy(P.ranges, ranges.data(), sizeof(XsRange) * I, hipMemcpyHostToDevice));
     if (!wide.empty())
@@ -627,7 +660,6 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.q = P.q;
     a.Wg = P.Wg;
     a.use_xcc = use_xcc;
-    SBLAS_HIP(hipMemsetAsync(P.qhead, 0, sizeof(int) * 8, s));
     using K = void (*)(const XsArgs, const double *, double, double, double *);
     K kern;
     const bool b = beta != 0.0;
@@ -641,11 +673,19 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         if (mode == 1) kern = b ? k_spmv_xsort<true, 1, W, true> : k_spmv_xsort<false, 1, W, true>;
         else if (mode == 2) kern = b ? k_spmv_xsort<true, 2, W, true> : k_spmv_xsort<false, 2, W, true>;
         else if (mode == 3) kern = b ? k_spmv_xsort<true, 3, W, true> : k_spmv_xsort<false, 3, W, true>;
+        else if (P.split == 6) kern = b ? k_spmv_xsort<true, 0, W, true, 6> : k_spmv_xsort<false, 0, W, true, 6>;
+        else if (P.split == 5) kern = b ? k_spmv_xsort<true, 0, W, true, 5> : k_spmv_xsort<false, 0, W, true, 5>;
+        else if (P.split == 7) kern = b ? k_spmv_xsort<true, 0, W, true, 7> : k_spmv_xsort<false, 0, W, true, 7>;
         else kern = b ? k_spmv_xsort<true, 0, W, true> : k_spmv_xsort<false, 0, W, true>;
     } else {
         kern = b ? k_spmv_xsort<true, 0, W, false> : k_spmv_xsort<false, 0, W, false>;
     }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
+    if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
+        if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
+        else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
+        else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;
+    }
     std::vector<long long> htrace;
     if (trace_path) {
         const size_t len = 1 + (size_t)kXsTrace * (P.nitems + P.grid);

@@ -149,6 +149,29 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
     assert np.array_equal(outs[4], outs[5])
 
 
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"}])
+def test_xsort_relaunch(torch_cuda, sb, orc, monkeypatch, env):
+    """The column-sorted kernel's work queues re-arm themselves at the end of
+    each launch (no memset): five launches on one plan, each checked."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n = 20000
+    rp, col, val = orc.gen_synth(n)
+    x = orc.gen_vector(n, 43)
+    A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    A.analyse(5)
+    xd = torch_cuda.from_numpy(x).cuda()
+    want = orc.csr_spmv(rp, col, val, x, 1.5, 0.0, np.zeros(n))
+    bound = orc.spmv_bound(rp, col, val, x, 1.5, 0.0, np.zeros(n))
+    for it in range(5):
+        yd = torch_cuda.full((n,), np.nan, dtype=torch_cuda.float64, device="cuda")
+        A.spmv(5, 1.5, xd.data_ptr(), 0.0, yd.data_ptr())
+        torch_cuda.cuda.synchronize()
+        got = yd.cpu().numpy()
+        assert np.all(np.abs(got - want) <= bound), f"launch {it}"
+    A.close()
+
+
 @pytest.mark.parametrize("version", ["baseline", "v1", "v2"])
 @pytest.mark.parametrize("ngpu", [1, 2, 3, 8])
 def test_reference_api(torch_cuda, sb, orc, version, ngpu):
