@@ -169,6 +169,7 @@ struct XsPlan {
     long long nchunks = 0;       // 256-entry chunks (blocks padded to whole chunks)
     bool pair = true;            // items pair two sub-items (two teams of waves)
     int split = 8;               // waves of a pair's first team (of 16)
+    bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
     bool ready = false;
 };
 

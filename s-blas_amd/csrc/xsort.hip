@@ -168,11 +168,107 @@ __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
     }
 }
 
+// Dynamic form of xs_stream for paired items: instead of the fixed
+// wave-interleaved split, every wave claims U consecutive chunks at a time
+// from the stream's LDS counter (*ctr, chunks past c0), so a team that has
+// finished its own sub-item can drain its partner's: the two halves of a
+// pair end together however their narrow/wide costs compare.  Same pipeline
+// (gathers | next loads | adds), a claim per stage; claims are monotone per
+// wave, so the group walk over bnd[] stays forward-only.
+template <int kMode>
+__device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
+                                              const v2d *__restrict__ val2, int *ctr,
+                                              long long c0, long long c1, const long long *bnd,
+                                              int gb, int Wg, const double *__restrict__ x,
+                                              double *acc)
+{
+    if (c1 <= c0) return;  // uniform
+    if (__builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= c1 - c0)
+        return;  // drained already (the common case for a helper)
+    constexpr int U = kXsUnroll;
+    const int lane = threadIdx.x & 63;
+    int gi = 0;
+    long long nb = bnd[1];
+    auto claim = [&]() -> long long {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(ctr, U);
+        return c0 + __builtin_amdgcn_readfirstlane(v);
+    };
+    auto load = [&](long long cb, v4u *kk, v2d *va, v2d *vb, int *xo) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long c = cb + u;
+            const bool live = c < c1;
+            const long long ci = live ? c : c1 - 1;
+            kk[u] = __builtin_nontemporal_load(key4 + ci * 64 + (live ? lane : 0));
+            va[u] = __builtin_nontemporal_load(val2 + ci * 128 + (live ? lane : 0));
+            vb[u] = __builtin_nontemporal_load(val2 + ci * 128 + 64 + (live ? lane : 0));
+            while (ci >= nb) nb = bnd[++gi + 1];
+            xo[u] = (gb + gi) * Wg;
+        }
+    };
+    auto gather = [&](const v4u *kk, const int *xo, double (*xx)[4]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                const int idx = k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits);
+                xx[u][j] = x[(kMode & 2) ? 0 : idx];
+            }
+    };
+    auto accumulate = [&](long long cb, const v4u *kk, const v2d *va, const v2d *vb,
+                          double (*xx)[4]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool live = cb + u < c1;
+            const double v[4] = {va[u].x, va[u].y, vb[u].x, vb[u].y};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                const double p = (live && k != kXsPad) ? v[j] * xx[u][j] : 0.0;
+                double *slot = &acc[k & ((1u << kXsRowBits) - 1)];
+                if (kMode & 1) *slot = p;
+                else atomicAdd(slot, p);
+            }
+        }
+    };
+    v4u ka[U], kb[U];
+    v2d vaa[U], vab[U], vba[U], vbb[U];
+    double xa[U][4], xb[U][4];
+    int oa[U], ob[U];
+    long long ca = claim();
+    if (ca >= c1) return;
+    load(ca, ka, vaa, vab, oa);
+    for (;;) {
+        gather(ka, oa, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        const long long cb = claim();
+        load(cb, kb, vba, vbb, ob);
+        __builtin_amdgcn_sched_barrier(0);
+        accumulate(ca, ka, vaa, vab, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        if (cb >= c1) break;
+        gather(kb, ob, xb);
+        __builtin_amdgcn_sched_barrier(0);
+        ca = claim();
+        load(ca, ka, vaa, vab, oa);
+        __builtin_amdgcn_sched_barrier(0);
+        accumulate(cb, kb, vba, vbb, xb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ca >= c1) break;
+    }
+}
+
 // kWG threads per workgroup: 1024 (16384 LDS rows, one workgroup per CU) or
 // 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
 // two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
 // the item's two sub-items side by side; otherwise all waves run sub-item 0.
-template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false>
+// kDyn (pairs only): the chunks of both sub-items are claimed dynamically
+// (xs_stream_dyn); a team drains its own streams, then its partner's.
+template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false,
+          bool kDyn = false>
 __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     const double *__restrict__ x,
                                                     double alpha, double beta,
@@ -183,6 +279,9 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     __shared__ long long s_bnd_all[2][256];
     __shared__ unsigned long long s_tend[2];
     __shared__ int s_item;
+    __shared__ int s_ctr[2][2];  // kDyn: claimed chunks per (team, segment)
+    __shared__ int s_par[2][4];  // kDyn: per team {sub valid, k1, g0, n1}
+    static_assert(!kDyn || kPair, "dynamic claims pair two sub-items");
     // waves per team: team 0 (the pair's first, normally narrow, sub-item)
     // gets kWA waves, team 1 the rest
     constexpr int SA = kPair ? kWA : kWG / 64;
@@ -246,6 +345,14 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             if (!k1)
                 for (int j = ht; j <= g0; j += NT) s_bnd[128 + j] = bo[j];
         }
+        if (kDyn && ht == 0) {
+            s_ctr[half][0] = 0;
+            s_ctr[half][1] = 0;
+            s_par[half][0] = sub;
+            s_par[half][1] = k1;
+            s_par[half][2] = g0;
+            s_par[half][3] = n1;
+        }
         if (kTrace && ht == 0) s_tend[half] = 0;
         __syncthreads();
         // claim the next item now; its result is consumed after the stream,
@@ -256,7 +363,20 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             pre = atomicAdd(&a.qhead[xcc], 1);
             if (kTrace) t0 = (long long)__builtin_amdgcn_s_memrealtime();
         }
-        if (sub >= 0) {
+        if constexpr (kDyn) {
+            // own segment 1, own segment 2 (narrow wrap), then the partner's
+            // two: one inlined stream, its operands chosen per pass
+            for (int p = 0; p < 4; ++p) {
+                const int h = p < 2 ? half : 1 - half;
+                const int seg = p & 1;
+                const int hs = s_par[h][0], hk1 = s_par[h][1], hg0 = s_par[h][2], hn1 = s_par[h][3];
+                if (hs < 0 || (seg && (hk1 || hg0 == 0))) continue;  // uniform
+                const long long *hb = s_bnd_all[h] + (seg ? 128 : 0);
+                const int hn = seg ? hg0 : hn1;
+                xs_stream_dyn<kMode>(key4, val2, &s_ctr[h][seg], hb[0], hb[hn], hb, seg ? 0 : hg0,
+                                     a.Wg, x, acc_all + h * kXsHalfRows);
+            }
+        } else if (sub >= 0) {
             if (SA == SB || half == 0) {  // one inlined copy when the teams are equal
                 xs_stream<kMode, SA>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
                 if (!k1 && g0 > 0)
@@ -365,6 +485,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     P.pair = P.nt == kXsThreads && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
     P.split = 8;  // waves of the first (narrow) team of a pair: 5, 6, 7 or 8
     if (const char *e = getenv("SBLAS_XS_SPLIT")) P.split = std::min(8, std::max(5, atoi(e)));
+    P.dyn = P.pair && P.split == 8 && !(getenv("SBLAS_XS_DYN") && atoi(getenv("SBLAS_XS_DYN")) == 0);
     int dev = 0, ncu = 0, per_cu = 0;
     SBLAS_HIP(hipGetDevice(&dev));
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -676,6 +797,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else if (P.split == 6) kern = b ? k_spmv_xsort<true, 0, W, true, 6> : k_spmv_xsort<false, 0, W, true, 6>;
         else if (P.split == 5) kern = b ? k_spmv_xsort<true, 0, W, true, 5> : k_spmv_xsort<false, 0, W, true, 5>;
         else if (P.split == 7) kern = b ? k_spmv_xsort<true, 0, W, true, 7> : k_spmv_xsort<false, 0, W, true, 7>;
+        else if (P.dyn) kern = b ? k_spmv_xsort<true, 0, W, true, 8, false, true> : k_spmv_xsort<false, 0, W, true, 8, false, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, true> : k_spmv_xsort<false, 0, W, true>;
     } else {
         kern = b ? k_spmv_xsort<true, 0, W, false> : k_spmv_xsort<false, 0, W, false>;
@@ -683,6 +805,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
     if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
         if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
+        else if (P.pair && P.dyn) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true> : k_spmv_xsort<false, 0, W, true, 8, true, true>;
         else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;
     }

@@ -25,9 +25,10 @@ pytestmark = pytest.mark.gpu
 ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"})]
+         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"})]
 ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide", "xsort_unpaired", "xsort_wg512"]
+            "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
