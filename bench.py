@@ -13,8 +13,12 @@ placement (strong scaling: the same matrix at every N).  The headline is
 cold-cache (a 1 GiB scrub before each of the K
 timed steps, so that at N = 8 a rank's ~67 MB slice cannot sit in the 256 MB
 Infinity Cache; each step between its own barrier + synchronize pair, the
-scrub outside the timed region); the warm number (K back-to-back steps
-between one barrier pair) is reported beside it under `warm`.
+scrub outside the timed region).  A cold step's time is its device span: HIP
+events on the launch stream from before the kernel to after the exchange and
+merge, max over ranks (the host's barrier round trips between scrub and step
+are reported beside as `cold_host_wall_ms_per_step`).  The warm number (K
+back-to-back steps between one barrier pair, host wall clock) is reported
+beside it under `warm`.
 
   python bench.py [--gpus N --steps K --warmup W] [--algo auto|xsort|panel|rowsplit|csr5]
                   [--cache cold|warm] [--partition cyclic|nnz]
@@ -211,6 +215,8 @@ def main() -> int:
         if ev is not None:
             ev[1].record(stream)
         op.exchange(sp)
+        if ev is not None:
+            ev[2].record(stream)  # after the collective and the device merge
 
     scrub = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
 
@@ -220,28 +226,41 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def events():
+        return [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+                for _ in range(args.steps)]
+
     def run_warm():
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
+        # the contract's timed region: K back-to-back steps between barrier +
+        # synchronize, host wall clock
+        evs = events()
         sync_barrier()
         t0 = time.perf_counter()
         for k in range(args.steps):
             step(evs[k])
         sync_barrier()
-        return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
 
     def run_cold():
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        el = 0.0
+        # every step starts from scrubbed caches, so the steps cannot run back
+        # to back: each is timed on the device, HIP events on its stream from
+        # before the kernel to after the exchange + merge (a rank that waits
+        # in the collective for a slower one counts that wait); the host
+        # barrier that separates scrub and step is not part of the step.
+        # The host wall clock around each step is kept beside (wall_el).
+        evs = events()
+        wall_el = 0.0
         for k in range(args.steps):
             scrub.add_(1)  # 1 GiB read+write: evicts MALL (256 MB) and L2
             sync_barrier()
             t0 = time.perf_counter()
             step(evs[k])
             sync_barrier()
-            el += time.perf_counter() - t0
-        return el, float(np.mean([a.elapsed_time(b) for a, b in evs]))
+            wall_el += time.perf_counter() - t0
+        run_cold.wall_el = wall_el
+        el = float(np.sum([a.elapsed_time(c) for a, _, c in evs])) * 1e-3
+        return el, float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    run_cold.wall_el = 0.0
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -273,7 +292,8 @@ def main() -> int:
             bound = orc.spmv_bound(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
             check = bool(np.all(np.abs(y_dev - want) <= bound))
     stats_dev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
-    stats = torch.tensor([el, kern_ms, local_bytes, local_flops, el_o, kern_o], dtype=torch.float64,
+    stats = torch.tensor([el, kern_ms, local_bytes, local_flops, el_o, kern_o, run_cold.wall_el],
+                         dtype=torch.float64,
                          device=stats_dev)
     if dist is not None:
         mx = stats.clone()
@@ -282,9 +302,11 @@ def main() -> int:
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         el, kern_ms_max = float(mx[0]), float(mx[1])
         el_o, kern_o_max = float(mx[4]), float(mx[5])
+        cold_wall = float(mx[6])
         tot_bytes = float(sm[2])
     else:
         kern_ms_max, tot_bytes, kern_o_max = kern_ms, float(local_bytes), kern_o
+        cold_wall = run_cold.wall_el
     ms_step = el / args.steps * 1e3
     total_flops = 2.0 * nnz
 
@@ -330,6 +352,9 @@ def main() -> int:
             "algorithmic_bytes_all_ranks": int(tot_bytes),
             "host_gen_s": round(t_gen, 2),
             "cache": args.cache,
+            # cold steps are timed on the device (run_cold); the host wall
+            # clock around each, barrier round trips included, for comparison
+            "cold_host_wall_ms_per_step": round(cold_wall / args.steps * 1e3, 5),
             ("warm" if args.cache == "cold" else "cold"): {
                 "value": round(total_flops / (el_o / args.steps) / 1e9, 3),
                 "ms_per_step": round(el_o / args.steps * 1e3, 5),
