@@ -23,7 +23,7 @@ beside it under `warm`.
   python bench.py [--gpus N --steps K --warmup W] [--algo auto|xsort|panel|rowsplit|csr5]
                   [--cache cold|warm] [--partition cyclic|nnz]
 
-Default kernel (`auto`): `xsort` while a rank holds >= 12M nonzeros (N <= 2
+Default kernel (`auto`): `xsort` while a rank holds >= 8M nonzeros (N <= 4
 for config 2), else `panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
 (row range x column group) blocks, column groups dealt to the XCDs so every
 x gather stays in the XCD's own L2, lane-consecutive gathers, LDS fp64 row
@@ -113,7 +113,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--algo", choices=["auto", "rowsplit", "csr5", "panel", "xsort"], default="auto",
-                    help="auto (default): xsort when a rank holds >= 12M nonzeros, else panel "
+                    help="auto (default): xsort when a rank holds >= 8M nonzeros, else panel "
                          "(s-blas_amd/tools/bench_slice.py: per-rank kernel times at N = 1..8)")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
@@ -173,8 +173,8 @@ def main() -> int:
     if args.algo == "auto":
         # the column-sorted kernel's per-item costs (padding to 256-entry
         # chunks, item set-up) pay off on large slices; the XCD-panel row
-        # split wins below ~12M nonzeros per rank
-        args.algo = "xsort" if nnz / world >= 12e6 else "panel"
+        # split wins below ~8M nonzeros per rank
+        args.algo = "xsort" if nnz / world >= 8e6 else "panel"
     algo = algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
