@@ -37,7 +37,9 @@
 // the 1024-thread workgroup (8 waves and 8192 LDS rows each) run them side by
 // side and every CU mixes both kinds of traffic.  Items sit in one queue per
 // XCD; a persistent grid claims from its own XCD's queue (XCC_ID hardware
-// register) and steals when it runs dry.
+// register) and steals when it runs dry.  Inside an item the waves claim
+// chunks from LDS counters (xs_stream_dyn), so a team that drains its own
+// sub-item continues on its partner's and both halves end together.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
