@@ -247,14 +247,27 @@ def main() -> int:
         # before the kernel to after the exchange + merge (a rank that waits
         # in the collective for a slower one counts that wait); the host
         # barrier that separates scrub and step is not part of the step.
-        # The host wall clock around each step is kept beside (wall_el).
+        # A short device-side spin queued ahead of the start event lets the
+        # host enqueue the whole step before the stream reaches it, so the
+        # events see device time, not the host's launch latency (with the
+        # stream idle after the barrier, the start event would fire at once
+        # and the kernel arrive ~10 us later: rocprofv3's kernel trace of the
+        # same command reads ~12 us less than unpadded events did).
+        # The host wall clock around each cold step is measured in a second,
+        # spin-free pass and kept beside (wall_el).
         evs = events()
-        wall_el = 0.0
         for k in range(args.steps):
             scrub.add_(1)  # 1 GiB read+write: evicts MALL (256 MB) and L2
             sync_barrier()
-            t0 = time.perf_counter()
+            torch.cuda._sleep(500_000)
             step(evs[k])
+            sync_barrier()
+        wall_el = 0.0
+        for k in range(args.steps):
+            scrub.add_(1)
+            sync_barrier()
+            t0 = time.perf_counter()
+            step()
             sync_barrier()
             wall_el += time.perf_counter() - t0
         run_cold.wall_el = wall_el
