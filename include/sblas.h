@@ -90,6 +90,17 @@ int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx,
                           const double *b, const double *x_ref, double *gflops,
                           int ngpu);
 
+/* sptrsv_v3's overload (sptrsv/sptrsv_v3/src/sptrsv_syncfree_cuda.h:227-241):
+ * the columns are cut into ngpu*task equal-count tasks, task d runs on device
+ * d % ngpu (round robin, :276-400).  One process drives all devices (the
+ * reference: one MPI rank per PE over NVSHMEM); tasks run as concurrent
+ * blocks of the multi-device pull executor.  Prints v3's lines. */
+int sblas_sptrsv_syncfree_v3(const int *cscColPtr, const int *cscRowIdx,
+                             const double *cscVal, int m, int n, int nnz,
+                             int substitution, int rhs, int opt, double *x,
+                             const double *b, const double *x_ref, double *gflops,
+                             int ngpu, int task);
+
 /* ------------------------------------------------------------------------ */
 /* 2. Persistent device API. */
 typedef struct sblas_csr_s *sblas_csr;
@@ -175,11 +186,19 @@ int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const i
  * HOST CSC in, x out.  nnz-balanced blocks of the solve order, one per device
  * ordinal (d % count); full-length x per device in fine-grained memory;
  * producers push x_i to every later block over xGMI; consumers poll local
- * memory.  b, x: n x rhs row-major (x[i*rhs+k], the reference's layout).
+ * memory.  Blocks that wrap onto one GPU run concurrently (own streams).  b, x: n x rhs row-major (x[i*rhs+k], the reference's layout).
  * solve_ms (optional) = wall time of the kernels. */
 int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val,
                           int n, int substitution, int rhs, const double *b, double *x,
                           int ngpu, double *solve_ms);
+/* Same executor over ngpu*tasks blocks, block d on device d % ngpu (wrapping
+ * onto the visible GPUs); balance 0 = nnz-balanced blocks, 1 = equal row
+ * counts (sptrsv_v3's split).  All blocks are launched on their own streams
+ * before any is waited for, so blocks sharing a GPU run concurrently (each
+ * with that GPU's workgroup budget divided by its block count). */
+int sblas_trsv_mgpu_solve_tasks(const int *colptr, const int *rowidx, const double *val,
+                                int n, int substitution, int rhs, const double *b, double *x,
+                                int ngpu, int tasks, int balance, double *solve_ms);
 
 /* Multi-partition y assembly after an allgather of padded slices: partition
  * r's slice starts at d_gathered + r*stride; d_meta (DEVICE, 3*g ints) holds
@@ -205,7 +224,11 @@ int sblas_assemble_cyclic(const double *d_gathered, int g, long long stride,
 /* Host utilities (no GPU needed). */
 /* Matrix-Market: mode 0 = full mmio_data semantics (symmetric expansion,
  * pattern -> 1.0); mode 1 = test_spmv 'f' loader (file order, Q1/Q2);
- * mode 2 = test_spmv 'b' (values 1e-5).  Call with rowptr==NULL to size. */
+ * mode 2 = test_spmv 'b' (values 1e-5); mode 3 = test_spmm's loader
+ * (dspmm_baseline_test.cu:420-455: "%d %d %lg" entries, no symmetric
+ * expansion) bucketed by row stably, file order within a row (feed it to
+ * sblas_coo_sortbyrow for the reference's (row, col) order).  Call with
+ * rowptr==NULL to size. */
 int sblas_mm_read(const char *path, int mode, int *m, int *n, long long *nnz,
                   long long *rowptr, int *col, double *val);
 /* Binary CSR cache.  sblas_mm_read keeps one automatically
@@ -216,6 +239,12 @@ int sblas_csrbin_write(const char *path, int m, int n, long long nnz, const long
                        const int *col, const double *val);
 int sblas_csrbin_read(const char *path, int *m, int *n, long long *nnz, long long *rowptr,
                       int *col, double *val);
+
+/* sortbyrow + COO -> CSR of test_spmm (spmm/test/dspmm_baseline_test.cu:
+ * 41-55, 461-493): row/col/val (nnz entries) sorted in place by (row, col),
+ * rowptr[m+1] filled from the row counts.  Duplicates keep their input order
+ * (the reference's qsort leaves it unspecified). */
+int sblas_coo_sortbyrow(int m, long long nnz, int *row, int *col, double *val, int *rowptr);
 
 /* nnz-balanced partition of spMV_mgpu_v1 (dspmv_mgpu_v1.cu:60-94, Q5 fixed).
  * Arrays of g entries. */

@@ -5,6 +5,7 @@
  *   spmv/include/spmv_kernel.h:11-36    (spMV_mgpu_baseline/v1/v2, helpers)
  *   spmm/include/spmm_kernel.h:6-31     (cusparse_mgpu_csrmm[_omp])
  *   sptrsv/sptrsv_v1/src/sptrsv_syncfree_cuda.h:287-300 (sptrsv_syncfree_cuda)
+ *   sptrsv/sptrsv_v3/src/sptrsv_syncfree_cuda.h:227-241 (its `int task` overload)
  *   sptrans/sptrans_v1/src/sptrans_cuda.h:11-23, sptrans_kernal.h:80-93
  *                                       (cuda_sptrans, kernal_sptrans)
  * Each forwards to the extern "C" sblas_* entry of the same arguments
@@ -40,6 +41,12 @@ int sptrsv_syncfree_cuda(const int *cscColPtrTR, const int *cscRowIdxTR,
                          const double *cscValTR, int m, int n, int nnzTR, int substitution,
                          int rhs, int opt, double *x, const double *b, const double *x_ref,
                          double *gflops, int ngpu);
+/* sptrsv/sptrsv_v3/src/sptrsv_syncfree_cuda.h:227-241: ngpu*task
+ * equal-column tasks, task d on device d % ngpu (single process here). */
+int sptrsv_syncfree_cuda(const int *cscColPtrTR, const int *cscRowIdxTR,
+                         const double *cscValTR, int m, int n, int nnzTR, int substitution,
+                         int rhs, int opt, double *x, const double *b, const double *x_ref,
+                         double *gflops, int ngpu, int task);
 
 int cuda_sptrans(const int m, const int n, const int nnz, const int *csrRowPtr,
                  const int *csrColIdx, const double *csrVal, int *cscRowIdx, int *cscColPtr,

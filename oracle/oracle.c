@@ -182,6 +182,21 @@ void orc_csr_spmv_omp(int m, const long long *rowptr, const int *col,
     }
 }
 
+void orc_spmv_bound(int m, const long long *rowptr, const int *col, const double *val,
+                    const double *x, double alpha, double beta, const double *y0,
+                    double *bound)
+{
+    const double u = 0x1p-53;
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int i = 0; i < m; ++i) {
+        double s = 0.0;
+        for (long long j = rowptr[i]; j < rowptr[i + 1]; ++j) s += fabs(alpha * val[j] * x[col[j]]);
+        const double k = (double)(rowptr[i + 1] - rowptr[i]);
+        const double gam = k * u / (1.0 - k * u);
+        bound[i] = 4.0 * gam * s + 4.0 * u * fabs(beta * y0[i]) + 1e-300;
+    }
+}
+
 int orc_get_row_from_index_ref(int n, const long long *a, long long idx)
 {
     /* spmv_helper.cu:16-39: bisection that returns on the first equal key */
@@ -512,6 +527,45 @@ void orc_spmm(int m, int n, int k, double alpha, const int *rowptr,
             double *o = C + (long long)c * ldc + i;
             *o = (beta == 0.0) ? alpha * s : alpha * s + beta * *o;
         }
+}
+
+void orc_spmm_omp(int m, int n, double alpha, const int *rowptr, const int *col,
+                  const double *val, const double *B, int ldb, int b_rowmajor, double beta,
+                  double *C, int ldc, double *bound, int nthreads)
+{
+    const double u = 0x1p-53;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+    {
+        /* per (row, column of C) the sum runs over the row's entries in
+         * storage order, as orc_spmm; the column loop is inside so B rows
+         * are read contiguously when B is row-major */
+        double *s = (double *)malloc(sizeof(double) * 2 * (size_t)(n > 0 ? n : 1));
+        double *a = s + n;
+#pragma omp for schedule(dynamic, 4)
+        for (int i = 0; i < m; ++i) {
+            const double k = (double)(rowptr[i + 1] - rowptr[i]);
+            const double gam = k * u / (1.0 - k * u);
+            for (int c = 0; c < n; ++c) s[c] = a[c] = 0.0;
+            for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) {
+                const double v = val[j];
+                for (int c = 0; c < n; ++c) {
+                    const double b = b_rowmajor ? B[(long long)col[j] * ldb + c]
+                                                : B[(long long)c * ldb + col[j]];
+                    s[c] += v * b;
+                    a[c] += fabs(alpha * v * b);
+                }
+            }
+            for (int c = 0; c < n; ++c) {
+                double *o = C + (long long)c * ldc + i;
+                if (bound) bound[(long long)c * ldc + i] = 4.0 * gam * a[c] + 4.0 * u * fabs(beta * *o) + 1e-300;
+                *o = (beta == 0.0) ? alpha * s[c] : alpha * s[c] + beta * *o;
+            }
+        }
+        free(s);
+    }
 }
 
 typedef struct { int r, c; double v; } coo_t;

@@ -58,6 +58,12 @@ void orc_csr_spmv(int m, const long long *rowptr, const int *col,
 void orc_csr_spmv_omp(int m, const long long *rowptr, const int *col,
                       const double *val, const double *x, double alpha,
                       double beta, double *y, int nthreads);
+/* Checker helper (tests only): the per-row fp64 bound of DESIGN.md §3,
+ * bound[i] = 4*gamma_k*sum_j |alpha*a_ij*x_j| + 4u*|beta*y0[i]| + 1e-300,
+ * gamma_k = k*u/(1-k*u), u = 2^-53, k = row length.  OpenMP over rows. */
+void orc_spmv_bound(int m, const long long *rowptr, const int *col, const double *val,
+                    const double *x, double alpha, double beta, const double *y0,
+                    double *bound);
 
 /* The reference's binary search, verbatim semantics (spmv_helper.cu:16-39). */
 int orc_get_row_from_index_ref(int n, const long long *a, long long idx);
@@ -136,6 +142,15 @@ int orc_levels_lower(int n, const int *colptr, const int *rowidx, int *level_of)
 void orc_spmm(int m, int n, int k, double alpha, const int *rowptr,
               const int *col, const double *val, const double *B, int ldb,
               double beta, double *C, int ldc);
+/* orc_spmm's arithmetic (same per-entry storage-order sum) in OpenMP over
+ * rows, for full-size checks; if bound != NULL also the per-entry fp64 bound
+ * (ld = ldc) 4*gamma_k*sum_j |alpha*a_ij*b_jc| + 4u*|beta*c0|, computed
+ * from the C passed in (before it is overwritten).  B is read with stride
+ * ldb per column when b_rowmajor == 0 (column-major, ld = ldb) and as
+ * B[j*ldb + c] when b_rowmajor != 0. */
+void orc_spmm_omp(int m, int n, double alpha, const int *rowptr, const int *col,
+                  const double *val, const double *B, int ldb, int b_rowmajor, double beta,
+                  double *C, int ldc, double *bound, int nthreads);
 
 /* qsort-by-(row,col) COO -> CSR as test_spmm does
  * (spmm/test/dspmm_baseline_test.cu:41-55,461-493). */

@@ -331,7 +331,7 @@ int parse_entries(const MMFile &F, int mode, const char *path, std::vector<int> 
                     } else {
                         v = 1.0;
                     }
-                } else if (mode == 1) {
+                } else if (mode == 1 || mode == 3) {
                     ok = (p = parse_dbl(p, v)) != nullptr;
                 } else {
                     v = 0.00001;
@@ -395,7 +395,7 @@ int mm_to_csr(const MMFile &F, int mode, const char *path, HostCsr &A)
     A.n = F.n;
     A.nnz = cnt[(size_t)F.m];
     A.rowptr = cnt;
-    if (mode != 0) {
+    if (mode == 1 || mode == 2) {
         // Q1: col/val keep FILE order; only the row counts build rowptr.
         A.col = std::move(ci);
         A.val = std::move(vi);
@@ -471,6 +471,8 @@ int sblas_get_row_from_index(int n, long long *a, long long idx)
 
 // mode 0: mmio_data (sptrsv_v1/src/mmio_highlevel.h:137-296)
 // mode 1/2: test_spmv 'f'/'b' loader (spmv/test/dspmv_test.cu:101-136,217-251)
+// mode 3: test_spmm loader (spmm/test/dspmm_baseline_test.cu:420-455), rows
+//         bucketed stably (the row order sortbyrow then refines by column)
 //
 // the entries are parsed in parallel (OpenMP, one chunk of
 // whole lines per thread, concatenated in file order, so the result is
@@ -481,7 +483,7 @@ int sblas_get_row_from_index(int n, long long *a, long long idx)
 int sblas_mm_read(const char *path, int mode, int *m, int *n, long long *nnz,
                   long long *rowptr, int *col, double *val)
 {
-    if (!path || !m || !n || !nnz || mode < 0 || mode > 2) return SBLAS_ERR_INVALID;
+    if (!path || !m || !n || !nnz || mode < 0 || mode > 3) return SBLAS_ERR_INVALID;
     HostCsr *A = memo_lookup(path, mode);
     if (!A) {
         const int st = load_matrix(path, mode, memo_slot(path, mode));
@@ -695,6 +697,55 @@ int sblas_gen_vector(int n, unsigned long long seed, double *v)
     if (n < 0 || !v) return SBLAS_ERR_INVALID;
     unsigned long long s = seed;
     for (int i = 0; i < n; ++i) v[i] = to_u01(splitmix(s));
+    return SBLAS_OK;
+}
+
+// sortbyrow + CSR build of test_spmm (spmm/test/dspmm_baseline_test.cu:41-55,
+// 461-493): COO sorted by (row, col) in place, rowptr[m+1] from row counts.
+// The reference's qsort is unstable, so it leaves the order of duplicate
+// (row, col) entries unspecified; here it is their input order (stable
+// counting sort by row, then a stable sort by column inside each row).
+// Rows outside [0, m) are rejected.
+int sblas_coo_sortbyrow(int m, long long nnz, int *row, int *col, double *val, int *rowptr)
+{
+    if (m < 0 || nnz < 0 || (nnz && (!row || !col || !val)) || !rowptr) return SBLAS_ERR_INVALID;
+    if (nnz >= (1LL << 31)) return SBLAS_ERR_UNSUPPORTED;
+    std::vector<long long> start((size_t)m + 1, 0);
+    for (long long i = 0; i < nnz; ++i) {
+        if (row[i] < 0 || row[i] >= m) return SBLAS_ERR_INVALID;
+        start[(size_t)row[i] + 1]++;
+    }
+    for (int r = 0; r < m; ++r) start[(size_t)r + 1] += start[(size_t)r];
+    std::vector<int> c2((size_t)nnz);
+    std::vector<double> v2((size_t)nnz);
+    {
+        std::vector<long long> pos(start.begin(), start.end() - 1);
+        for (long long i = 0; i < nnz; ++i) {
+            const long long p = pos[(size_t)row[i]]++;
+            c2[(size_t)p] = col[i];
+            v2[(size_t)p] = val[i];
+        }
+    }
+#pragma omp parallel
+    {
+        std::vector<std::pair<int, double>> t;
+#pragma omp for schedule(dynamic, 256)
+        for (int r = 0; r < m; ++r) {
+            const long long a = start[(size_t)r], b = start[(size_t)r + 1];
+            t.resize((size_t)(b - a));
+            for (long long k = a; k < b; ++k) t[(size_t)(k - a)] = {c2[(size_t)k], v2[(size_t)k]};
+            std::stable_sort(t.begin(), t.end(),
+                             [](const std::pair<int, double> &u, const std::pair<int, double> &v) {
+                                 return u.first < v.first;
+                             });
+            for (long long k = a; k < b; ++k) {
+                row[k] = r;
+                col[k] = t[(size_t)(k - a)].first;
+                val[k] = t[(size_t)(k - a)].second;
+            }
+        }
+    }
+    for (int r = 0; r <= m; ++r) rowptr[r] = (int)start[(size_t)r];
     return SBLAS_OK;
 }
 

@@ -333,12 +333,67 @@ int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const doub
 }
 
 
+// sptrsv_v3's driver (sptrsv_v3/src/sptrsv_syncfree_cuda.h:227-612): the
+// columns are cut into ngpu*task equal-count tasks (:276-300) and task d runs
+// on PE d % ngpu (:390-400, round robin).  The reference runs one MPI rank
+// per PE over NVSHMEM; here one process drives the ngpu devices and every
+// task is its own concurrently running block of the multi-device pull
+// executor (x pushed to later tasks' fine-grained copies, over xGMI between
+// GPUs).  Prints v3's lines; validation against x_ref as v1.
+int sblas_sptrsv_syncfree_v3(const int *cscColPtr, const int *cscRowIdx, const double *cscVal,
+                             int m, int n, int nnz, int substitution, int rhs, int opt, double *x,
+                             const double *b, const double *x_ref, double *gflops, int ngpu,
+                             int task)
+{
+    (void)opt;
+    if (m != n) {
+        printf("This is not a square matrix, return.\n");
+        return -1;
+    }
+    if (rhs <= 0 || n < 0 || nnz < 0 || ngpu <= 0 || task <= 0 || !cscColPtr || !x || !b)
+        return SBLAS_ERR_INVALID;
+    int count;
+    if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
+    const int T = ngpu * task;
+    for (int d = 0; d < T; ++d) {
+        const int c0 = (int)((long long)d * m / T), c1 = (int)((long long)(d + 1) * m / T);
+        printf("start from %d value, has %d nnz for device %d\n", cscColPtr[c0],
+               cscColPtr[c1] - cscColPtr[c0], d);
+    }
+    double warm = 0.0, ms = 0.0;
+    SBLAS_TRY(sblas_trsv_mgpu_solve_tasks(cscColPtr, cscRowIdx, cscVal, n, substitution, rhs, b, x,
+                                          ngpu, task, 1, &warm));
+    SBLAS_TRY(sblas_trsv_mgpu_solve_tasks(cscColPtr, cscRowIdx, cscVal, n, substitution, rhs, b, x,
+                                          ngpu, task, 1, &ms));
+    const double flop = 2.0 * rhs * (double)nnz;
+    printf("device:%d --\n", 0);
+    printf("cuda syncfree SpTRSV solve used %4.2f ms, throughput is %4.2f gflops\n", ms,
+           flop / (1e6 * ms));
+    if (gflops) *gflops = flop / (1e6 * ms);
+    if (x_ref) {
+        double ref = 0.0, res = 0.0;
+        for (long long i = 0; i < (long long)n * rhs; ++i) {
+            ref += std::fabs(x_ref[i]);
+            res += std::fabs(x[i] - x_ref[i]);
+        }
+        res = ref == 0 ? res : res / ref;
+        printf("device:%d cuda syncfree SpTRSV executor %s |x-xref|/|xref| = %8.2e\n", 0,
+               res < 1e-4 ? "passed!" : "_NOT_ passed!", res);
+    }
+    return SBLAS_OK;
+}
+
 // cuda_sptrans / kernal_sptrans (sptrans/sptrans_v1/src/sptrans_cuda.h:11-220,
 // sptrans_kernal.h:80-555): transpose, print the timing lines, compare with
 // the reference CSC the driver computed on the CPU (main.cu:150-200).
-int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const int *csrColIdx,
-                  const double *csrVal, int *cscRowIdx, int *cscColPtr, double *cscVal,
-                  const int *cscRowIdx_ref, const int *cscColPtr_ref, const double *cscVal_ref)
+}  // extern "C"
+
+// multi_lines: print kernal_sptrans's multi-GPU lines (it prints them for any
+// ngpu, sptrans_kernal.h:470-520); otherwise cuda_sptrans's single-GPU form.
+static int sptrans_report(int m, int n, int nnz, int ngpu, bool multi_lines, const int *csrRowPtr,
+                          const int *csrColIdx, const double *csrVal, int *cscRowIdx, int *cscColPtr,
+                          double *cscVal, const int *cscRowIdx_ref, const int *cscColPtr_ref,
+                          const double *cscVal_ref)
 {
     double t_tr = 0.0, t_co = 0.0;
     const int st = sblas_csr2csc_mgpu(m, n, nnz, ngpu, csrRowPtr, csrColIdx, csrVal, cscColPtr,
@@ -347,8 +402,8 @@ int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const i
         printf("sptrans failed: %s\n", sblas_last_error());
         return st;
     }
-    const char *where = ngpu == 1 ? "single GPU" : "multiple GPU";
-    if (ngpu == 1) {
+    const char *where = multi_lines ? "multiple GPU" : "single GPU";
+    if (!multi_lines) {
         printf("HIP trans used %4.2f ms,\n", t_tr + t_co);
     } else {
         printf("HIP transposition on multiple gpu used %4.8f ms,\n", t_tr);
@@ -383,6 +438,16 @@ int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const i
                bad == 0 ? "passed!" : "_NOT_ passed!", bad);
     }
     return SBLAS_OK;
+}
+
+extern "C" {
+
+int sblas_sptrans(int m, int n, int nnz, int ngpu, const int *csrRowPtr, const int *csrColIdx,
+                  const double *csrVal, int *cscRowIdx, int *cscColPtr, double *cscVal,
+                  const int *cscRowIdx_ref, const int *cscColPtr_ref, const double *cscVal_ref)
+{
+    return sptrans_report(m, n, nnz, ngpu, ngpu > 1, csrRowPtr, csrColIdx, csrVal, cscRowIdx,
+                          cscColPtr, cscVal, cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
 }
 
 }  // extern "C"
@@ -436,13 +501,21 @@ int sptrsv_syncfree_cuda(const int *cscColPtrTR, const int *cscRowIdxTR, const d
                                  opt, x, b, x_ref, gflops, ngpu);
 }
 
+int sptrsv_syncfree_cuda(const int *cscColPtrTR, const int *cscRowIdxTR, const double *cscValTR,
+                         int m, int n, int nnzTR, int substitution, int rhs, int opt, double *x,
+                         const double *b, const double *x_ref, double *gflops, int ngpu, int task)
+{
+    return sblas_sptrsv_syncfree_v3(cscColPtrTR, cscRowIdxTR, cscValTR, m, n, nnzTR, substitution,
+                                    rhs, opt, x, b, x_ref, gflops, ngpu, task);
+}
+
 int cuda_sptrans(const int m, const int n, const int nnz, const int *csrRowPtr,
                  const int *csrColIdx, const double *csrVal, int *cscRowIdx, int *cscColPtr,
                  double *cscVal, const int *cscRowIdx_ref, const int *cscColPtr_ref,
                  const double *cscVal_ref)
 {
-    return sblas_sptrans(m, n, nnz, 1, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr, cscVal,
-                         cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
+    return sptrans_report(m, n, nnz, 1, false, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr,
+                          cscVal, cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
 }
 
 int kernal_sptrans(const int m, const int n, const int nnz, int ngpu, const int *csrRowPtr,
@@ -450,6 +523,6 @@ int kernal_sptrans(const int m, const int n, const int nnz, int ngpu, const int 
                    double *cscVal, const int *cscRowIdx_ref, const int *cscColPtr_ref,
                    const double *cscVal_ref)
 {
-    return sblas_sptrans(m, n, nnz, ngpu, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr,
-                         cscVal, cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
+    return sptrans_report(m, n, nnz, ngpu, true, csrRowPtr, csrColIdx, csrVal, cscRowIdx, cscColPtr,
+                          cscVal, cscRowIdx_ref, cscColPtr_ref, cscVal_ref);
 }

@@ -24,6 +24,7 @@
 //     iteration, so rows that depend on rows of the same wave resolve across
 //     iterations.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -55,7 +56,22 @@ constexpr unsigned kSpinLimit = 1u << 25;  // ~1 s of polling per wave
 // control block: ticket counter at word 0, abort/timeout word on its own
 // 128-B line (word 32) -- polling it next to the hot ticket atomics is slow
 constexpr int kAbort = 32;
-constexpr int kCtlBytes = 256;
+// multi-device blocks: first-start / last-exit timestamps (s_memrealtime,
+// 100 MHz) as 64-bit words on a third line, so a test can see that blocks
+// sharing a GPU overlap in time; start is kept as (~0 - t) under atomicMax
+constexpr int kTStart64 = 32, kTEnd64 = 33;
+constexpr int kCtlBytes = 384;
+
+__device__ __forceinline__ void stamp_start(unsigned *ctl)
+{
+    if (threadIdx.x == 0)
+        atomicMax((unsigned long long *)ctl + kTStart64,
+                  ~0ULL - (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void stamp_end(unsigned *ctl)
+{
+    atomicMax((unsigned long long *)ctl + kTEnd64, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
 
 __device__ __forceinline__ int ld_sc1_i32(const int *p)
 {
@@ -271,11 +287,15 @@ __global__ __launch_bounds__(256) void k_trsv_pull_part(const TrsvPart P, unsign
     constexpr int kBatch = 8;
     const int lane = threadIdx.x & 63;
     unsigned long long *xl = P.xs[P.d];
+    stamp_start(ctl);
     for (;;) {
         int t0 = 0;
         if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? P.nloc : (int)atomicAdd(&ctl[0], 64u);
         t0 = __shfl(t0, 0, 64);
-        if (t0 >= P.nloc) return;
+        if (t0 >= P.nloc) {
+            if (lane == 0) stamp_end(ctl);
+            return;
+        }
         const int t = t0 + lane;
         const bool live = t < P.nloc;
         const int o = P.o0 + (live ? t : 0);
@@ -379,11 +399,15 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
     const int lane = threadIdx.x & 63;
     const int slot = lane / RP, kl = lane % RP;
     const unsigned long long *xl = P.xown;
+    stamp_start(ctl);
     for (;;) {
         int t0 = 0;
         if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? P.nloc : (int)atomicAdd(&ctl[0], (unsigned)R);
         t0 = __shfl(t0, 0, 64);
-        if (t0 >= P.nloc) return;
+        if (t0 >= P.nloc) {
+            if (lane == 0) stamp_end(ctl);
+            return;
+        }
         const int t = t0 + slot;
         const bool live = t < P.nloc;
         const int o = P.o0 + (live ? t : 0);
@@ -639,17 +663,32 @@ int sblas_trsv_destroy(sblas_trsv T)
 }
 
 
+}  // extern "C"
+
+namespace {
+
 // Multi-device solve from HOST CSC (diagonal first / last per column as in the
-// reference).  Returns x on the host.  Partition d's rows run on ordinal
-// d % count; partitions sharing a GPU run in order on that GPU's stream,
-// different GPUs run concurrently (peer access + fine-grained x).
-int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val, int n,
-                          int substitution, int rhs, const double *b, double *x, int ngpu,
-                          double *solve_ms)
+// reference).  Returns x on the host.  nblocks blocks of the solve order;
+// block d runs on ordinal (d % ndev) % count.  balance 0 = nnz-balanced
+// blocks (sptrsv_v1/v2's intent), 1 = equal row counts (sptrsv_v3's
+// floor(d*m/(np*task)), sptrsv_v3/src/sptrsv_syncfree_cuda.h:276-300).
+// Every block has its own stream and all are launched before any is waited
+// for, so blocks that share a GPU run CONCURRENTLY like blocks on different
+// GPUs: each gets grid_for(dev) / (blocks on dev) workgroups, so the blocks
+// of one device are co-resident.  Launches go in block order; a block only
+// waits for lower blocks, which were enqueued first on every hardware queue,
+// so streams sharing a queue cannot deadlock.  SBLAS_TRSV_MGPU_SERIAL=1 runs
+// the blocks of one device in order on one stream instead (A/B timing).
+static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *val, int n,
+                          int substitution, int rhs, const double *b, double *x, int nblocks,
+                          int ndev, int balance, double *solve_ms)
 {
-    if (n < 0 || ngpu <= 0 || rhs <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
+    if (n < 0 || nblocks <= 0 || ndev <= 0 || rhs <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
+    const int ngpu = nblocks;
+    const bool serial = getenv("SBLAS_TRSV_MGPU_SERIAL") && atoi(getenv("SBLAS_TRSV_MGPU_SERIAL")) != 0;
+    const bool trace = getenv("SBLAS_TRSV_TRACE") != nullptr;
     const int nnz = colptr[n];
     const bool bwd = substitution == 1;
     // CSC of L == CSR of L^T; stable transpose gives CSR of L with columns
@@ -671,7 +710,9 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
     auto row_of = [&](int o) { return bwd ? n - 1 - o : o; };
     std::vector<int> ob(ngpu + 1, n);
     ob[0] = 0;
-    {
+    if (balance == 1) {
+        for (int d = 1; d < ngpu; ++d) ob[d] = (int)((long long)d * n / ngpu);
+    } else {
         long long acc = 0;
         int d = 1;
         for (int o = 0; o < n && d < ngpu; ++o) {
@@ -690,7 +731,7 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
         unsigned *ctl = nullptr;
     };
     std::vector<Dev> D(ngpu);
-    std::vector<hipStream_t> streams(count, nullptr);
+    std::vector<hipStream_t> streams(ngpu, nullptr);  // per block
     int st = SBLAS_OK;
     auto cleanup = [&]() {
         for (auto &q : D) {
@@ -703,10 +744,10 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
             (void)hipFree(q.xs);
             (void)hipFree(q.ctl);
         }
-        for (int p = 0; p < count; ++p)
-            if (streams[p]) {
-                DeviceGuard g(p);
-                (void)hipStreamDestroy(streams[p]);
+        for (int d = 0; d < ngpu; ++d)
+            if (streams[d]) {
+                DeviceGuard g(D[d].phys);
+                (void)hipStreamDestroy(streams[d]);
             }
     };
 #define MG(expr)                                                               \
@@ -718,11 +759,23 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
             return SBLAS_ERR_HIP;                                              \
         }                                                                      \
     } while (0)
-    for (int d = 0; d < ngpu; ++d) D[d].phys = d % count;
-    for (int p = 0; p < std::min(count, ngpu); ++p) {
+    const int nphys = std::min(count, ndev);
+    std::vector<int> on_phys(count, 0), first_on(count, -1);
+    for (int d = 0; d < ngpu; ++d) {
+        D[d].phys = (d % ndev) % count;
+        on_phys[D[d].phys]++;
+        if (first_on[D[d].phys] < 0) first_on[D[d].phys] = d;
+    }
+    for (int d = 0; d < ngpu; ++d) {
+        // serial mode: the blocks of one device share its first block's stream
+        if (serial && first_on[D[d].phys] != d) continue;
+        DeviceGuard g(D[d].phys);
+        MG(hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking));
+    }
+    auto stream_of = [&](int d) { return streams[serial ? first_on[D[d].phys] : d]; };
+    for (int p = 0; p < nphys; ++p) {
         DeviceGuard g(p);
-        MG(hipStreamCreateWithFlags(&streams[p], hipStreamNonBlocking));
-        for (int q = 0; q < std::min(count, ngpu); ++q) {
+        for (int q = 0; q < nphys; ++q) {
             if (q == p) continue;
             int can = 0;
             if (hipDeviceCanAccessPeer(&can, p, q) == hipSuccess && can) {
@@ -771,32 +824,33 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
     // reset: sentinel x everywhere, zero control words
     for (int d = 0; d < ngpu; ++d) {
         DeviceGuard g(D[d].phys);
-        hipStream_t s = streams[D[d].phys];
+        hipStream_t s = stream_of(d);
         fill_pending(D[d].x, (long long)n * rhs, s);
         MG(hipMemsetAsync(D[d].ctl, 0, kCtlBytes, s));
     }
-    for (int p = 0; p < std::min(count, ngpu); ++p) {
-        DeviceGuard g(p);
-        MG(hipStreamSynchronize(streams[p]));
+    for (int d = 0; d < ngpu; ++d) {
+        DeviceGuard g(D[d].phys);
+        MG(hipStreamSynchronize(stream_of(d)));
     }
     const double t0 = sblas_get_time();
     for (int d = 0; d < ngpu; ++d) {
         Dev &q = D[d];
         DeviceGuard g(q.phys);
         const int nloc = ob[d + 1] - ob[d];
+        // co-resident blocks: the device's workgroup budget split between them
+        const int grid = serial ? grid_for(q.phys) : std::max(1, grid_for(q.phys) / on_phys[q.phys]);
         if (nloc > 0 && rhs == 1) {
             TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
-            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid_for(q.phys)), dim3(256), 0, streams[q.phys], P,
-                               q.ctl);
+            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, stream_of(d), P, q.ctl);
         } else if (nloc > 0) {
             TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0};
-            launch_trsm(P, q.ctl, grid_for(q.phys), streams[q.phys]);
+            launch_trsm(P, q.ctl, grid, stream_of(d));
         }
         MG(hipGetLastError());
     }
-    for (int p = 0; p < std::min(count, ngpu); ++p) {
-        DeviceGuard g(p);
-        MG(hipStreamSynchronize(streams[p]));
+    for (int d = 0; d < ngpu; ++d) {
+        DeviceGuard g(D[d].phys);
+        MG(hipStreamSynchronize(stream_of(d)));
     }
     if (solve_ms) *solve_ms = (sblas_get_time() - t0) * 1e3;
     for (int d = 0; d < ngpu && st == SBLAS_OK; ++d) {
@@ -809,6 +863,12 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
             st = SBLAS_ERR_HIP;
             break;
         }
+        if (trace && ob[d + 1] > ob[d]) {  // debugging aid: block d's span on its device's clock
+            const unsigned long long *h64 = (const unsigned long long *)h;
+            printf("trsv_block %d dev %d rows %d start_us %.3f end_us %.3f\n", d, q.phys,
+                   ob[d + 1] - ob[d], (double)(~0ULL - h64[kTStart64]) * 1e-2,
+                   (double)h64[kTEnd64] * 1e-2);
+        }
         // x rows of this block: contiguous rows in row space
         const int nloc = ob[d + 1] - ob[d];
         if (nloc == 0) continue;
@@ -818,5 +878,24 @@ int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *va
 #undef MG
     cleanup();
     return st;
+}
+}  // namespace
+
+extern "C" {
+
+int sblas_trsv_mgpu_solve(const int *colptr, const int *rowidx, const double *val, int n,
+                          int substitution, int rhs, const double *b, double *x, int ngpu,
+                          double *solve_ms)
+{
+    return trsv_mgpu_impl(colptr, rowidx, val, n, substitution, rhs, b, x, ngpu, ngpu, 0, solve_ms);
+}
+
+int sblas_trsv_mgpu_solve_tasks(const int *colptr, const int *rowidx, const double *val, int n,
+                                int substitution, int rhs, const double *b, double *x, int ngpu,
+                                int tasks, int balance, double *solve_ms)
+{
+    if (tasks <= 0 || ngpu <= 0 || (balance != 0 && balance != 1)) return SBLAS_ERR_INVALID;
+    return trsv_mgpu_impl(colptr, rowidx, val, n, substitution, rhs, b, x, ngpu * tasks, ngpu,
+                          balance, solve_ms);
 }
 }  // extern "C"

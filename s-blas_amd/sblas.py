@@ -84,6 +84,8 @@ _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
 _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
 _sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
+_sig("sblas_trsv_mgpu_solve_tasks", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _i, _i, _p)
+_sig("sblas_sptrsv_syncfree_v3", _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _i)
 _sig("sblas_spmv_ooc", _i, _i, _i, _ll, _d, _p, _p, _p, _p, _d, _p, _i, _ll, _i, _p)
 _sig("sblas_csr2csc_mgpu", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_sptrans", _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p)
@@ -94,6 +96,7 @@ _sig("sblas_csrbin_write", _i, C.c_char_p, _i, _i, _ll, _p, _p, _p)
 _sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)
+_sig("sblas_coo_sortbyrow", _i, _i, _ll, _p, _p, _p, _p)
 _sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
 _sig("sblas_gen_synth_rows", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _i, _i, _p, _p)
 _sig("sblas_gen_vector", _i, _i, C.c_ulonglong, _p)
@@ -127,7 +130,8 @@ def device_count() -> int:
 # --------------------------------------------------------------------------
 def mm_read(path: str, mode: int = 0):
     """Matrix-Market -> (m, n, rowptr int64, col int32, val f64).
-    mode 0 = mmio_data semantics, 1 = test_spmv 'f', 2 = test_spmv 'b'."""
+    mode 0 = mmio_data semantics, 1 = test_spmv 'f', 2 = test_spmv 'b',
+    3 = test_spmm's loader (rows bucketed stably, no symmetric expansion)."""
     m, n, nnz = C.c_int(), C.c_int(), C.c_longlong()
     check(lib.sblas_mm_read(path.encode(), mode, C.byref(m), C.byref(n), C.byref(nnz),
                             None, None, None), f"mm_read {path}")
@@ -168,6 +172,17 @@ def partition_nnz(rowptr: np.ndarray, g: int):
     check(lib.sblas_partition_nnz(m, nnz, ptr(rp), g, ptr(si), ptr(ei), ptr(sr), ptr(er), ptr(sf)),
           "partition_nnz")
     return si, ei, sr, er, sf
+
+
+def coo_sortbyrow(m: int, row, col, val):
+    """sortbyrow + COO -> CSR of test_spmm (sblas_coo_sortbyrow): returns
+    sorted (row, col, val) copies and the int32 rowptr."""
+    r = np.array(row, np.int32, copy=True)
+    c = np.array(col, np.int32, copy=True)
+    v = np.array(val, np.float64, copy=True)
+    rp = np.zeros(m + 1, np.int32)
+    check(lib.sblas_coo_sortbyrow(m, len(r), ptr(r), ptr(c), ptr(v), ptr(rp)), "coo_sortbyrow")
+    return r, c, v, rp
 
 
 def partition_rowblock(m: int, g: int) -> np.ndarray:
@@ -216,6 +231,24 @@ def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int
     ms = C.c_double(0.0)
     check(lib.sblas_trsv_mgpu_solve(ptr(cp), ptr(ri), ptr(v), n, substitution, rhs, ptr(bb),
                                     ptr(x), ngpu, C.byref(ms)), "trsv_mgpu_solve")
+    x = x[:n * rhs]
+    return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
+
+
+def trsv_mgpu_solve_tasks(colptr, rowidx, val, n: int, b, ngpu: int, tasks: int,
+                          substitution: int = 0, rhs: int = 1, balance: int = 1):
+    """ngpu*tasks concurrently running blocks, block d on device d % ngpu
+    (sblas_trsv_mgpu_solve_tasks; balance 1 = sptrsv_v3's equal-row split).
+    Returns (x, kernel ms)."""
+    cp = np.ascontiguousarray(colptr, np.int32)
+    ri = np.ascontiguousarray(rowidx, np.int32)
+    v = np.ascontiguousarray(val, np.float64)
+    bb = np.ascontiguousarray(b, np.float64)
+    x = np.zeros(max(n, 1) * rhs, np.float64)
+    ms = C.c_double(0.0)
+    check(lib.sblas_trsv_mgpu_solve_tasks(ptr(cp), ptr(ri), ptr(v), n, substitution, rhs, ptr(bb),
+                                          ptr(x), ngpu, tasks, balance, C.byref(ms)),
+          "trsv_mgpu_solve_tasks")
     x = x[:n * rhs]
     return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
 

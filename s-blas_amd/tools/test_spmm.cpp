@@ -3,7 +3,8 @@
 //   test_spmm <matrix.mtx> <ncols of B> <ngpu> <repeat (unused)>
 //
 // Loader: banner + "%d %d %lg" entries in file order (no symmetric
-// expansion), then sorted by (row, col) as sortbyrow does (:41-55).  B and C
+// expansion; sblas_mm_read mode 3), then sorted by (row, col) with
+// sblas_coo_sortbyrow as sortbyrow does (:41-55).  B and C
 // are rand()/RAND_MAX (unseeded), alpha = -0.7, beta = 0.8 (:518-519).  The
 // single-device run is the check target (the reference used single-GPU
 // cuSPARSE); the multi-device run is compared with abs 0.001 (:544-549).
@@ -12,7 +13,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
-#include <numeric>
 #include <vector>
 
 #include "../../include/sblas.h"
@@ -44,34 +44,25 @@ int main(int argc, char *argv[])
 
     int m = 0, k = 0;
     long long nnz64 = 0;
-    if (sblas_mm_read(filename_A, 1, &m, &k, &nnz64, nullptr, nullptr, nullptr) != SBLAS_OK) {
+    // mode 3: the test's own "%d %d %lg" loader (no symmetric expansion)
+    if (sblas_mm_read(filename_A, 3, &m, &k, &nnz64, nullptr, nullptr, nullptr) != SBLAS_OK) {
         cout << "Could not open matrix A file.\n";
         return -1;
     }
     vector<long long> rp64((size_t)m + 1);
-    vector<int> col((size_t)max(nnz64, 1LL));
+    vector<int> col((size_t)max(nnz64, 1LL)), row((size_t)max(nnz64, 1LL));
     vector<double> val((size_t)max(nnz64, 1LL));
-    sblas_mm_read(filename_A, 1, &m, &k, &nnz64, rp64.data(), col.data(), val.data());
+    sblas_mm_read(filename_A, 3, &m, &k, &nnz64, rp64.data(), col.data(), val.data());
     const int nnz = (int)nnz64;
     cout << "Matrix A -- #row: " << m << " #col: " << k << " nnz: " << nnz << endl;
     cout << "Loading input matrix A from " << filename_A << "\n";
-    // sortbyrow: order each row by column (rows are already bucketed)
+    // sortbyrow + COO -> CSR (dspmm_baseline_test.cu:41-55, 461-493)
+    for (int r = 0; r < m; ++r)
+        for (long long e = rp64[(size_t)r]; e < rp64[(size_t)r + 1]; ++e) row[(size_t)e] = r;
     vector<int> csrRowPtr((size_t)m + 1);
-    for (int i = 0; i <= m; ++i) csrRowPtr[(size_t)i] = (int)rp64[(size_t)i];
-    vector<int> perm;
-    for (int r = 0; r < m; ++r) {
-        const int a = csrRowPtr[(size_t)r], b = csrRowPtr[(size_t)r + 1];
-        perm.resize((size_t)(b - a));
-        iota(perm.begin(), perm.end(), a);
-        stable_sort(perm.begin(), perm.end(), [&](int u, int v) { return col[(size_t)u] < col[(size_t)v]; });
-        vector<int> c2(perm.size());
-        vector<double> v2(perm.size());
-        for (size_t t = 0; t < perm.size(); ++t) {
-            c2[t] = col[(size_t)perm[t]];
-            v2[t] = val[(size_t)perm[t]];
-        }
-        copy(c2.begin(), c2.end(), col.begin() + a);
-        copy(v2.begin(), v2.end(), val.begin() + a);
+    if (sblas_coo_sortbyrow(m, nnz64, row.data(), col.data(), val.data(), csrRowPtr.data()) != SBLAS_OK) {
+        cout << "sortbyrow failed: " << sblas_last_error() << "\n";
+        return -1;
     }
     cout << "Matrix B -- #row: " << k << " #col: " << n << " (dense)" << endl;
     cout << "Start generating data for Matrix B\n" << std::flush;

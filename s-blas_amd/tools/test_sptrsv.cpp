@@ -22,10 +22,11 @@ using namespace std;
 int main(int argc, char **argv)
 {
     if (argc < 8) {
-        printf("Usage: ./test_sptrsv -n [number of GPU(s)] -rhs 1 -forward -mtx [input sparse matrix A file]\n");
+        printf("Usage: ./test_sptrsv -n [number of GPU(s)] -rhs 1 -forward -mtx [input sparse matrix A file] "
+               "[-k tasks per GPU (sptrsv_v3)]\n");
         return -1;
     }
-    int ngpu = 1, rhs = 1, substitution = 0, opt = 3;
+    int ngpu = 1, rhs = 1, substitution = 0, opt = 3, task = 0;
     unsigned seed = 1;
     const char *filename = nullptr;
     for (int i = 1; i < argc; ++i) {
@@ -36,6 +37,7 @@ int main(int argc, char **argv)
         else if (!strcmp(argv[i], "-mtx") && i + 1 < argc) filename = argv[++i];
         else if (!strcmp(argv[i], "-seed") && i + 1 < argc) seed = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "-opt") && i + 1 < argc) opt = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-k") && i + 1 < argc) task = atoi(argv[++i]);  // v3: tasks per GPU
     }
     printf("---------------------------------------------------------------------------------------------\n");
     printf("PRECISION = 64-bit Double Precision\n");
@@ -128,8 +130,12 @@ int main(int argc, char **argv)
                 b[(size_t)ri[(size_t)j] * R + k] += cv[(size_t)j] * x_ref[(size_t)c * R + k];
     printf("----------------------------start-----------------------------------------------------\n");
     double gflops = 0;
-    const int rc = sptrsv_syncfree_cuda(cp.data(), ri.data(), cv.data(), m, n, nnzTR, substitution,
-                                        rhs, opt, x.data(), b.data(), x_ref.data(), &gflops, ngpu);
+    // -k <task>: sptrsv_v3's overload (ngpu*task round-robin tasks)
+    const int rc = task > 0
+        ? sptrsv_syncfree_cuda(cp.data(), ri.data(), cv.data(), m, n, nnzTR, substitution, rhs, opt,
+                               x.data(), b.data(), x_ref.data(), &gflops, ngpu, task)
+        : sptrsv_syncfree_cuda(cp.data(), ri.data(), cv.data(), m, n, nnzTR, substitution, rhs, opt,
+                               x.data(), b.data(), x_ref.data(), &gflops, ngpu);
     if (rc != 0) printf("sptrsv failed: %s\n", sblas_last_error());
     printf("----------------------------done------------------------------------------------------------\n");
     return rc == 0 ? 0 : 1;

@@ -53,6 +53,8 @@ _sig(lib, "orc_sptrsv_serial", _i, _p, _p, _p, _i, _i, _i, _p, _p)
 _sig(lib, "orc_levels_lower", _i, _i, _p, _p, _p)
 _sig(lib, "orc_spmm", None, _i, _i, _i, _d, _p, _p, _p, _p, _i, _d, _p, _i)
 _sig(lib, "orc_coo_sort_to_csr", None, _i, _i, _p, _p, _p, _p)
+_sig(lib, "orc_spmv_bound", None, _i, _p, _p, _p, _p, _d, _d, _p, _p)
+_sig(lib, "orc_spmm_omp", None, _i, _i, _d, _p, _p, _p, _p, _i, _i, _d, _p, _i, _p, _i)
 if ref is not None:
     _sig(ref, "ref_mm_header", _i, C.c_char_p, _p, _p, _p, _p)
     _sig(ref, "ref_mmio_info", _i, C.c_char_p, _p, _p, _p, _p)
@@ -110,16 +112,16 @@ def csr_spmv_omp(rowptr, col, val, x, alpha, beta, y, nthreads=0):
 
 
 def spmv_bound(rowptr, col, val, x, alpha, beta, y0):
-    """Per-row fp64 bound of DESIGN.md: 4*gamma_k*sum|alpha*a*x| + 4u|beta*y0|."""
-    u = 2.0 ** -53
-    rp = np.asarray(rowptr, np.int64)
-    k = np.diff(rp).astype(np.float64)
-    gam = k * u / (1.0 - k * u)
-    absprod = np.abs(alpha * val * x[col])
-    rows = np.repeat(np.arange(len(rp) - 1), np.diff(rp))
-    s = np.zeros(len(rp) - 1)
-    np.add.at(s, rows, absprod)
-    return 4.0 * gam * s + 4.0 * u * np.abs(beta * y0) + 1e-300
+    """Per-row fp64 bound of DESIGN.md: 4*gamma_k*sum|alpha*a*x| + 4u|beta*y0|
+    (orc_spmv_bound, OpenMP over rows)."""
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    m = len(rp) - 1
+    out = np.zeros(m)
+    lib.orc_spmv_bound(m, P(rp), P(np.ascontiguousarray(col, np.int32)),
+                       P(np.ascontiguousarray(val, np.float64)),
+                       P(np.ascontiguousarray(x, np.float64)), alpha, beta,
+                       P(np.ascontiguousarray(y0, np.float64)), P(out))
+    return out
 
 
 def partition_nnz(rowptr, g):
@@ -205,3 +207,21 @@ def spmm(m, n, k, alpha, rowptr, col, val, B, beta, C):
     lib.orc_spmm(m, n, k, alpha, P(rp), P(np.ascontiguousarray(col, np.int32)),
                  P(np.ascontiguousarray(val, np.float64)), P(Bf), k, beta, P(out), m)
     return out
+
+
+def spmm_checked(m, n, alpha, rowptr, col, val, B, beta, C, b_rowmajor=True, nthreads=0):
+    """orc_spmm's arithmetic in OpenMP (orc_spmm_omp) plus the per-entry bound.
+    B: (k, n) array; C: (m, n) array.  Returns (C_out, bound) as (m, n)."""
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    if b_rowmajor:
+        Bc = np.ascontiguousarray(B, np.float64)
+        ldb = n
+    else:
+        Bc = np.asfortranarray(B, np.float64)
+        ldb = B.shape[0]
+    out = np.array(C, np.float64, copy=True, order="F")
+    bound = np.zeros((m, n), np.float64, order="F")
+    lib.orc_spmm_omp(m, n, alpha, P(rp), P(np.ascontiguousarray(col, np.int32)),
+                     P(np.ascontiguousarray(val, np.float64)), P(Bc), ldb, int(b_rowmajor), beta,
+                     P(out), m, P(bound), nthreads)
+    return out, bound

@@ -197,3 +197,48 @@ def test_mm_read_truncated(sb, tmp_path):
     p.write_text("%%MatrixMarket matrix coordinate real general\n3 3 4\n1 1 1.0\n2 2 2.0\n")
     with pytest.raises(sb.SblasError, match="entries"):
         sb.mm_read(str(p))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_coo_sortbyrow_matches_oracle(sb, orc, seed):
+    """sortbyrow + COO -> CSR (dspmm_baseline_test.cu:41-55,
+    461-493): distinct (row, col) entries in random order sort bit-exactly
+    as the reference's qsort by (row, col); empty rows get empty ranges."""
+    rng = np.random.default_rng(seed)
+    m, k, nnz = 500, 300, 6000
+    flat = rng.choice(m * k, nnz, replace=False)
+    row = (flat // k).astype(np.int32)
+    col = (flat % k).astype(np.int32)
+    row[row == 7] = 8  # one empty row
+    flat = np.unique(row.astype(np.int64) * k + col)
+    rng.shuffle(flat)
+    row, col = (flat // k).astype(np.int32), (flat % k).astype(np.int32)
+    val = rng.standard_normal(len(row))
+    r1, c1, v1, rp1 = sb.coo_sortbyrow(m, row, col, val)
+    r2, c2, v2 = row.copy(), col.copy(), val.copy()
+    rp2 = np.zeros(m + 1, np.int32)
+    orc.lib.orc_coo_sort_to_csr(m, len(r2), orc.P(r2), orc.P(c2), orc.P(v2), orc.P(rp2))
+    assert np.array_equal(r1, r2) and np.array_equal(c1, c2) and np.array_equal(v1, v2)
+    assert np.array_equal(rp1, rp2) and rp1[8] == rp1[7 + 1]
+
+
+def test_coo_sortbyrow_test_spmm_loader(sb, orc):
+    """test_spmm's loader (mode 3) + sortbyrow on qh768 gives the CSR that the
+    mmio_data loader gives for a general (non-symmetric) file, once each row
+    is ordered by column; duplicates keep file order; bad rows rejected."""
+    path = os.path.join(GOLDEN, "qh768.mtx")
+    m, n, rp, col, val = sb.mm_read(path, 3)
+    row = np.repeat(np.arange(m, dtype=np.int32), np.diff(rp))
+    r, c, v, rp32 = sb.coo_sortbyrow(m, row, col, val)
+    assert np.array_equal(rp32, rp)
+    key = r.astype(np.int64) * n + c
+    assert np.all(np.diff(key) >= 0)
+    # same multiset of entries as the file
+    _, _, rp0, col0, val0 = sb.mm_read(path, 1)
+    assert sorted(zip(col0.tolist(), val0.tolist())) == sorted(zip(c.tolist(), v.tolist()))
+    # duplicates: stable
+    rr, cc, vv, _ = sb.coo_sortbyrow(2, np.array([1, 0, 1, 1], np.int32), np.array([5, 1, 5, 2], np.int32),
+                                     np.array([1.0, 2.0, 3.0, 4.0]))
+    assert rr.tolist() == [0, 1, 1, 1] and cc.tolist() == [1, 2, 5, 5] and vv.tolist() == [2.0, 4.0, 1.0, 3.0]
+    with pytest.raises(sb.SblasError):
+        sb.coo_sortbyrow(2, np.array([2], np.int32), np.array([0], np.int32), np.array([1.0]))

@@ -264,6 +264,86 @@ def test_sptrsv_mgpu_banded_matches_single(torch_cuda, sb, ngpu):
     assert np.abs(x - xref).sum() / np.abs(xref).sum() < 1e-10
 
 
+def _banded_system(sb, n, seed=11):
+    cp, ri, v = sb.gen_lower_banded(n, 4, 5000, seed)
+    xref = np.floor(sb.gen_vector(n, seed + 1) * 10.0) + 1.0
+    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
+    b = np.bincount(ri, weights=v * xref[cols], minlength=n)
+    return cp, ri, v, b, xref
+
+
+def _block_spans(out):
+    spans = {}
+    for line in out.splitlines():
+        w = line.split()
+        if w and w[0] == "trsv_block":
+            spans[int(w[1])] = (int(w[3]), float(w[7]), float(w[9]))
+    return [spans[d] for d in sorted(spans)]
+
+
+@pytest.mark.parametrize("blocks", [2, 4])
+def test_sptrsv_blocks_run_concurrently(torch_cuda, sb, monkeypatch, capfd, blocks):
+    """Blocks of the multi-device executor that wrap onto ONE GPU run at the
+    same time (own streams, co-resident grids): every block starts before its
+    predecessor -- the block it waits on -- has finished, so producer and
+    consumer are live together and the spin-on-peer-store protocol runs as it
+    does across GPUs.  SBLAS_TRSV_MGPU_SERIAL=1 (in order on one stream) is
+    the control: there no block starts before its predecessor ends.  Both
+    solves are bit-identical to the single-block solve."""
+    n = 300_000
+    cp, ri, v, b, xref = _banded_system(sb, n)
+    want, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, 1, 0)
+    monkeypatch.setenv("SBLAS_TRSV_TRACE", "1")
+    capfd.readouterr()
+    x, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, blocks, 0)
+    spans = _block_spans(capfd.readouterr().out)
+    assert np.array_equal(x, want)
+    assert len(spans) == blocks and len({s[0] for s in spans}) == 1
+    for d in range(1, blocks):
+        assert spans[d][1] < spans[d - 1][2], f"block {d} did not overlap block {d - 1}: {spans}"
+    monkeypatch.setenv("SBLAS_TRSV_MGPU_SERIAL", "1")
+    x, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, blocks, 0)
+    spans = _block_spans(capfd.readouterr().out)
+    assert np.array_equal(x, want)
+    for d in range(1, blocks):
+        assert spans[d][1] >= spans[d - 1][2], f"serial control overlapped: {spans}"
+
+
+@pytest.mark.parametrize("ngpu,tasks", [(1, 4), (2, 3), (3, 2), (4, 2)])
+@pytest.mark.parametrize("balance", [0, 1])
+def test_sptrsv_tasks_kat(torch_cuda, sb, ngpu, tasks, balance):
+    """sptrsv_v3's task decomposition: ngpu*tasks blocks, block d on device
+    d % ngpu, all running concurrently; exact on the KATs, and equal to the
+    single-block solve on the banded system."""
+    for name, sub in (("qh768", "fwd"), ("ash85", "bwd")):
+        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
+        n = len(g["colptr"]) - 1
+        x, _ = sb.trsv_mgpu_solve_tasks(g["colptr"], g["rowidx"], g["val"], n, g["b"], ngpu, tasks,
+                                        0 if sub == "fwd" else 1, balance=balance)
+        assert np.array_equal(x, g["x_ref"])
+    n = 300_000
+    cp, ri, v, b, _ = _banded_system(sb, n)
+    want, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, 1, 0)
+    x, _ = sb.trsv_mgpu_solve_tasks(cp, ri, v, n, b, ngpu, tasks, balance=balance)
+    assert np.array_equal(x, want)
+
+
+def test_sptrsv_v3_reference_api(torch_cuda, sb, capfd):
+    """sptrsv_syncfree_cuda(..., ngpu, task) (sptrsv_v3): prints v3's lines."""
+    g = np.load(os.path.join(GOLDEN, "trsv_qh768_fwd.npz"))
+    cp, ri, cv, b, xref = g["colptr"], g["rowidx"], g["val"], g["b"], g["x_ref"]
+    n = len(cp) - 1
+    x = np.zeros(n)
+    gf = np.zeros(1)
+    rc = sb.lib.sblas_sptrsv_syncfree_v3(sb.ptr(cp), sb.ptr(ri), sb.ptr(cv), n, n, len(ri), 0, 1, 3,
+                                         sb.ptr(x), sb.ptr(b), sb.ptr(xref), sb.ptr(gf), 2, 3)
+    assert rc == 0 and np.array_equal(x, xref) and gf[0] > 0
+    out = capfd.readouterr().out
+    assert out.count("nnz for device") == 6
+    assert "cuda syncfree SpTRSV solve used" in out
+    assert "device:0 cuda syncfree SpTRSV executor passed!" in out
+
+
 def test_sptrsv_reference_api_mgpu(torch_cuda, sb, capfd):
     g = np.load(os.path.join(GOLDEN, "trsv_ash85_bwd.npz"))
     cp, ri, cv, b, xref = g["colptr"], g["rowidx"], g["val"], g["b"], g["x_ref"]

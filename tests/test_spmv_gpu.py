@@ -21,14 +21,19 @@ pytestmark = pytest.mark.gpu
 # matrices; a tiny work target forces many ranges, most of them wide (one
 # sub-item per XCD + the partial reduce) and paired with narrow ones, ALLWIDE
 # forces every range with entries through the wide path (wide sub-items paired
-# with each other), and PAIR=0 runs one sub-item per workgroup.
+# with each other), and PAIR=0 runs one sub-item per workgroup.  Q = 2 / 3
+# column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
+# cover the wide sub-items' group ranges and the narrow wrap at q > 1.
 ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"})]
+         (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_Q": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_Q": "3"}),
+         (5, {"SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"})]
 ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50"]
+            "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
+            "xsort_q2_w50", "xsort_q3", "xsort_q3_w50"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
