@@ -221,6 +221,46 @@ int sblas_assemble_cyclic(const double *d_gathered, int g, long long stride,
                           long long chunk_rows, long long m, double *d_y, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* 3. Multi-GPU context (single process, RCCL over xGMI).  Replaces the
+ *    reference's host-driven multi-GPU SpMV (spmv/src/dspmv_mgpu_v1.cu:16-280)
+ *    for callers that keep the matrix: the slices stay resident per device,
+ *    x is replicated with ncclBroadcast, the y slices are exchanged with ONE
+ *    ncclAllGather and placed on the device, so every device holds the full
+ *    y.  Devices must be distinct (no wrapping: one RCCL rank per GPU). */
+typedef struct sblas_ctx_s *sblas_ctx;
+/* ncclCommInitAll over devlist[0..ngpu) (NULL: 0..ngpu-1). */
+int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist);
+int sblas_ctx_destroy(sblas_ctx ctx);
+int sblas_ctx_ngpu(sblas_ctx ctx, int *ngpu);
+/* HOST CSR (int64 rowptr) distributed over the devices and analysed for
+ * `algo` (sblas_spmv_algo).  partition 0 = cyclic row chunks (chunk j of
+ * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
+ * nnz-balanced split with split rows merged on the device. */
+int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr,
+                            const int *col, const double *val, int algo, int partition);
+int sblas_ctx_set_x(sblas_ctx ctx, const double *x); /* host x -> every device */
+int sblas_ctx_set_y(sblas_ctx ctx, const double *y); /* host y (beta input) */
+/* y = alpha*A*x + beta*y on every device; afterwards each device holds the
+ * full y, which is also the next call's y input.  stats (optional, 3
+ * doubles, ms, max over devices): kernel, exchange (all-gather + placement),
+ * whole step. */
+int sblas_ctx_spmv(sblas_ctx ctx, double alpha, double beta, double *stats);
+int sblas_ctx_get_y(sblas_ctx ctx, int device_index, double *y); /* -> host */
+/* Bind (or unbind with NULL) a context for the reference API: while bound,
+ * sblas_spMV_mgpu_v1 / spMV_mgpu_v1 with ngpu == the context's size run on
+ * it (RCCL exchange) instead of the host merge. */
+int sblas_ctx_bind(sblas_ctx ctx);
+/* The cyclic distribution's plan: chunk_rows = ceil(m/(g*chunks_per_rank)),
+ * stride = rows of one device's padded slice.  No GPU needed. */
+int sblas_cyclic_plan(long long m, int g, int chunks_per_rank, long long *chunk_rows,
+                      long long *stride);
+/* Local CSR of partition d under it: chunks d, d+g, ... concatenated (host
+ * arrays; call with lrowptr/lcol/lval NULL to size).  No GPU needed. */
+int sblas_cyclic_local_csr(int m, const long long *rowptr, const int *col, const double *val,
+                           int g, long long chunk_rows, int d, long long *local_m,
+                           long long *local_nnz, long long *lrowptr, int *lcol, double *lval);
+
+/* ------------------------------------------------------------------------ */
 /* Host utilities (no GPU needed). */
 /* Matrix-Market: mode 0 = full mmio_data semantics (symmetric expansion,
  * pattern -> 1.0); mode 1 = test_spmv 'f' loader (file order, Q1/Q2);

@@ -1,0 +1,400 @@
+// ctx.hip -- single-process multi-GPU SpMV context over RCCL (include/sblas.h
+// "3. Multi-GPU context").
+//
+// Replaces the reference's host-driven multi-GPU SpMV (spmv/src/
+// dspmv_mgpu_v1.cu:16-280: per-call H2D of every slice, csrmv per GPU, D2H
+// and a host merge of the split rows, :224-248) for C/C++ callers that keep
+// the matrix: ONE process drives g GPUs, each GPU keeps its slice resident,
+// x is replicated with ncclBroadcast, and after the per-device kernels the y
+// slices are exchanged with ONE ncclAllGather over xGMI and placed by a
+// device kernel, so every GPU ends with the full, bit-identical y (SURVEY §5
+// "Distributed communication backend", §8 G1).  The communicator comes from
+// ncclCommInitAll over the context's devices.
+//
+// Partitions: 0 = cyclic row chunks (chunk j of ceil(m / (g*8)) rows on
+// device j % g, whole rows, equal padded slices: no split rows, no carries;
+// sblas_dist.CyclicPlan is the same distribution for one-process-per-GPU
+// runs); 1 = spMV_mgpu_v1's nnz-balanced split (dspmv_mgpu_v1.cu:60-94, Q5
+// fixed) with the split rows added in partition order on the device
+// (k_assemble_carry).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "sblas_internal.hpp"
+
+struct sblas_ctx_s {
+    int g = 0;
+    std::vector<int> dev;
+    std::vector<ncclComm_t> comm;
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;  // [g][3]: start, after kernel, after exchange + placement
+    // the matrix (absent until sblas_ctx_matrix_upload)
+    bool loaded = false;
+    int m = 0, n = 0, algo = 0, partition = 0;
+    long long nnz = 0, stride = 0, chunk_rows = 0;
+    std::vector<sblas_csr> A;
+    std::vector<double *> x, ylocal, gathered, yfull;
+    std::vector<int *> meta;           // nnz partition: {row0, nrows, cont} per partition
+    std::vector<int> h_meta;
+    std::vector<long long> lrows;      // rows per device
+};
+
+// Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
+// context's size runs on it (device-resident slices for the call, x
+// broadcast, kernels, ncclAllGather, device merge) instead of the per-device
+// host merge.  Process-global, as the reference's device state is.
+namespace sblas {
+static sblas_ctx g_bound = nullptr;
+sblas_ctx bound_ctx() { return g_bound; }
+}  // namespace sblas
+
+namespace {
+
+using namespace sblas;
+
+#define SBLAS_NCCL(expr)                                                        \
+    do {                                                                        \
+        ncclResult_t r_ = (expr);                                               \
+        if (r_ != ncclSuccess) {                                                \
+            ::sblas::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,     \
+                               ncclGetErrorString(r_));                         \
+            return SBLAS_ERR_RCCL;                                              \
+        }                                                                       \
+    } while (0)
+
+void free_matrix(sblas_ctx_s &C)
+{
+    for (int d = 0; d < (int)C.A.size(); ++d) {
+        DeviceGuard g(C.dev[d]);
+        sblas_csr_destroy(C.A[d]);
+        (void)hipFree(C.x[d]);
+        (void)hipFree(C.ylocal[d]);
+        (void)hipFree(C.gathered[d]);
+        (void)hipFree(C.yfull[d]);
+        (void)hipFree(C.meta[d]);
+    }
+    C.A.clear();
+    C.x.clear();
+    C.ylocal.clear();
+    C.gathered.clear();
+    C.yfull.clear();
+    C.meta.clear();
+    C.h_meta.clear();
+    C.lrows.clear();
+    C.loaded = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sblas_cyclic_plan(long long m, int g, int chunks_per_rank, long long *chunk_rows,
+                      long long *stride)
+{
+    if (m < 0 || g <= 0 || chunks_per_rank <= 0 || !chunk_rows || !stride) return SBLAS_ERR_INVALID;
+    const long long R = std::max(1LL, (m + (long long)g * chunks_per_rank - 1) / ((long long)g * chunks_per_rank));
+    const long long nchunks = m ? (m + R - 1) / R : 0;
+    *chunk_rows = R;
+    *stride = std::max(1LL, ((nchunks + g - 1) / g) * R);
+    return SBLAS_OK;
+}
+
+int sblas_cyclic_local_csr(int m, const long long *rowptr, const int *col, const double *val, int g,
+                           long long chunk_rows, int d, long long *local_m, long long *local_nnz,
+                           long long *lrowptr, int *lcol, double *lval)
+{
+    if (m < 0 || !rowptr || g <= 0 || chunk_rows <= 0 || d < 0 || d >= g || !local_m || !local_nnz)
+        return SBLAS_ERR_INVALID;
+    const long long nchunks = m ? (m + chunk_rows - 1) / chunk_rows : 0;
+    long long lm = 0, lz = 0;
+    for (long long j = d; j < nchunks; j += g) {
+        const long long a = j * chunk_rows, b = std::min<long long>(m, a + chunk_rows);
+        if (lrowptr) {
+            for (long long r = a; r < b; ++r) lrowptr[lm + (r - a) + 1] = lz + (rowptr[r + 1] - rowptr[a]);
+            if (lm == 0) lrowptr[0] = 0;
+        }
+        const long long cnt = rowptr[b] - rowptr[a];
+        if (lcol && cnt) std::memcpy(lcol + lz, col + rowptr[a], sizeof(int) * (size_t)cnt);
+        if (lval && cnt) std::memcpy(lval + lz, val + rowptr[a], sizeof(double) * (size_t)cnt);
+        lm += b - a;
+        lz += cnt;
+    }
+    if (lrowptr && lm == 0) lrowptr[0] = 0;
+    *local_m = lm;
+    *local_nnz = lz;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist)
+{
+    if (!out || ngpu <= 0) return SBLAS_ERR_INVALID;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
+    std::vector<int> dev(ngpu);
+    for (int d = 0; d < ngpu; ++d) {
+        dev[d] = devlist ? devlist[d] : d;
+        if (dev[d] < 0 || dev[d] >= count) {
+            set_error("sblas_ctx_create: device %d of %d visible (one rank per GPU: no wrapping)",
+                      dev[d], count);
+            return SBLAS_ERR_INVALID;
+        }
+        for (int e = 0; e < d; ++e)
+            if (dev[e] == dev[d]) {
+                set_error("sblas_ctx_create: device %d listed twice", dev[d]);
+                return SBLAS_ERR_INVALID;
+            }
+    }
+    auto *C = new sblas_ctx_s();
+    C->g = ngpu;
+    C->dev = dev;
+    C->comm.assign(ngpu, nullptr);
+    ncclResult_t r = ncclCommInitAll(C->comm.data(), ngpu, dev.data());
+    if (r != ncclSuccess) {
+        set_error("ncclCommInitAll(%d): %s", ngpu, ncclGetErrorString(r));
+        C->comm.clear();
+        sblas_ctx_destroy(C);
+        return SBLAS_ERR_RCCL;
+    }
+    C->st.assign(ngpu, nullptr);
+    C->ev.assign((size_t)3 * ngpu, nullptr);
+    for (int d = 0; d < ngpu; ++d) {
+        DeviceGuard g(dev[d]);
+        hipError_t e = hipStreamCreateWithFlags(&C->st[d], hipStreamNonBlocking);
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreate(&C->ev[(size_t)3 * d + k]);
+        if (e != hipSuccess) {
+            set_error("sblas_ctx_create: %s", hipGetErrorString(e));
+            sblas_ctx_destroy(C);
+            return SBLAS_ERR_HIP;
+        }
+    }
+    *out = C;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_destroy(sblas_ctx C)
+{
+    if (!C) return SBLAS_OK;
+    if (g_bound == C) g_bound = nullptr;
+    free_matrix(*C);
+    for (int d = 0; d < C->g; ++d) {
+        DeviceGuard g(C->dev[d]);
+        if (d < (int)C->comm.size() && C->comm[d]) (void)ncclCommDestroy(C->comm[d]);
+        if (d < (int)C->st.size() && C->st[d]) (void)hipStreamDestroy(C->st[d]);
+        for (int k = 0; k < 3; ++k)
+            if ((size_t)3 * d + k < C->ev.size() && C->ev[(size_t)3 * d + k])
+                (void)hipEventDestroy(C->ev[(size_t)3 * d + k]);
+    }
+    delete C;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_ngpu(sblas_ctx C, int *ngpu)
+{
+    if (!C || !ngpu) return SBLAS_ERR_INVALID;
+    *ngpu = C->g;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
+                            const double *val, int algo, int partition)
+{
+    if (!C || m < 0 || n < 0 || !rowptr || (partition != 0 && partition != 1)) return SBLAS_ERR_INVALID;
+    if (algo < SBLAS_SPMV_ROWSPLIT || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
+    free_matrix(*C);
+    const int g = C->g;
+    C->m = m;
+    C->n = n;
+    C->nnz = rowptr[m];
+    C->algo = algo;
+    C->partition = partition;
+    C->A.assign(g, nullptr);
+    C->x.assign(g, nullptr);
+    C->ylocal.assign(g, nullptr);
+    C->gathered.assign(g, nullptr);
+    C->yfull.assign(g, nullptr);
+    C->meta.assign(g, nullptr);
+    C->lrows.assign(g, 0);
+    std::vector<long long> si(g), ei(g);
+    std::vector<int> sr(g), er(g), sf(g);
+    if (partition == 0) {
+        SBLAS_TRY(sblas_cyclic_plan(m, g, 8, &C->chunk_rows, &C->stride));
+    } else {
+        SBLAS_TRY(sblas_partition_nnz(m, C->nnz, rowptr, g, si.data(), ei.data(), sr.data(), er.data(),
+                                      sf.data()));
+        C->h_meta.assign((size_t)3 * g, 0);
+        long long mx = 1;
+        for (int d = 0; d < g; ++d) {
+            const long long nr = std::max(0, er[d] - sr[d] + 1);
+            C->h_meta[(size_t)3 * d] = sr[d];
+            C->h_meta[(size_t)3 * d + 1] = (int)nr;
+            C->h_meta[(size_t)3 * d + 2] = sf[d];
+            mx = std::max(mx, nr);
+        }
+        C->stride = mx;
+    }
+    int st = SBLAS_OK;
+    for (int d = 0; d < g && st == SBLAS_OK; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        if (partition == 0) {
+            long long lm = 0, lz = 0;
+            SBLAS_TRY(sblas_cyclic_local_csr(m, rowptr, col, val, g, C->chunk_rows, d, &lm, &lz,
+                                             nullptr, nullptr, nullptr));
+            std::vector<long long> lrp((size_t)lm + 1);
+            std::vector<int> lcol((size_t)std::max(lz, 1LL));
+            std::vector<double> lval((size_t)std::max(lz, 1LL));
+            SBLAS_TRY(sblas_cyclic_local_csr(m, rowptr, col, val, g, C->chunk_rows, d, &lm, &lz,
+                                             lrp.data(), lcol.data(), lval.data()));
+            C->lrows[d] = lm;
+            st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, lrp.data(), lcol.data(), lval.data(), 0,
+                                        (int)lm, 0, lz, C->st[d]);
+        } else {
+            C->lrows[d] = std::max(0, er[d] - sr[d] + 1);
+            st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, rowptr, col, val, sr[d], er[d] + 1,
+                                        si[d], ei[d] + 1, C->st[d]);
+        }
+        if (st != SBLAS_OK) break;
+        st = sblas_csr_analyse(C->A[d], algo, C->st[d]);
+        if (st != SBLAS_OK) break;
+        hipError_t e = hipMalloc(&C->x[d], sizeof(double) * std::max(n, 1));
+        if (e == hipSuccess) e = hipMalloc(&C->ylocal[d], sizeof(double) * C->stride);
+        if (e == hipSuccess) e = hipMalloc(&C->gathered[d], sizeof(double) * C->stride * g);
+        if (e == hipSuccess) e = hipMalloc(&C->yfull[d], sizeof(double) * std::max(m, 1));
+        if (e == hipSuccess) e = hipMemsetAsync(C->ylocal[d], 0, sizeof(double) * C->stride, C->st[d]);
+        if (e == hipSuccess && partition == 1) {
+            e = hipMalloc(&C->meta[d], sizeof(int) * 3 * g);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(C->meta[d], C->h_meta.data(), sizeof(int) * 3 * g, hipMemcpyHostToDevice,
+                                   C->st[d]);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(C->st[d]);
+        if (e != hipSuccess) {
+            set_error("sblas_ctx_matrix_upload: %s", hipGetErrorString(e));
+            st = SBLAS_ERR_HIP;
+        }
+    }
+    if (st != SBLAS_OK) {
+        free_matrix(*C);
+        return st;
+    }
+    C->loaded = true;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_set_x(sblas_ctx C, const double *x)
+{
+    if (!C || !C->loaded || !x) return SBLAS_ERR_INVALID;
+    if (C->n == 0) return SBLAS_OK;
+    {
+        DeviceGuard g(C->dev[0]);
+        SBLAS_HIP(hipMemcpyAsync(C->x[0], x, sizeof(double) * C->n, hipMemcpyHostToDevice, C->st[0]));
+    }
+    // replicate x from device 0 over xGMI
+    SBLAS_NCCL(ncclGroupStart());
+    for (int d = 0; d < C->g; ++d) {
+        DeviceGuard g(C->dev[d]);
+        SBLAS_NCCL(ncclBroadcast(C->x[d], C->x[d], (size_t)C->n, ncclDouble, 0, C->comm[d], C->st[d]));
+    }
+    SBLAS_NCCL(ncclGroupEnd());
+    for (int d = 0; d < C->g; ++d) {
+        DeviceGuard g(C->dev[d]);
+        SBLAS_HIP(hipStreamSynchronize(C->st[d]));
+    }
+    return SBLAS_OK;
+}
+
+int sblas_ctx_set_y(sblas_ctx C, const double *y)
+{
+    if (!C || !C->loaded || !y) return SBLAS_ERR_INVALID;
+    std::vector<double> h((size_t)C->stride);
+    for (int d = 0; d < C->g; ++d) {
+        std::fill(h.begin(), h.end(), 0.0);
+        long long o = 0;
+        if (C->partition == 0) {
+            const long long nch = C->m ? (C->m + C->chunk_rows - 1) / C->chunk_rows : 0;
+            for (long long j = d; j < nch; j += C->g) {
+                const long long a = j * C->chunk_rows, b = std::min<long long>(C->m, a + C->chunk_rows);
+                std::memcpy(h.data() + o, y + a, sizeof(double) * (size_t)(b - a));
+                o += b - a;
+            }
+        } else {
+            const int r0 = C->h_meta[(size_t)3 * d], nr = C->h_meta[(size_t)3 * d + 1];
+            if (nr > 0) std::memcpy(h.data(), y + r0, sizeof(double) * nr);
+            if (nr > 0 && C->h_meta[(size_t)3 * d + 2]) h[0] = 0.0;  // continuation: partial only
+        }
+        DeviceGuard g(C->dev[d]);
+        SBLAS_HIP(hipMemcpyAsync(C->ylocal[d], h.data(), sizeof(double) * C->stride, hipMemcpyHostToDevice,
+                                 C->st[d]));
+        SBLAS_HIP(hipStreamSynchronize(C->st[d]));
+    }
+    return SBLAS_OK;
+}
+
+int sblas_ctx_spmv(sblas_ctx C, double alpha, double beta, double *stats)
+{
+    if (!C || !C->loaded) return SBLAS_ERR_INVALID;
+    const int g = C->g;
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d], C->st[d]));
+        if (C->lrows[d] > 0)
+            SBLAS_TRY(sblas_spmv(C->A[d], C->algo, alpha, C->x[d], beta, C->ylocal[d], C->st[d]));
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 1], C->st[d]));
+    }
+    // the exchange: one all-gather of equal padded slices over xGMI
+    SBLAS_NCCL(ncclGroupStart());
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        SBLAS_NCCL(ncclAllGather(C->ylocal[d], C->gathered[d], (size_t)C->stride, ncclDouble, C->comm[d],
+                                 C->st[d]));
+    }
+    SBLAS_NCCL(ncclGroupEnd());
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        if (C->partition == 0)
+            SBLAS_TRY(sblas_assemble_cyclic(C->gathered[d], g, C->stride, C->chunk_rows, C->m, C->yfull[d],
+                                            C->st[d]));
+        else  // also re-primes this device's slice as the next call's y input
+            SBLAS_TRY(sblas_assemble_slices(C->gathered[d], g, C->stride, C->meta[d], C->yfull[d], d,
+                                            C->ylocal[d], C->st[d]));
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 2], C->st[d]));
+    }
+    double kmax = 0.0, xmax = 0.0, tmax = 0.0;
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        SBLAS_HIP(hipEventSynchronize(C->ev[(size_t)3 * d + 2]));
+        float k = 0.f, t = 0.f;
+        SBLAS_HIP(hipEventElapsedTime(&k, C->ev[(size_t)3 * d], C->ev[(size_t)3 * d + 1]));
+        SBLAS_HIP(hipEventElapsedTime(&t, C->ev[(size_t)3 * d], C->ev[(size_t)3 * d + 2]));
+        kmax = std::max(kmax, (double)k);
+        xmax = std::max(xmax, (double)(t - k));
+        tmax = std::max(tmax, (double)t);
+    }
+    if (stats) {
+        stats[0] = kmax;  // kernel, max over devices (ms)
+        stats[1] = xmax;  // all-gather + placement, max over devices
+        stats[2] = tmax;  // whole step, max over devices
+    }
+    return SBLAS_OK;
+}
+
+int sblas_ctx_get_y(sblas_ctx C, int device_index, double *y)
+{
+    if (!C || !C->loaded || !y || device_index < 0 || device_index >= C->g) return SBLAS_ERR_INVALID;
+    if (C->m == 0) return SBLAS_OK;
+    DeviceGuard g(C->dev[device_index]);
+    SBLAS_HIP(hipMemcpyAsync(y, C->yfull[device_index], sizeof(double) * C->m, hipMemcpyDeviceToHost,
+                             C->st[device_index]));
+    SBLAS_HIP(hipStreamSynchronize(C->st[device_index]));
+    return SBLAS_OK;
+}
+
+}  // extern "C"
+
+extern "C" int sblas_ctx_bind(sblas_ctx C)
+{
+    sblas::g_bound = C;
+    return SBLAS_OK;
+}

@@ -153,7 +153,10 @@ int sblas_spMV_mgpu_baseline(int m, int n, long long nnz, double *alpha, double 
                      SBLAS_SPMV_ROWSPLIT);
 }
 
-// dspmv_mgpu_v1.cu:16-280
+// dspmv_mgpu_v1.cu:16-280.  With a bound context of ngpu devices
+// (sblas_ctx_bind) the exchange runs over RCCL on the devices; otherwise
+// partitions wrap onto the visible GPUs and merge on the host, as the
+// reference does.
 int sblas_spMV_mgpu_v1(int m, int n, long long nnz, double *alpha, double *csrVal,
                        long long *csrRowPtr, int *csrColIndex, double *x, double *beta, double *y,
                        int ngpu, int kernel)
@@ -162,6 +165,20 @@ int sblas_spMV_mgpu_v1(int m, int n, long long nnz, double *alpha, double *csrVa
     if (kernel < 1 || kernel > 3) return SBLAS_ERR_INVALID;
     int count;
     if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
+    if (sblas_ctx C = bound_ctx()) {
+        int g = 0;
+        if (sblas_ctx_ngpu(C, &g) == SBLAS_OK && g == ngpu) {
+            // bound RCCL context (sblas_ctx_bind): the same nnz split, slices
+            // resident for the call, x broadcast, kernels, one ncclAllGather
+            // and the split-row merge on the device; y from device 0
+            SBLAS_TRY(sblas_ctx_matrix_upload(C, m, n, csrRowPtr, csrColIndex, csrVal,
+                                              algo_of_kernel(kernel), 1));
+            SBLAS_TRY(sblas_ctx_set_x(C, x));
+            SBLAS_TRY(sblas_ctx_set_y(C, y));
+            SBLAS_TRY(sblas_ctx_spmv(C, *alpha, *beta, nullptr));
+            return sblas_ctx_get_y(C, 0, y);
+        }
+    }
     std::vector<long long> si(ngpu), ei(ngpu);
     std::vector<int> sr(ngpu), er(ngpu), sf(ngpu);
     sblas_partition_nnz(m, nnz, csrRowPtr, ngpu, si.data(), ei.data(), sr.data(), er.data(), sf.data());

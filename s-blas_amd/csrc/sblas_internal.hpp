@@ -249,5 +249,6 @@ struct DeviceGuard {
 // Host helpers shared by capi / refapi (host_utils.cpp).
 int row_of_index(int m, const long long *rowptr, long long idx);
 int resolve_device(int ordinal, int *phys);  // wraps ordinals on few GPUs
+sblas_ctx bound_ctx();                       // ctx.hip: sblas_ctx_bind's context (or null)
 
 }  // namespace sblas

@@ -97,6 +97,17 @@ _sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)
 _sig("sblas_coo_sortbyrow", _i, _i, _ll, _p, _p, _p, _p)
+_sig("sblas_ctx_create", _i, _p, _i, _p)
+_sig("sblas_ctx_destroy", _i, _p)
+_sig("sblas_ctx_ngpu", _i, _p, _p)
+_sig("sblas_ctx_matrix_upload", _i, _p, _i, _i, _p, _p, _p, _i, _i)
+_sig("sblas_ctx_set_x", _i, _p, _p)
+_sig("sblas_ctx_set_y", _i, _p, _p)
+_sig("sblas_ctx_spmv", _i, _p, _d, _d, _p)
+_sig("sblas_ctx_get_y", _i, _p, _i, _p)
+_sig("sblas_ctx_bind", _i, _p)
+_sig("sblas_cyclic_plan", _i, _ll, _i, _i, _p, _p)
+_sig("sblas_cyclic_local_csr", _i, _i, _p, _p, _p, _i, _ll, _i, _p, _p, _p, _p, _p)
 _sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
 _sig("sblas_gen_synth_rows", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _i, _i, _p, _p)
 _sig("sblas_gen_vector", _i, _i, C.c_ulonglong, _p)
@@ -183,6 +194,30 @@ def coo_sortbyrow(m: int, row, col, val):
     rp = np.zeros(m + 1, np.int32)
     check(lib.sblas_coo_sortbyrow(m, len(r), ptr(r), ptr(c), ptr(v), ptr(rp)), "coo_sortbyrow")
     return r, c, v, rp
+
+
+def cyclic_plan(m: int, g: int, chunks_per_rank: int = 8):
+    """(chunk_rows, stride) of the cyclic row-chunk distribution."""
+    R, S = C.c_longlong(), C.c_longlong()
+    check(lib.sblas_cyclic_plan(m, g, chunks_per_rank, C.byref(R), C.byref(S)), "cyclic_plan")
+    return R.value, S.value
+
+
+def cyclic_local_csr(rowptr, col, val, g: int, chunk_rows: int, d: int):
+    """Partition d's local CSR (int64 rowptr, col, val) under the cyclic plan."""
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    ci = np.ascontiguousarray(col, np.int32)
+    v = np.ascontiguousarray(val, np.float64)
+    m = len(rp) - 1
+    lm, lz = C.c_longlong(), C.c_longlong()
+    check(lib.sblas_cyclic_local_csr(m, ptr(rp), ptr(ci), ptr(v), g, chunk_rows, d, C.byref(lm),
+                                     C.byref(lz), None, None, None), "cyclic_local_csr")
+    lrp = np.zeros(lm.value + 1, np.int64)
+    lc = np.zeros(max(lz.value, 1), np.int32)
+    lv = np.zeros(max(lz.value, 1), np.float64)
+    check(lib.sblas_cyclic_local_csr(m, ptr(rp), ptr(ci), ptr(v), g, chunk_rows, d, C.byref(lm),
+                                     C.byref(lz), ptr(lrp), ptr(lc), ptr(lv)), "cyclic_local_csr")
+    return lrp, lc[:lz.value], lv[:lz.value]
 
 
 def partition_rowblock(m: int, g: int) -> np.ndarray:
@@ -362,6 +397,61 @@ class DeviceCSR:
     def close(self) -> None:
         if self.h:
             lib.sblas_csr_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceCtx:
+    """Single-process multi-GPU SpMV context (sblas_ctx: RCCL communicator
+    over `ngpu` distinct devices, resident slices, ncclAllGather exchange)."""
+
+    def __init__(self, ngpu: int, devices=None):
+        self.h = C.c_void_p()
+        dl = None if devices is None else np.ascontiguousarray(devices, np.int32)
+        check(lib.sblas_ctx_create(C.byref(self.h), ngpu, ptr(dl)), "ctx_create")
+        self.ngpu = ngpu
+        self.m = 0
+
+    def upload(self, m: int, n: int, rowptr, col, val, algo: int, partition: int = 0) -> None:
+        self._keep = (np.ascontiguousarray(rowptr, np.int64), np.ascontiguousarray(col, np.int32),
+                      np.ascontiguousarray(val, np.float64))
+        rp, ci, v = self._keep
+        check(lib.sblas_ctx_matrix_upload(self.h, m, n, ptr(rp), ptr(ci), ptr(v), algo, partition),
+              "ctx_matrix_upload")
+        self.m = m
+
+    def set_x(self, x) -> None:
+        check(lib.sblas_ctx_set_x(self.h, ptr(np.ascontiguousarray(x, np.float64))), "ctx_set_x")
+
+    def set_y(self, y) -> None:
+        check(lib.sblas_ctx_set_y(self.h, ptr(np.ascontiguousarray(y, np.float64))), "ctx_set_y")
+
+    def spmv(self, alpha: float, beta: float):
+        """Returns (kernel ms, exchange ms, step ms), max over devices."""
+        st = np.zeros(3)
+        check(lib.sblas_ctx_spmv(self.h, alpha, beta, ptr(st)), "ctx_spmv")
+        return tuple(st)
+
+    def get_y(self, device_index: int = 0) -> np.ndarray:
+        y = np.zeros(max(self.m, 1))
+        check(lib.sblas_ctx_get_y(self.h, device_index, ptr(y)), "ctx_get_y")
+        return y[:self.m]
+
+    def bind(self) -> None:
+        check(lib.sblas_ctx_bind(self.h), "ctx_bind")
+
+    @staticmethod
+    def unbind() -> None:
+        lib.sblas_ctx_bind(None)
+
+    def close(self) -> None:
+        if self.h:
+            lib.sblas_ctx_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

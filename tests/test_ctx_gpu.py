@@ -1,0 +1,121 @@
+"""Single-process multi-GPU context over RCCL (sblas_ctx, include/sblas.h §3).
+
+The context is the C-ABI's multi-GPU SpMV: ncclCommInitAll over distinct
+devices, resident slices, ncclBroadcast of x, ONE ncclAllGather of the y
+slices and device placement.  On the one-GPU box it runs with a 1-rank
+communicator (the collectives execute; the partition/placement logic for
+g > 1 is covered on the CPU by tests/test_host.py and by the torch
+ranks of tests/test_cli_gpu.py, which use the same distribution).  Parity:
+the oracle's CSR SpMV with the per-row fp64 bound.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_csr(rng, m, n, maxlen, long_rows=()):
+    lens = rng.integers(0, maxlen, m)
+    lens[rng.random(m) < 0.1] = 0
+    for r, L in long_rows:
+        lens[r] = L
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+    return rp, col, rng.standard_normal(int(rp[-1]))
+
+
+@pytest.mark.parametrize("algo", [1, 2, 4, 5])
+@pytest.mark.parametrize("partition", [0, 1])
+def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition):
+    """Two chained steps (the second's beta input is the first's y, kept on
+    the devices by the context) against the oracle."""
+    rng = np.random.default_rng(algo + 10 * partition)
+    m, n = 5000, 7000
+    rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(3, 6000), (4000, 2500)])
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(1)
+    ctx.upload(m, n, rp, col, val, algo, partition)
+    ctx.set_x(x)
+    ctx.set_y(y0)
+    k, xch, tot = ctx.spmv(alpha, beta)
+    assert k >= 0 and xch >= 0 and tot >= k
+    y1 = ctx.get_y()
+    want1 = orc.csr_spmv(rp, col, val, x, alpha, beta, y0)
+    assert np.all(np.abs(y1 - want1) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+    ctx.spmv(alpha, beta)
+    y2 = ctx.get_y()
+    want2 = orc.csr_spmv(rp, col, val, x, alpha, beta, y1)
+    assert np.all(np.abs(y2 - want2) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y1))
+    ctx.close()
+
+
+@pytest.mark.parametrize("algo", [2, 5])
+def test_ctx_config2_full_size(torch_cuda, sb, orc, algo):
+    n = 2_000_000
+    rp = sb.gen_synth_rowptr(n)
+    col, val = sb.gen_synth_rows(n, rp, 0, n)
+    x = sb.gen_vector(n, 43)
+    y0 = sb.gen_vector(n, 44)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(1)
+    ctx.upload(n, n, rp, col, val, algo, 0)
+    ctx.set_x(x)
+    ctx.set_y(y0)
+    ctx.spmv(alpha, beta)
+    got = ctx.get_y()
+    want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
+    assert np.all(np.abs(got - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+    ctx.close()
+
+
+def test_ctx_bound_reference_api(torch_cuda, sb, orc):
+    """spMV_mgpu_v1 with a bound context of the same size runs the RCCL path;
+    other ngpu values keep the host-merge path; both match the oracle."""
+    rng = np.random.default_rng(4)
+    m, n = 2500, 3000
+    rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(10, 2500)])
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    want = orc.csr_spmv(rp, col, val, x, alpha, beta, y0)
+    bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y0)
+    ctx = sb.DeviceCtx(1)
+    ctx.bind()
+    try:
+        for ngpu, kernel in ((1, 1), (1, 2), (2, 1), (3, 3)):
+            y = y0.copy()
+            assert sb.spmv_mgpu("v1", m, n, rp, col, val, x, y, alpha, beta, ngpu=ngpu, kernel=kernel) == 0
+            assert np.all(np.abs(y - want) <= bound), (ngpu, kernel)
+    finally:
+        sb.DeviceCtx.unbind()
+        ctx.close()
+
+
+def test_ctx_rejects_shared_devices(torch_cuda, sb):
+    """One RCCL rank per GPU: no ordinal wrapping, no duplicates."""
+    count = sb.device_count()
+    with pytest.raises(sb.SblasError):
+        sb.DeviceCtx(count + 1)
+    with pytest.raises(sb.SblasError):
+        sb.DeviceCtx(2, devices=[0, 0])
+
+
+@pytest.mark.parametrize("algo,partition", [(5, 0), (2, 1), (1, 0)])
+def test_cli_spmv_ctx(algo, partition):
+    """The C++ driver (tools/spmv_ctx.cpp): a C caller reaching the RCCL path
+    with no Python; it checks device agreement, the host-merge reference API
+    and the bound reference API."""
+    exe = os.path.join(ROOT, "s-blas_amd", "bin", "spmv_ctx")
+    r = subprocess.run([exe, "1", "2000000", str(algo), str(partition), "5"], capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ctx devices agree: PASS" in r.stdout
+    assert "(RCCL): PASS" in r.stdout
+    assert "ctx spmv: kernel" in r.stdout

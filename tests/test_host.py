@@ -242,3 +242,29 @@ def test_coo_sortbyrow_test_spmm_loader(sb, orc):
     assert rr.tolist() == [0, 1, 1, 1] and cc.tolist() == [1, 2, 5, 5] and vv.tolist() == [2.0, 4.0, 1.0, 3.0]
     with pytest.raises(sb.SblasError):
         sb.coo_sortbyrow(2, np.array([2], np.int32), np.array([0], np.int32), np.array([1.0]))
+
+
+@pytest.mark.parametrize("m,g", [(0, 1), (1, 3), (1000, 1), (1003, 2), (2_000_00, 8), (77, 5)])
+def test_cyclic_partition_matches_dist_plan(sb, m, g):
+    """The C-ABI context's cyclic distribution (sblas_cyclic_plan /
+    sblas_cyclic_local_csr, used by sblas_ctx) is the one sblas_dist's
+    CyclicPlan deals to torch.distributed ranks: same chunk size, slice
+    stride and local CSR, bit for bit, and the slices tile the matrix."""
+    import sblas_dist
+    rng = np.random.default_rng(m + g)
+    lens = rng.integers(0, 7, m)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = rng.integers(0, max(m, 1), int(rp[-1])).astype(np.int32)
+    val = rng.standard_normal(int(rp[-1]))
+    plan = sblas_dist.make_cyclic_plan(rp, m, g)
+    R, S = sb.cyclic_plan(m, g)
+    assert (R, S) == (plan.chunk_rows, plan.stride)
+    total_rows = total_nnz = 0
+    for d in range(g):
+        lrp, lc, lv = sb.cyclic_local_csr(rp, col, val, g, R, d)
+        wrp, wc, wv = sblas_dist.cyclic_local_csr(rp, plan, d, lambda a, b: (col[rp[a]:rp[b]], val[rp[a]:rp[b]]))
+        assert np.array_equal(lrp, wrp) and np.array_equal(lc, wc) and np.array_equal(lv, wv)
+        assert len(lrp) - 1 == plan.local_rows(d) <= S
+        total_rows += len(lrp) - 1
+        total_nnz += int(lrp[-1])
+    assert total_rows == m and total_nnz == int(rp[-1])
