@@ -134,7 +134,7 @@ struct XsRange {
     int row0;
     int nrows;
     int wide;
-    int pad;
+    int widx;         // wide: index among the wide ranges (arrival counter), else -1
     long long pbase;  // wide: offset of the range's [G][nrows] partials
 };
 
@@ -144,12 +144,21 @@ struct XsArgs {
     const uint32_t *key;
     const double *val;
     const int *qitems;      // [8][qstride][2] sub-item pairs (range << 8 | XCD + 1, 0 = narrow; -1 = none)
-    int *qhead;             // [8] claim counters + [8] exit count; the last workgroup re-zeroes them
+    int *qhead;             // [8] claim heads of this launch (start past the static items)
+    int *qreset;            // the other parity's heads, re-armed to qstat by block 0
+    int qstat[8];           // items per queue taken statically (block b: queue b%8, index b/8)
+    int dynamic;            // items beyond the static share exist (claims needed)
+    int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
+    int nrtasks;
+    const int2 *rtasks;     // (range, first row) reduce tasks
+    unsigned *arrive;       // per wide range: sub-items counted in, cumulative
+    unsigned epoch;         // this launch's number (want 8 * epoch arrivals)
     double *partial;
     int qlen[8];
     int qstride;
     int G, q, Wg;
     int use_xcc;
+    int kstride, vstride;   // chunk strides in 16-B units (keys, values)
     long long *trace;       // debugging aid (SBLAS_XS_TRACE), else null
 };
 
@@ -159,12 +168,21 @@ struct XsPlan {
     XsRange *ranges = nullptr;
     int *wide = nullptr;         // [nwide] range ids
     long long *blk = nullptr;
-    uint32_t *key = nullptr;
-    double *val = nullptr;
+    uint32_t *key = nullptr;     // owns the chunk storage (keys and values)
+    double *val = nullptr;       // values inside it (interleaved per chunk by default)
+    int kstride = 64, vstride = 128;
     int *qitems = nullptr;
-    int *qhead = nullptr;
+    int *qhead = nullptr;        // [2][16]: claim heads per launch parity
+    mutable int parity = 0;      // flips every launch (stream-ordered launches)
     double *partial = nullptr;
     int qlen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int qstat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int dynamic = 0;
+    bool fused = false;          // in-kernel reduce of the wide ranges
+    int nrtasks = 0;
+    int2 *rtasks = nullptr;
+    unsigned *arrive = nullptr;
+    mutable long long epoch = 0; // launches so far (arrival counters are cumulative)
     int qstride = 0;
     long long nchunks = 0;       // 256-entry chunks (blocks padded to whole chunks)
     bool pair = true;            // items pair two sub-items (two teams of waves)

@@ -73,15 +73,28 @@ __device__ __forceinline__ int xs_xcc_id()
 }
 
 // Claims a work item: returns its slot in qitems (queue * qstride + index),
-// own XCD's queue first, or -1 when every queue is empty.
+// own XCD's queue first, or -1 when every queue is empty.  Called by a whole
+// wave: lanes 0-7 read the eight claim heads at once (agent-scope loads that
+// go past the XCD's L2, ~1-2 us each under load), so finding every queue
+// empty -- what each workgroup does at its end -- costs one round trip
+// instead of eight in a row.  The result is valid in every lane.
 __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 {
-    for (int k = 0; k < 8; ++k) {
-        const int qq = (xcc + k) & 7;
-        if (__hip_atomic_load(&a.qhead[qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.qlen[qq])
-            continue;
-        const int idx = atomicAdd(&a.qhead[qq], 1);
-        if (idx < a.qlen[qq]) return qq * a.qstride + idx;
+    const int lane = threadIdx.x & 63;
+    int qq = (xcc + lane) & 7, ql = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ql = qq == k ? a.qlen[k] : ql;
+    const bool open = lane < 8 &&
+                      __hip_atomic_load(&a.qhead[qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ql;
+    unsigned long long mask = __ballot(open);
+    while (mask) {
+        const int l = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        const int q = __builtin_amdgcn_readfirstlane((xcc + l) & 7);
+        int idx = 0;
+        if (lane == 0) idx = atomicAdd(&a.qhead[q], 1);
+        idx = __shfl(idx, 0, 64);
+        if (idx < a.qlen[q]) return q * a.qstride + idx;
     }
     return -1;
 }
@@ -101,7 +114,7 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 // bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0].
 template <int kMode, int S>
 __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
-                                          const v2d *__restrict__ val2, long long c0,
+                                          const v2d *__restrict__ val2, int ks, int vs, long long c0,
                                           long long c1, const long long *bnd, int gb, int Wg,
                                           const double *__restrict__ x, double *acc, int wave)
 {
@@ -116,9 +129,9 @@ __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
             const long long c = c0 + wave + (t * U + u) * S;
             const bool live = c < c1;
             const long long ci = live ? c : c1 - 1;
-            kk[u] = __builtin_nontemporal_load(key4 + ci * 64 + (live ? lane : 0));
-            va[u] = __builtin_nontemporal_load(val2 + ci * 128 + (live ? lane : 0));
-            vb[u] = __builtin_nontemporal_load(val2 + ci * 128 + 64 + (live ? lane : 0));
+            kk[u] = __builtin_nontemporal_load(key4 + ci * ks + (live ? lane : 0));
+            va[u] = __builtin_nontemporal_load(val2 + ci * vs + (live ? lane : 0));
+            vb[u] = __builtin_nontemporal_load(val2 + ci * vs + 64 + (live ? lane : 0));
             while (ci >= nb) nb = bnd[++gi + 1];
             xo[u] = (gb + gi) * Wg;
         }
@@ -177,9 +190,9 @@ __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
 // pair end together however their narrow/wide costs compare.  Same pipeline
 // (gathers | next loads | adds), a claim per stage; claims are monotone per
 // wave, so the group walk over bnd[] stays forward-only.
-template <int kMode>
+template <int kMode, int U = kXsUnroll>
 __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
-                                              const v2d *__restrict__ val2, int *ctr,
+                                              const v2d *__restrict__ val2, int ks, int vs, int *ctr,
                                               long long c0, long long c1, const long long *bnd,
                                               int gb, int Wg, const double *__restrict__ x,
                                               double *acc)
@@ -188,7 +201,6 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
     if (__builtin_amdgcn_readfirstlane(
             __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= c1 - c0)
         return;  // drained already (the common case for a helper)
-    constexpr int U = kXsUnroll;
     const int lane = threadIdx.x & 63;
     int gi = 0;
     long long nb = bnd[1];
@@ -203,9 +215,15 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
             const long long c = cb + u;
             const bool live = c < c1;
             const long long ci = live ? c : c1 - 1;
-            kk[u] = __builtin_nontemporal_load(key4 + ci * 64 + (live ? lane : 0));
-            va[u] = __builtin_nontemporal_load(val2 + ci * 128 + (live ? lane : 0));
-            vb[u] = __builtin_nontemporal_load(val2 + ci * 128 + 64 + (live ? lane : 0));
+            if constexpr ((kMode & 4) != 0) {  // experiment: plain (temporal) loads
+                kk[u] = key4[ci * ks + (live ? lane : 0)];
+                va[u] = val2[ci * vs + (live ? lane : 0)];
+                vb[u] = val2[ci * vs + 64 + (live ? lane : 0)];
+            } else {
+                kk[u] = __builtin_nontemporal_load(key4 + ci * ks + (live ? lane : 0));
+                va[u] = __builtin_nontemporal_load(val2 + ci * vs + (live ? lane : 0));
+                vb[u] = __builtin_nontemporal_load(val2 + ci * vs + 64 + (live ? lane : 0));
+            }
             while (ci >= nb) nb = bnd[++gi + 1];
             xo[u] = (gb + gi) * Wg;
         }
@@ -263,6 +281,51 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
     }
 }
 
+// Fused reduce of the wide ranges (replaces k_xsort_reduce when a.fused):
+// after its last item a workgroup claims reduce tasks (a wide range's rows
+// [r0, r0 + blockDim)) from a global head, waits until all 8 sub-items of
+// that range have counted in, and writes y = alpha * sum_k partial[k] (XCD
+// order) + beta*y.  Arrival counters are cumulative over launches (a launch
+// waits for 8 * epoch), so nothing is reset.  Every sub-item belongs to an
+// item already claimed by a running workgroup (the queues are empty when a
+// workgroup gets here), so the wait ends; it is bounded all the same.
+template <bool kBeta>
+__device__ void xs_reduce_phase(const XsArgs &a, double alpha, double beta, double *__restrict__ y)
+{
+    __shared__ int s_task;
+    for (;;) {
+        if (threadIdx.x == 0) s_task = atomicAdd(&a.qhead[8], 1);
+        __syncthreads();
+        const int t = s_task;
+        __syncthreads();
+        if (t >= a.nrtasks) return;
+        const int2 task = a.rtasks[t];
+        const XsRange R = a.ranges[task.x];
+        if (threadIdx.x == 0) {
+            const unsigned want = 8u * a.epoch;
+            unsigned spins = 0;
+            while (__hip_atomic_load(&a.arrive[R.widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24)) break;  // bounded: a broken protocol gives a wrong y, not a hang
+            }
+        }
+        __syncthreads();
+        const int r = task.y + (int)threadIdx.x;
+        if (r < R.nrows) {
+            const double *p = a.partial + R.pbase + r;
+            double v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                v[k] = __hip_atomic_load(p + (long long)k * R.nrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += v[k];
+            double *yr = y + R.row0 + r;
+            *yr = kBeta ? alpha * s + beta * *yr : alpha * s;
+        }
+    }
+}
+
 // kWG threads per workgroup: 1024 (16384 LDS rows, one workgroup per CU) or
 // 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
 // two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
@@ -270,7 +333,7 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
 // kDyn (pairs only): the chunks of both sub-items are claimed dynamically
 // (xs_stream_dyn); a team drains its own streams, then its partner's.
 template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false,
-          bool kDyn = false>
+          bool kDyn = false, int kU = kXsUnroll>
 __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     const double *__restrict__ x,
                                                     double alpha, double beta,
@@ -299,22 +362,36 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     const v2d *val2 = reinterpret_cast<const v2d *>(a.val);
     const int xcc = a.use_xcc ? xs_xcc_id() : (int)(blockIdx.x & 7);
     const long long t_entry = kTrace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-    if (threadIdx.x == 0) s_item = xs_claim(a, xcc);
+    // First item: static, block b takes index b/8 of queue b%8 (the hardware
+    // deals blocks to the XCDs round robin, so queue b%8 is normally b's own
+    // XCD's; placement only matters for speed).  Items beyond the static
+    // share (a.dynamic) are claimed from the per-XCD queues, whose heads
+    // start past the static items.  No atomic on the common path.
+    int first = -1;
+    {
+        const int qb = (int)(blockIdx.x & 7), ib = (int)(blockIdx.x >> 3);
+        if (ib < a.qstat[qb]) first = qb * a.qstride + ib;
+    }
+    // re-arm the other parity's heads for the next launch of this plan
+    // (launches of one plan are ordered by their stream; this launch's heads
+    // were armed by the previous one or by the plan build)
+    if (blockIdx.x == 0 && threadIdx.x == 8)  // the fused reduce's task head
+        __hip_atomic_store(&a.qreset[8], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x < 8) {
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = (int)threadIdx.x == k ? a.qstat[k] : v;
+        __hip_atomic_store(&a.qreset[threadIdx.x], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) {
+        const int it = (first >= 0 || !a.dynamic) ? first : xs_claim(a, xcc);
+        if (threadIdx.x == 0) s_item = it;
+    }
     for (;;) {
         __syncthreads();
         const int slot = s_item;
         if (slot < 0) {  // workgroup-uniform
-            // the last workgroup out re-arms the queues for the next launch
-            // (every claim has returned before its workgroup counts itself
-            // out), so no memset precedes the kernel; launches of one plan
-            // are serialised by their stream
-            if (threadIdx.x == 0) {
-                __threadfence();
-                if (atomicAdd(&a.qhead[8], 1) == (int)gridDim.x - 1) {
-                    for (int k = 0; k < 8; ++k) atomicExch(&a.qhead[k], 0);
-                    atomicExch(&a.qhead[8], 0);
-                }
-            }
+            if (a.fused) xs_reduce_phase<kBeta>(a, alpha, beta, y);
             if (kTrace && threadIdx.x == 0) {  // per-workgroup row: entry .. exit
                 const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
                 a.trace[ts] = -2;
@@ -362,7 +439,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
         int pre = 0;
         long long t0 = 0;
         if (threadIdx.x == 0) {
-            pre = atomicAdd(&a.qhead[xcc], 1);
+            if (a.dynamic) pre = atomicAdd(&a.qhead[xcc], 1);
             if (kTrace) t0 = (long long)__builtin_amdgcn_s_memrealtime();
         }
         if constexpr (kDyn) {
@@ -375,26 +452,29 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                 if (hs < 0 || (seg && (hk1 || hg0 == 0))) continue;  // uniform
                 const long long *hb = s_bnd_all[h] + (seg ? 128 : 0);
                 const int hn = seg ? hg0 : hn1;
-                xs_stream_dyn<kMode>(key4, val2, &s_ctr[h][seg], hb[0], hb[hn], hb, seg ? 0 : hg0,
+                xs_stream_dyn<kMode, kU>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], hb[0], hb[hn], hb, seg ? 0 : hg0,
                                      a.Wg, x, acc_all + h * kXsHalfRows);
             }
         } else if (sub >= 0) {
             if (SA == SB || half == 0) {  // one inlined copy when the teams are equal
-                xs_stream<kMode, SA>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
+                xs_stream<kMode, SA>(key4, val2, a.kstride, a.vstride, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
                 if (!k1 && g0 > 0)
-                    xs_stream<kMode, SA>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
+                    xs_stream<kMode, SA>(key4, val2, a.kstride, a.vstride, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
                                          a.Wg, x, acc, hwave);
             } else if constexpr (kPair && SA != SB) {
-                xs_stream<kMode, SB>(key4, val2, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
+                xs_stream<kMode, SB>(key4, val2, a.kstride, a.vstride, s_bnd[0], s_bnd[n1], s_bnd, g0, a.Wg, x, acc, hwave);
                 if (!k1 && g0 > 0)
-                    xs_stream<kMode, SB>(key4, val2, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
+                    xs_stream<kMode, SB>(key4, val2, a.kstride, a.vstride, s_bnd[128], s_bnd[128 + g0], s_bnd + 128, 0,
                                          a.Wg, x, acc, hwave);
             }
         }
         if (kTrace && (threadIdx.x & 63) == 0)  // debugging aid: this team's last wave
             atomicMax(&s_tend[half], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        if (threadIdx.x == 0)
-            s_item = pre < a.qlen[xcc] ? xcc * a.qstride + pre : xs_claim(a, xcc);
+        if (threadIdx.x < 64) {
+            const int own = __shfl(pre, 0, 64);
+            const int it = !a.dynamic ? -1 : own < a.qlen[xcc] ? xcc * a.qstride + own : xs_claim(a, xcc);
+            if (threadIdx.x == 0) s_item = it;
+        }
         __syncthreads();
         if (kTrace && threadIdx.x == 0) {  // debugging aid (SBLAS_XS_TRACE): item timeline
             const long long ts = 1 + (long long)kXsTrace * atomicAdd((unsigned long long *)a.trace, 1ULL);
@@ -406,14 +486,46 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             a.trace[ts + 5] = (long long)s_tend[1];
         }
         if (sub >= 0) {
+            // epilogue: a team owns <= kXsHalfRows rows (kWG rows per thread
+            // pass at most kEp passes); every y load of the thread is issued
+            // before the first use, so the y latency is paid once, not once
+            // per row (a rolled loop put ~10 us of serial latency on the end
+            // of every item)
+            constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
+            constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
             if (k1) {
                 double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
-                for (int r = ht; r < R.nrows; r += NT) out[r] = acc[r];
+                // agent-scope (sc1) stores: the fused reduce may read them on
+                // another XCD, whose L2 is not coherent with this one
+#pragma unroll
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = ht + e * NT;
+                    if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             } else {
                 double *yr = y + R.row0;
-                for (int r = ht; r < R.nrows; r += NT)
-                    yr[r] = kBeta ? alpha * acc[r] + beta * yr[r] : alpha * acc[r];
+                double y0[kEp];
+                if constexpr (kBeta) {
+#pragma unroll
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        y0[e] = r < R.nrows ? yr[r] : 0.0;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = ht + e * NT;
+                    if (r < R.nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
+                }
             }
+        }
+        if (a.fused) {
+            // count this team's wide sub-item in once every wave's partial
+            // stores have drained (vmcnt(0), then the barrier)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (sub >= 0 && k1 && ht == 0)
+                __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // (the barrier at the loop top orders these reads of acc before the
         // next item's zeroing, and s_bnd's reuse)
@@ -445,11 +557,12 @@ void free_xsort_plan(sblas_csr_s &A)
     (void)hipFree(P.ranges);
     (void)hipFree(P.wide);
     (void)hipFree(P.blk);
-    (void)hipFree(P.key);
-    (void)hipFree(P.val);
+    (void)hipFree(P.key);  // P.val points into the same allocation
     (void)hipFree(P.qitems);
     (void)hipFree(P.qhead);
     (void)hipFree(P.partial);
+    (void)hipFree(P.rtasks);
+    (void)hipFree(P.arrive);
     A.xs = XsPlan{};
 }
 
@@ -609,8 +722,22 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
 
     // pass 2: fill each block, sort it by (column, row), pad it to whole
     // chunks and store every chunk lane-transposed (header comment)
-    std::vector<uint32_t> hkey((size_t)nchunks * kXsChunk);
-    std::vector<double> hv((size_t)nchunks * kXsChunk);
+    // one allocation: interleaved (default) = per chunk 1 KiB of keys then
+    // 2 KiB of values, so a chunk is ONE 3-KiB run in HBM; split
+    // (SBLAS_XS_KV=0) = all keys, then all values
+    const bool kv = !(getenv("SBLAS_XS_KV") && atoi(getenv("SBLAS_XS_KV")) == 0);
+    const size_t cbytes = (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
+    std::vector<unsigned char> hbuf((size_t)std::max<long long>(nchunks, 1) * cbytes);
+    auto chunk_keys = [&](long long c) {
+        return (uint32_t *)(hbuf.data() + (kv ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
+    };
+    auto chunk_vals = [&](long long c) {
+        return (double *)(hbuf.data() + (kv ? (size_t)c * cbytes + kXsChunk * sizeof(uint32_t)
+                                            : (size_t)std::max<long long>(nchunks, 1) * kXsChunk * sizeof(uint32_t) +
+                                                  (size_t)c * kXsChunk * sizeof(double)));
+    };
+    P.kstride = kv ? (int)(cbytes / 16) : kXsChunk * 4 / 16;
+    P.vstride = kv ? (int)(cbytes / 16) : kXsChunk * 8 / 16;
     bool bad = false;
 #pragma omp parallel
     {
@@ -640,8 +767,8 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
                                         const std::pair<uint32_t, double> &v) { return u.first < v.first; });
                 const long long c0 = blk[(size_t)i * G + g], c1 = blk[(size_t)i * G + g + 1];
                 for (long long c = c0; c < c1; ++c) {
-                    uint32_t *kc = hkey.data() + c * kXsChunk;
-                    double *vc = hv.data() + c * kXsChunk;
+                    uint32_t *kc = chunk_keys(c);
+                    double *vc = chunk_vals(c);
                     for (int p = 0; p < kXsChunk; ++p) {
                         const long long src = (c - c0) * kXsChunk + p;
                         const bool in = src < (long long)b.size();
@@ -662,11 +789,15 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     std::vector<int> wide, nsub;
     std::vector<std::vector<int>> wsub(8);
     long long pbase = 0;
+    std::vector<int2> rtasks;  // fused reduce: (range, first row) per kXsThreads rows
     for (int i = 0; i < I; ++i) {
         XsRange &R = ranges[i];
+        R.widx = -1;
         if (R.wide) {
             R.pbase = pbase;
             pbase += 8LL * R.nrows;
+            R.widx = (int)wide.size();
+            for (int r0 = 0; r0 < R.nrows; r0 += kXsThreads) rtasks.push_back(make_int2(i, r0));
             wide.push_back(i);
             for (int k = 0; k < 8; ++k) wsub[k].push_back((i << 8) | (k + 1));
         } else {
@@ -725,6 +856,13 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         P.nitems += P.qlen[k];
     }
     P.grid = std::min(P.nitems, resident);
+    int nstat = 0;
+    for (int k = 0; k < 8; ++k) {
+        const int blocks_k = P.grid > k ? (P.grid - k + 7) / 8 : 0;  // blocks b < grid with b % 8 == k
+        P.qstat[k] = std::min(P.qlen[k], blocks_k);
+        nstat += P.qstat[k];
+    }
+    P.dynamic = nstat < P.nitems ? 1 : 0;
     std::vector<int> qflat((size_t)16 * P.qstride, -1);
     for (int k = 0; k < 8; ++k)
         for (size_t j = 0; j < q[k].size(); ++j) {
@@ -732,23 +870,39 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             qflat[2 * ((size_t)k * P.qstride + j) + 1] = q[k][j].second;
         }
 
-    const size_t ne = (size_t)std::max<long long>(nchunks, 1) * kXsChunk;
+
     SBLAS_HIP(hipMalloc(&P.ranges, sizeof(XsRange) * std::max(I, 1)));
     SBLAS_HIP(hipMalloc(&P.wide, sizeof(int) * std::max<size_t>(wide.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.blk, sizeof(long long) * blk.size()));
-    SBLAS_HIP(hipMalloc(&P.key, sizeof(uint32_t) * ne));
-    SBLAS_HIP(hipMalloc(&P.val, sizeof(double) * ne));
+    SBLAS_HIP(hipMalloc(&P.key, hbuf.size()));
+    P.val = (double *)((unsigned char *)P.key + ((unsigned char *)chunk_vals(0) - hbuf.data()));
     SBLAS_HIP(hipMalloc(&P.qitems, sizeof(int) * qflat.size()));
-    SBLAS_HIP(hipMalloc(&P.qhead, sizeof(int) * 16));  // [8] claim heads, [8] exit count
-    SBLAS_HIP(hipMemset(P.qhead, 0, sizeof(int) * 16));
+    SBLAS_HIP(hipMalloc(&P.qhead, sizeof(int) * 32));  // [2 parities][8 claim heads + pad]
+    {
+        std::vector<int> h(32, 0);
+        for (int k = 0; k < 8; ++k) h[k] = h[16 + k] = P.qstat[k];
+        SBLAS_HIP(hipMemcpy(P.qhead, h.data(), sizeof(int) * 32, hipMemcpyHostToDevice));
+    }
     SBLAS_HIP(hipMalloc(&P.partial, sizeof(double) * std::max<long long>(pbase, 1)));
+    // fused reduce (SBLAS_XS_FUSE=1; needs the 1024-thread workgroup, one
+    // task = kXsThreads rows).  Not the default: on config 2 its claim ->
+    // poll -> load chain lands ~18 us of latency on the kernel's tail
+    // against 6 us for the separate k_xsort_reduce launch.
+    P.fused = P.nt == kXsThreads && !wide.empty() && getenv("SBLAS_XS_FUSE") &&
+              atoi(getenv("SBLAS_XS_FUSE")) != 0;
+    P.nrtasks = (int)rtasks.size();
+    SBLAS_HIP(hipMalloc(&P.rtasks, sizeof(int2) * std::max<size_t>(rtasks.size(), 1)));
+    SBLAS_HIP(hipMalloc(&P.arrive, sizeof(unsigned) * std::max<size_t>(wide.size(), 1)));
+    SBLAS_HIP(hipMemset(P.arrive, 0, sizeof(unsigned) * std::max<size_t>(wide.size(), 1)));
+    if (!rtasks.empty())
+        SBLAS_HIP(hipMemcpy(P.rtasks, rtasks.data(), sizeof(int2) * rtasks.size(), hipMemcpyHostToDevice));
+    P.epoch = 0;
     if (I) SBLAS_HIP(hipMemcpy(P.ranges, ranges.data(), sizeof(XsRange) * I, hipMemcpyHostToDevice));
     if (!wide.empty())
         SBLAS_HIP(hipMemcpy(P.wide, wide.data(), sizeof(int) * wide.size(), hipMemcpyHostToDevice));
     SBLAS_HIP(hipMemcpy(P.blk, blk.data(), sizeof(long long) * blk.size(), hipMemcpyHostToDevice));
     if (nchunks) {
-        SBLAS_HIP(hipMemcpy(P.key, hkey.data(), sizeof(uint32_t) * hkey.size(), hipMemcpyHostToDevice));
-        SBLAS_HIP(hipMemcpy(P.val, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
+        SBLAS_HIP(hipMemcpy(P.key, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
     }
     SBLAS_HIP(hipMemcpy(P.qitems, qflat.data(), sizeof(int) * qflat.size(), hipMemcpyHostToDevice));
     P.ready = true;
@@ -774,10 +928,24 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.blk = P.blk;
     a.key = P.key;
     a.val = P.val;
+    a.kstride = P.kstride;
+    a.vstride = P.vstride;
     a.qitems = P.qitems;
-    a.qhead = P.qhead;
+    a.qhead = P.qhead + 16 * P.parity;        // this launch's claim heads
+    a.qreset = P.qhead + 16 * (1 - P.parity);  // re-armed for the next launch
+    P.parity ^= 1;
     a.partial = P.partial;
-    for (int k = 0; k < 8; ++k) a.qlen[k] = P.qlen[k];
+    for (int k = 0; k < 8; ++k) {
+        a.qlen[k] = P.qlen[k];
+        a.qstat[k] = P.qstat[k];
+    }
+    a.dynamic = P.dynamic;
+    a.fused = P.fused ? 1 : 0;
+    a.rtasks = P.rtasks;
+    a.nrtasks = P.nrtasks;
+    a.arrive = P.arrive;
+    if (P.fused) ++P.epoch;
+    a.epoch = (unsigned)P.epoch;
     a.qstride = P.qstride;
     a.G = P.G;
     a.q = P.q;
@@ -803,6 +971,19 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else kern = b ? k_spmv_xsort<true, 0, W, true> : k_spmv_xsort<false, 0, W, true>;
     } else {
         kern = b ? k_spmv_xsort<true, 0, W, false> : k_spmv_xsort<false, 0, W, false>;
+    }
+    static const int xu = [] {  // experiments: chunks per pipeline stage (dynamic claims)
+        const char *e = getenv("SBLAS_XS_U");
+        return e ? atoi(e) : kXsUnroll;
+    }();
+    if (P.pair && P.dyn && b && (xu != kXsUnroll || (mode & 4))) {
+#define XS_DYN(M, U) k_spmv_xsort<true, M, W, true, 8, false, true, U>
+        const int mm = mode & 6;
+        if (xu == 1) kern = mm == 0 ? XS_DYN(0, 1) : mm == 2 ? XS_DYN(2, 1) : mm == 4 ? XS_DYN(4, 1) : XS_DYN(6, 1);
+        else if (xu == 3) kern = mm == 0 ? XS_DYN(0, 3) : mm == 2 ? XS_DYN(2, 3) : mm == 4 ? XS_DYN(4, 3) : XS_DYN(6, 3);
+        else if (xu == 4) kern = mm == 0 ? XS_DYN(0, 4) : mm == 2 ? XS_DYN(2, 4) : mm == 4 ? XS_DYN(4, 4) : XS_DYN(6, 4);
+        else kern = mm == 4 ? XS_DYN(4, 2) : XS_DYN(6, 2);
+#undef XS_DYN
     }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
     if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
@@ -833,7 +1014,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
             fclose(f);
         }
     }
-    if (P.nwide) {
+    if (P.nwide && !P.fused) {
         const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
         if (b)
             hipLaunchKernelGGL(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide,

@@ -74,8 +74,8 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
 
 @pytest.mark.parametrize("algo,env", [
     (1, {}), (2, {}), (3, {}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
-    (5, {"SBLAS_XS_Q": "3"})],
-    ids=["rowsplit", "csr5", "csr5_alt", "panel", "xsort", "xsort_static", "xsort_q3"])
+    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"})],
+    ids=["rowsplit", "csr5", "csr5_alt", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
     for k, v in env.items():
