@@ -143,6 +143,7 @@ struct XsArgs {
     const long long *blk;   // [nranges*G + 1] block offsets
     const uint32_t *key;
     const double *val;
+    const long long *xrec;  // per (slot, team): sub, row0|nrows<<32, pbase, widx, G+1 block offsets
     const int *qitems;      // [8][qstride][2] sub-item pairs (range << 8 | XCD + 1, 0 = narrow; -1 = none)
     int *qhead;             // [8] claim heads of this launch (start past the static items)
     int *qreset;            // the other parity's heads, re-armed to qstat by block 0
@@ -172,6 +173,7 @@ struct XsPlan {
     double *val = nullptr;       // values inside it (interleaved per chunk by default)
     int kstride = 64, vstride = 128;
     int *qitems = nullptr;
+    long long *xrec = nullptr;   // item records (see XsArgs)
     int *qhead = nullptr;        // [2][16]: claim heads per launch parity
     mutable int parity = 0;      // flips every launch (stream-ordered launches)
     double *partial = nullptr;

@@ -342,6 +342,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     static_assert(kWG == 1024 || (kWG == 512 && !kPair), "workgroup shapes");
     __shared__ double acc_all[kWG == 1024 ? kXsRows : kXsHalfRows];
     __shared__ long long s_bnd_all[2][256];
+    __shared__ long long s_rec_all[2][128 + 5];
     __shared__ unsigned long long s_tend[2];
     __shared__ int s_item;
     __shared__ int s_ctr[2][2];  // kDyn: claimed chunks per (team, segment)
@@ -406,14 +407,25 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
         // sub = range << 8 | k: k+1 = wide sub-item of XCD k (its q groups
         // [kq, kq+q), partial slot k); 0 = narrow (all G groups, starting at
         // this XCD's first group and wrapping); -1 = nothing for this team
-        const int sub = a.qitems[2 * slot + half];
+        // the team's item record (host-built per (slot, team)): sub, row0 |
+        // nrows << 32, pbase, widx, then the range's G+1 block offsets -- one
+        // round trip of independent loads instead of sub -> range -> blocks
+        {
+            const long long *rec = a.xrec + (long long)(2 * slot + half) * (a.G + 5);
+            for (int j = ht; j < a.G + 5; j += NT) s_rec_all[half][j] = rec[j];
+        }
+        __syncthreads();
+        long long *s_rec = s_rec_all[half];
+        const int sub = (int)s_rec[0];
         XsRange R{};
         int k1 = 0, g0 = 0, n1 = 0;
         if (sub >= 0) {  // team-uniform
-            const int ri = sub >> 8;
             k1 = sub & 255;
-            R = a.ranges[ri];
-            const long long *bo = a.blk + (long long)ri * a.G;
+            R.row0 = (int)(s_rec[1] & 0xffffffffLL);
+            R.nrows = (int)(s_rec[1] >> 32);
+            R.pbase = s_rec[2];
+            R.widx = (int)s_rec[3];
+            const long long *bo = s_rec + 4;
             g0 = k1 ? (k1 - 1) * a.q : xcc * a.q;
             // s_bnd[j] = first chunk of group g0 + j: segment 1 is groups
             // [g0, g0+n1); a narrow sub-item's segment 2 is groups [0, g0)
@@ -486,11 +498,12 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             a.trace[ts + 5] = (long long)s_tend[1];
         }
         if (sub >= 0) {
-            // epilogue: a team owns <= kXsHalfRows rows (kWG rows per thread
-            // pass at most kEp passes); every y load of the thread is issued
-            // before the first use, so the y latency is paid once, not once
-            // per row (a rolled loop put ~10 us of serial latency on the end
-            // of every item)
+            // epilogue: a team owns <= kXsHalfRows rows, at most kEp per
+            // thread; every y load of the thread is issued before the first
+            // use, so the y latency is paid once, not once per row (a rolled
+            // loop put ~10 us of serial latency on the end of every item).
+            // (Issuing them before the barrier above spilled registers: the
+            // kernel sits at its 128-VGPR cap.)
             constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
             constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
             if (k1) {
@@ -562,6 +575,7 @@ void free_xsort_plan(sblas_csr_s &A)
     (void)hipFree(P.qhead);
     (void)hipFree(P.partial);
     (void)hipFree(P.rtasks);
+    (void)hipFree(P.xrec);
     (void)hipFree(P.arrive);
     A.xs = XsPlan{};
 }
@@ -905,6 +919,23 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMemcpy(P.key, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
     }
     SBLAS_HIP(hipMemcpy(P.qitems, qflat.data(), sizeof(int) * qflat.size(), hipMemcpyHostToDevice));
+    {
+        const size_t rl = (size_t)G + 5;
+        std::vector<long long> xrec(qflat.size() * rl, -1);
+        for (size_t s2 = 0; s2 < qflat.size(); ++s2) {
+            const int sub = qflat[s2];
+            long long *r = xrec.data() + s2 * rl;
+            r[0] = sub;
+            if (sub < 0) continue;
+            const XsRange &R = ranges[(size_t)(sub >> 8)];
+            r[1] = (long long)(unsigned)R.row0 | ((long long)R.nrows << 32);
+            r[2] = R.pbase;
+            r[3] = R.widx;
+            for (int g = 0; g <= G; ++g) r[4 + g] = blk[(size_t)(sub >> 8) * G + g];
+        }
+        SBLAS_HIP(hipMalloc(&P.xrec, sizeof(long long) * xrec.size()));
+        SBLAS_HIP(hipMemcpy(P.xrec, xrec.data(), sizeof(long long) * xrec.size(), hipMemcpyHostToDevice));
+    }
     P.ready = true;
     return SBLAS_OK;
 }
@@ -931,6 +962,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.kstride = P.kstride;
     a.vstride = P.vstride;
     a.qitems = P.qitems;
+    a.xrec = P.xrec;
     a.qhead = P.qhead + 16 * P.parity;        // this launch's claim heads
     a.qreset = P.qhead + 16 * (1 - P.parity);  // re-armed for the next launch
     P.parity ^= 1;

@@ -18,7 +18,9 @@ from typing import Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsblas.so")
+# SBLAS_LIB: an alternative build of the same library (A/B timing of two
+# builds on one box); the default is the in-tree build
+LIB_PATH = os.environ.get("SBLAS_LIB") or os.path.join(_HERE, "libsblas.so")
 
 ROWSPLIT = 1  # test_spmv kernel 1 (csrmv)
 CSR5 = 2      # test_spmv kernel 2/3 (csrmv_mp / CSR5)

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--cols", choices=["random", "prefix"], default="random")
     ap.add_argument("--cold", action="store_true", help="1 GiB scrub before every launch")
+    ap.add_argument("--scrub", choices=["write", "read"], default="write",
+                    help="cold scrub: read+write (add_) or read-only (sum)")
     a = ap.parse_args()
     import torch
     import sblas
@@ -43,7 +45,10 @@ def main():
         A.spmv(algo, 0.84, x.data_ptr(), 0.39, y.data_ptr(), s.cuda_stream)
         for _ in range(a.reps):
             if scrub is not None:
-                scrub.add_(1)
+                if a.scrub == "write":
+                    scrub.add_(1)
+                else:
+                    scrub.sum(dtype=torch.int64)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             A.spmv(algo, 0.84, x.data_ptr(), 0.39, y.data_ptr(), s.cuda_stream)
