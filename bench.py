@@ -10,10 +10,11 @@ the whole matrix with every input already resident in HBM; at N > 1 the
 rows are dealt to the ranks in equal cyclic chunks (x replicated) and a step
 also includes the RCCL allgather of the y slices plus their device-side
 placement (strong scaling: the same matrix at every N).  The headline is
-cold-cache (a 1 GiB scrub before each of the K
-timed steps, so that at N = 8 a rank's ~67 MB slice cannot sit in the 256 MB
-Infinity Cache; each step between its own barrier + synchronize pair, the
-scrub outside the timed region).  A cold step's time is its device span: HIP
+cold-cache (a 1 GiB read-only sweep before each
+of the K timed steps, so that at N = 8 a rank's ~67 MB slice cannot sit in the
+256 MB Infinity Cache; each step between its own barrier + synchronize pair,
+the sweep outside the timed region; `--scrub write` is round 1's read+write
+scrub, whose dirty lines the next step had to write back).  A cold step's time is its device span: HIP
 events on the launch stream from before the kernel to after the exchange and
 merge, max over ranks (the host's barrier round trips between scrub and step
 are reported beside as `cold_host_wall_ms_per_step`).  The warm number (K
@@ -82,11 +83,20 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
             if el > share or reps >= 200:
                 return reps, el / reps
 
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     r_mt, t_mt = timeit(f, (threads,), budget_s * 0.5)
     r_st, t_st = timeit(g, (), budget_s * 0.5)
     return {
         "value": round(2.0 * nnz / t_mt / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
-        "kind": "port",
+        "kind": "port", "cpu_model": model,
         "sample": (f"full config-2 matrix, orc_csr_spmv_omp (OpenMP, schedule dynamic) x{r_mt} "
                    f"reps, {t_mt * 1e3:.1f} ms/SpMV; single-core scalar port orc_csr_spmv "
                    f"x{r_st}: {t_st * 1e3:.1f} ms/SpMV = {2.0 * nnz / t_st / 1e9:.3f} GFLOP/s"),
@@ -128,7 +138,7 @@ def main() -> int:
                          "oracle (rank 0; small n only)")
     ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
                     help="cold (default; SURVEY M1-cache / BASELINE.md: the headline uses cold "
-                         "timing): a 1 GiB scrub before every timed step evicts the 256 MB "
+                         "timing): a 1 GiB sweep (--scrub) before every timed step evicts the 256 MB "
                          "Infinity Cache and the L2s, each of the K steps bracketed by its own "
                          "barrier + synchronize; warm: K back-to-back steps bracketed by one "
                          "barrier + synchronize on each side.  The other mode is always measured "
@@ -137,6 +147,12 @@ def main() -> int:
                     help="N > 1 row distribution: cyclic equal-row chunks (default; no padding, "
                          "whole rows) or one nnz-balanced range per rank (spMV_mgpu_v1's split, "
                          "with split-row carries; always used with --exchange allreduce)")
+    ap.add_argument("--scrub", choices=["read", "write"], default="read",
+                    help="cold-cache eviction before each cold step: a 1 GiB read-only sweep "
+                         "(default: leaves no dirty lines whose write-back the next step would "
+                         "pay) or read+write (add_, round 1's method)")
+    ap.add_argument("--no-rowsplit-beside", action="store_true",
+                    help="skip the row-split kernel's figure reported beside the headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -170,11 +186,14 @@ def main() -> int:
     nnz = int(rowptr[-1])
     prefix = args.cols == "prefix"
     t_gen = time.perf_counter()
-    if args.algo == "auto":
+    auto = args.algo == "auto"
+    if auto:
         # the column-sorted kernel's per-item costs (padding to 256-entry
         # chunks, item set-up) pay off on large slices; the XCD-panel row
-        # split wins below ~8M nonzeros per rank
-        args.algo = "xsort" if nnz / world >= 8e6 else "panel"
+        # split wins below ~8M nonzeros per rank.  Its column
+        # groups cover at most 127 x 2^18 columns; past ~120 MiB of x the
+        # panel kernel is used as well.
+        args.algo = "xsort" if nnz / world >= 8e6 and n * 8 <= 120 * 2**20 else "panel"
     algo = algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
@@ -183,7 +202,13 @@ def main() -> int:
             lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, args.heavy, args.light,
                                               prefix=prefix, seed=42))
         t_gen = time.perf_counter() - t_gen
-        op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
+        try:
+            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
+        except sblas.SblasError:
+            if not (auto and algo == sblas.XSORT):
+                raise
+            args.algo, algo = "panel", sblas.PANEL  # the layout does not apply: fall back
+            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
         local_nnz = int(lrp[-1])
         partition = f"cyclic row chunks ({plan.chunk_rows} rows, {plan.nchunks} chunks)"
     else:
@@ -220,6 +245,12 @@ def main() -> int:
 
     scrub = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
 
+    def evict():
+        if args.scrub == "write":
+            scrub.add_(1)
+        else:
+            scrub.sum(dtype=torch.int64)
+
     def sync_barrier():
         torch.cuda.synchronize()
         if dist is not None:
@@ -239,6 +270,7 @@ def main() -> int:
         for k in range(args.steps):
             step(evs[k])
         sync_barrier()
+        run_warm.xch = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
         return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
 
     def run_cold():
@@ -257,23 +289,25 @@ def main() -> int:
         # spin-free pass and kept beside (wall_el).
         evs = events()
         for k in range(args.steps):
-            scrub.add_(1)  # 1 GiB read+write: evicts MALL (256 MB) and L2
+            evict()  # 1 GiB sweep: evicts MALL (256 MB) and L2
             sync_barrier()
             torch.cuda._sleep(500_000)
             step(evs[k])
             sync_barrier()
         wall_el = 0.0
         for k in range(args.steps):
-            scrub.add_(1)
+            evict()
             sync_barrier()
             t0 = time.perf_counter()
             step()
             sync_barrier()
             wall_el += time.perf_counter() - t0
         run_cold.wall_el = wall_el
+        run_cold.xch = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
         el = float(np.sum([a.elapsed_time(c) for a, _, c in evs])) * 1e-3
         return el, float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
     run_cold.wall_el = 0.0
+    run_cold.xch = run_warm.xch = 0.0
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -285,6 +319,31 @@ def main() -> int:
         else:
             el, kern_ms = run_warm()
             el_o, kern_o = run_cold()
+    xch_ms = run_cold.xch if args.cache == "cold" else run_warm.xch
+    rowsplit_beside = None
+    if world == 1 and algo != sblas.ROWSPLIT and not args.no_rowsplit_beside:
+        # configs[1] names the row-split kernel: its figure on the same
+        # matrix, same cold protocol, kernel events only
+        op.A.analyse(sblas.ROWSPLIT)
+        with torch.cuda.stream(stream):
+            for _ in range(2):
+                op.A.spmv(sblas.ROWSPLIT, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp)
+            rs = []
+            for _ in range(args.steps):
+                evict()
+                torch.cuda.synchronize()
+                torch.cuda._sleep(500_000)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                op.A.spmv(sblas.ROWSPLIT, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp)
+                e1.record(stream)
+                rs.append((e0, e1))
+            torch.cuda.synchronize()
+        rk = float(np.mean([a.elapsed_time(b) for a, b in rs]))
+        rowsplit_beside = {"kernel_ms": round(rk, 5),
+                           "gflops": round(2.0 * nnz / (rk * 1e-3) / 1e9, 3),
+                           "roofline_frac": round(local_bytes / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "cache": "cold"}
     del scrub
 
     check = None
@@ -305,7 +364,8 @@ def main() -> int:
             bound = orc.spmv_bound(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
             check = bool(np.all(np.abs(y_dev - want) <= bound))
     stats_dev = dev if (dist is None or args.dist_backend == "nccl") else torch.device("cpu")
-    stats = torch.tensor([el, kern_ms, local_bytes, local_flops, el_o, kern_o, run_cold.wall_el],
+    stats = torch.tensor([el, kern_ms, local_bytes, local_flops, el_o, kern_o, run_cold.wall_el, xch_ms,
+                          getattr(op, "plan_s", 0.0)],
                          dtype=torch.float64,
                          device=stats_dev)
     if dist is not None:
@@ -316,10 +376,12 @@ def main() -> int:
         el, kern_ms_max = float(mx[0]), float(mx[1])
         el_o, kern_o_max = float(mx[4]), float(mx[5])
         cold_wall = float(mx[6])
+        xch_max, plan_s_max = float(mx[7]), float(mx[8])
         tot_bytes = float(sm[2])
     else:
         kern_ms_max, tot_bytes, kern_o_max = kern_ms, float(local_bytes), kern_o
         cold_wall = run_cold.wall_el
+        xch_max, plan_s_max = xch_ms, getattr(op, "plan_s", 0.0)
     ms_step = el / args.steps * 1e3
     total_flops = 2.0 * nnz
 
@@ -364,7 +426,15 @@ def main() -> int:
             "algorithmic_bytes_per_launch": int(local_bytes),
             "algorithmic_bytes_all_ranks": int(tot_bytes),
             "host_gen_s": round(t_gen, 2),
+            "plan": {"build_s_max_over_ranks": round(plan_s_max, 3),
+                     "device_bytes_rank0": int(op.A.plan_bytes(algo)),
+                     "csr_device_bytes_rank0": int(12 * local_nnz + 4 * (op.A.info()[0] + 1))},
+            "exchange_ms_max_over_ranks": round(xch_max, 5),
+            "timing": ("cold steps: device time, HIP events on the launch stream from before the "
+                       "kernel to after exchange + merge, max over ranks; host wall clock beside"
+                       if args.cache == "cold" else "warm: host wall clock over K back-to-back steps"),
             "cache": args.cache,
+            "scrub": args.scrub,
             # cold steps are timed on the device (run_cold); the host wall
             # clock around each, barrier round trips included, for comparison
             "cold_host_wall_ms_per_step": round(cold_wall / args.steps * 1e3, 5),
@@ -380,6 +450,8 @@ def main() -> int:
             out["note"] = f"rehearsal: {world} ranks on {ndev} GPU(s) over {args.dist_backend}"
         if check is not None:
             out["check_vs_oracle"] = check
+        if rowsplit_beside is not None:
+            out["rowsplit_beside"] = rowsplit_beside
         if world == 1 and not args.no_cpu_baseline:
             rp_all = rowptr
             out["cpu_baseline"] = cpu_baseline(rp_all, col, val, x_h, plan.m, nnz, args.cpu_budget)

@@ -126,6 +126,9 @@ int sblas_csr_analyse(sblas_csr A, int algo, void *stream);
 /* y = alpha*A*x + beta*y on the handle's device; x, y DEVICE pointers. */
 int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x,
                double beta, double *d_y, void *stream);
+/* Device bytes held by the analysis of `algo` (free memory before - after
+ * sblas_csr_analyse; 0 if not analysed): the layout's cost beside the CSR. */
+long long sblas_csr_plan_bytes(sblas_csr A, int algo);
 /* bytes the algorithm must move per call (DESIGN.md "Algorithmic bytes"). */
 long long sblas_spmv_algorithmic_bytes(sblas_csr A, int beta_nonzero);
 

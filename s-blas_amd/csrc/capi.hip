@@ -187,14 +187,28 @@ int sblas_csr_analyse(sblas_csr A, int algo, void *stream)
     if (!A) return SBLAS_ERR_INVALID;
     DeviceGuard g(A->device);
     hipStream_t s = (hipStream_t)stream;
+    if (algo < SBLAS_SPMV_ROWSPLIT || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
+    // device bytes the plan holds: free memory before - after (the builders
+    // synchronise before returning)
+    size_t f0 = 0, f1 = 0, tot = 0;
+    (void)hipMemGetInfo(&f0, &tot);
+    int st = SBLAS_ERR_INVALID;
     switch (algo) {
-    case SBLAS_SPMV_ROWSPLIT: return build_rowsplit_plan(*A, s);
+    case SBLAS_SPMV_ROWSPLIT: st = build_rowsplit_plan(*A, s); break;
     case SBLAS_SPMV_CSR5:
-    case SBLAS_SPMV_CSR5_ALT: return build_csr5_plan(*A, s);
-    case SBLAS_SPMV_PANEL: return build_panel_plan(*A, s);
-    case SBLAS_SPMV_XSORT: return build_xsort_plan(*A, s);
-    default: return SBLAS_ERR_INVALID;
+    case SBLAS_SPMV_CSR5_ALT: st = build_csr5_plan(*A, s); break;
+    case SBLAS_SPMV_PANEL: st = build_panel_plan(*A, s); break;
+    case SBLAS_SPMV_XSORT: st = build_xsort_plan(*A, s); break;
     }
+    if (st == SBLAS_OK && A->plan_bytes[algo] == 0 && hipMemGetInfo(&f1, &tot) == hipSuccess && f0 > f1)
+        A->plan_bytes[algo] = (long long)(f0 - f1);
+    return st;
+}
+
+long long sblas_csr_plan_bytes(sblas_csr A, int algo)
+{
+    if (!A || algo < 0 || algo > SBLAS_SPMV_XSORT) return -1;
+    return A->plan_bytes[algo];
 }
 
 int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x, double beta, double *d_y,

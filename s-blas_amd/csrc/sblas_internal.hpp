@@ -218,6 +218,7 @@ struct sblas_csr_s {
     sblas::SpmmPlan mm;
     sblas::XsPlan xs;
     std::vector<int> h_rowptr;  // host copy (analysis)
+    long long plan_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device bytes per algorithm's plan
 };
 
 namespace sblas {

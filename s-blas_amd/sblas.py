@@ -78,6 +78,7 @@ _sig("sblas_csr_info", _i, _p, _p, _p, _p)
 _sig("sblas_csr_analyse", _i, _p, _i, _p)
 _sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
 _sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
+_sig("sblas_csr_plan_bytes", _ll, _p, _i)
 _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
 _sig("sblas_csr_transpose", _i, _p, _p, _p, _p, _p)
 _sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
@@ -392,6 +393,10 @@ class DeviceCSR:
     def transpose(self, colptr_ptr: int, rowidx_ptr: int, cval_ptr: int, stream=None) -> None:
         check(lib.sblas_csr_transpose(self.h, colptr_ptr, rowidx_ptr, cval_ptr, stream),
               "csr_transpose")
+
+    def plan_bytes(self, algo: int) -> int:
+        """Device bytes the algorithm's analysis holds beside the CSR."""
+        return int(lib.sblas_csr_plan_bytes(self.h, algo))
 
     def algorithmic_bytes(self, beta_nonzero: bool) -> int:
         return int(lib.sblas_spmv_algorithmic_bytes(self.h, int(beta_nonzero)))

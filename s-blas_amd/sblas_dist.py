@@ -16,6 +16,7 @@ libsblas's.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -79,7 +80,9 @@ class DistSpMV:
                                                      col_base, val_base, r0, r1, i0, i1, None),
                     "csr_upload_slice")
         self.A = sblas.DeviceCSR(h.value)
+        t0 = time.perf_counter()
         self.A.analyse(algo)
+        self.plan_s = time.perf_counter() - t0
         self.dm = r1 - r0
         stride = plan.stride
         f64 = torch.float64
@@ -213,7 +216,9 @@ class DistSpMVCyclic:
         self.A = sblas.DeviceCSR.upload(device, plan.n, np.ascontiguousarray(local_rowptr, np.int64),
                                         np.ascontiguousarray(col, np.int32),
                                         np.ascontiguousarray(val, np.float64))
+        t0 = time.perf_counter()
         self.A.analyse(algo)
+        self.plan_s = time.perf_counter() - t0
         f64 = torch.float64
         self.y_local = torch.zeros(plan.stride, dtype=f64, device=dev)
         self.y_full = torch.zeros(plan.m, dtype=f64, device=dev)
