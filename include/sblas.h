@@ -123,7 +123,15 @@ int sblas_csr_destroy(sblas_csr A);
 int sblas_csr_info(sblas_csr A, int *m, int *n, long long *nnz);
 /* Build the analysis for an algorithm (row blocks / CSR5 tiles); run once. */
 int sblas_csr_analyse(sblas_csr A, int algo, void *stream);
-/* y = alpha*A*x + beta*y on the handle's device; x, y DEVICE pointers. */
+/* y = alpha*A*x + beta*y on the handle's device; x, y DEVICE pointers.
+ * Concurrency: the analysis keeps per-launch scratch on the device (XSORT:
+ * work-queue claim heads that each launch re-arms for the next one, and the
+ * wide-range partial sums; PANEL: the panel partials; ROWSPLIT: long-row
+ * partials; CSR5: tile carries).  A handle therefore allows ONE launch in
+ * flight at a time: issue its launches on one stream (they are then
+ * ordered), or synchronise between launches on different streams.  Two
+ * overlapping launches of one handle give wrong y in both.  Distinct handles
+ * (even of the same matrix) are independent. */
 int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x,
                double beta, double *d_y, void *stream);
 /* Device bytes held by the analysis of `algo` (free memory before - after
@@ -150,7 +158,9 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz,
                       const int *d_colptr, const int *d_rowidx,
                       const double *d_val, int substitution, void *stream);
 /* algo 0 = sync-free CSC push (reference algorithm), 1 = CSR pull with ready
- * flags (deterministic sums). */
+ * flags (deterministic sums), 2 = level-set (rows grouped by level,
+ * findlevel.h:71-147; one synchronisation per level; built on the first
+ * algo-2 solve; x bit-identical to algo 1). */
 int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x,
                      void *stream);
 int sblas_trsv_levels(sblas_trsv T, int *nlevel);

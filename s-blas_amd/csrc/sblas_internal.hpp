@@ -116,6 +116,17 @@ struct SpmmPlan {
     unsigned short *l2_col = nullptr;    // column - s*W
     double *l2_val = nullptr;
     double *l2_part = nullptr;           // [8][m][64]
+    // Column-sorted C-tile form (default where the L2-slice form applies):
+    // columns of A cut into slabs of 2^ct_wlog columns, slab s owned by XCD
+    // s % 8 and its slabs split into ct_ns contiguous sets; rows into ct_nrb
+    // blocks of ct_R.  Entries of (XCD, set, row block) sorted by (column,
+    // row) with packed keys (XCD-local column << ct_rbits | local row).  A
+    // workgroup accumulates one (row block x 16 C columns) tile in LDS and
+    // writes it to its (XCD, set) partial; a reduce adds the partials.
+    int ct_ns = 0, ct_nrb = 0, ct_R = 0, ct_rbits = 0, ct_wlog = 0;
+    unsigned *ct_key = nullptr;
+    double *ct_val = nullptr;
+    long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets
     double fill_thresh = 0.25;
     bool ready = false;
 };

@@ -329,6 +329,171 @@ static int build_l2slice(sblas_csr_s &A, const std::vector<int> &rp, const std::
     return SBLAS_OK;
 }
 
+// ---- column-sorted C-tile SpMM (few rows, tall B) -------------------------
+// The row forms move one B row (n*8 B) from L2 to the CU per NONZERO: 5.8 GB
+// per call on rail4284, at the L2/Infinity-Cache gather rate.  Here a
+// workgroup owns a tile of C -- R rows x 16 columns, accumulated in LDS --
+// and walks its entries sorted by column: the nonzeros of one column inside
+// the tile's rows sit next to each other, so their 128-B B segment is
+// fetched once (same address in one instruction, or an L1 hit in the next)
+// and applied to all of them.  A's entries are read once per 16 C columns
+// instead.  Per nonzero: 12 B of A per column group + one 128-B segment per
+// (column, tile) instead of n*8 B; the products land in LDS with ds_add_f64.
+// XCD k owns the column slabs s % 8 == k (its B rows stay in its L2); its
+// slabs are split into ns sets, and each (set, row block, column group) is
+// one workgroup writing an alpha-free partial, added in slot order after.
+constexpr int kCtCols = 16;      // C columns per tile (one 128-B B segment)
+constexpr int kCtPad = 17;       // LDS row stride in doubles (bank spread)
+constexpr int kCtThreads = 1024;
+constexpr int kCtU = 8;          // 4-entry steps in flight per wave
+constexpr int kCtMaxRows = 163840 / (kCtPad * 8);  // 1204: one tile per CU
+
+__global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
+    const unsigned *__restrict__ key, const double *__restrict__ val,
+    const long long *__restrict__ off, int ns, int nrb, int R, int rbits, int wlog, int ncg,
+    const double *__restrict__ B, long long ldb, int n, int m, double *__restrict__ part)
+{
+    extern __shared__ double tile[];  // [R][kCtPad]
+    const int x = (int)(blockIdx.x & 7);
+    int rest = (int)(blockIdx.x >> 3);
+    const int cg = rest % ncg;
+    rest /= ncg;
+    const int rb = rest % nrb, ss = rest / nrb;
+    const int slot = x * ns + ss;
+    const int r0 = rb * R, nr = min(R, m - r0);
+    for (int i = threadIdx.x; i < nr * kCtPad; i += kCtThreads) tile[i] = 0.0;
+    __syncthreads();
+    const long long e0 = off[(long long)slot * nrb + rb], e1 = off[(long long)slot * nrb + rb + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sub = lane >> 4, cl = lane & 15;
+    const int col = cg * kCtCols + cl;
+    const bool live_c = col < n;
+    const int cc = live_c ? col : 0;
+    const unsigned rmask = (1u << rbits) - 1;
+    const unsigned wmask = (1u << wlog) - 1;
+    // XCD-local column jc -> global column: slab (jc >> wlog) * 8 + x
+    auto gcol = [&](unsigned jc) -> long long {
+        return ((long long)(jc >> wlog) << (wlog + 3)) | ((long long)x << wlog) | (jc & wmask);
+    };
+    constexpr long long kStride = (long long)(kCtThreads / 64) * 4 * kCtU;
+    for (long long it = e0 + (long long)wv * 4 * kCtU; it < e1; it += kStride) {
+        unsigned k[kCtU];
+        double v[kCtU], b[kCtU];
+#pragma unroll
+        for (int u = 0; u < kCtU; ++u) {
+            const long long e = it + 4 * u + sub;
+            const long long ec = e < e1 ? e : e1 - 1;
+            k[u] = key[ec];
+            v[u] = e < e1 ? val[ec] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kCtU; ++u) b[u] = B[gcol(k[u] >> rbits) * ldb + cc];
+#pragma unroll
+        for (int u = 0; u < kCtU; ++u) {
+            const long long e = it + 4 * u + sub;
+            if (live_c && e < e1) atomicAdd(&tile[(k[u] & rmask) * kCtPad + cl], v[u] * b[u]);
+        }
+    }
+    __syncthreads();
+    // partial [slot][column][row] (column-major like C): coalesced over rows
+    const int ncol = min(kCtCols, n - cg * kCtCols);
+    double *out = part + ((long long)slot * n + cg * kCtCols) * m + r0;
+    for (int i = threadIdx.x; i < nr * ncol; i += kCtThreads) {
+        const int c = i / nr, r = i - c * nr;
+        out[(long long)c * m + r] = tile[r * kCtPad + c];
+    }
+}
+
+// C = alpha * sum_slot part[slot] (+ beta * C), slots in order
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmm_ctreduce(const double *__restrict__ part, int nslot, int m, int n,
+                                                       double alpha, double beta, double *__restrict__ C,
+                                                       long long ldc)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)m * n) return;
+    const int c = (int)(i / m), r = (int)(i - (long long)c * m);
+    double s = 0.0;
+    for (int q = 0; q < nslot; ++q) s += part[((long long)q * n + c) * m + r];
+    double *o = C + (long long)c * ldc + r;
+    *o = kBeta ? alpha * s + beta * *o : alpha * s;
+}
+
+// host: the C-tile layout.  Returns SBLAS_ERR_UNSUPPORTED (caller keeps the
+// other forms) when the packed key cannot hold XCD-local column and row.
+static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
+                       const std::vector<double> &hval)
+{
+    SpmmPlan &P = A.mm;
+    const int m = A.m, k = A.n;
+    int wlog = 11;  // 2048 B rows = 1 MiB of B per slab at n = 64
+    if (const char *e = getenv("SBLAS_SPMM_CTW")) wlog = std::max(4, std::min(20, atoi(e)));
+    const int nrb = (m + kCtMaxRows - 1) / kCtMaxRows;
+    const int R = (m + nrb - 1) / nrb;
+    int rbits = 1;
+    while ((1 << rbits) < R) ++rbits;
+    const long long nslab = ((long long)k + (1LL << wlog) - 1) >> wlog;
+    const long long jc_max = ((nslab + 7) / 8) << wlog;  // XCD-local columns
+    if (rbits + 1 > 32 || jc_max > (1LL << (32 - rbits))) return SBLAS_ERR_UNSUPPORTED;
+    // slab sets per XCD: about one workgroup per CU at n = 64 (4 column groups)
+    int ns = std::max(1, 32 / (nrb * 4));
+    if (const char *e = getenv("SBLAS_SPMM_CTNS")) ns = std::max(1, atoi(e));
+    // per-slab entry counts -> contiguous sets of about equal entries per XCD
+    std::vector<long long> scount((size_t)nslab, 0);
+    for (long long e = 0; e < A.nnz; ++e) scount[(size_t)(hcol[(size_t)e] >> wlog)]++;
+    std::vector<int> set_of((size_t)nslab, 0);
+    for (int x = 0; x < 8; ++x) {
+        long long tot = 0;
+        for (long long s = x; s < nslab; s += 8) tot += scount[(size_t)s];
+        long long run = 0;
+        for (long long s = x; s < nslab; s += 8) {
+            set_of[(size_t)s] = tot ? (int)std::min<long long>(ns - 1, run * ns / tot) : 0;
+            run += scount[(size_t)s];
+        }
+    }
+    const int nbk = 8 * ns * nrb;  // buckets (XCD, set, row block)
+    auto bucket = [&](int row, int c) {
+        const int s = c >> wlog;
+        return ((s & 7) * ns + set_of[(size_t)s]) * nrb + row / R;
+    };
+    std::vector<long long> off((size_t)nbk + 1, 0);
+    for (int r = 0; r < m; ++r)
+        for (int e = rp[r]; e < rp[r + 1]; ++e) off[(size_t)bucket(r, hcol[e]) + 1]++;
+    for (int b = 0; b < nbk; ++b) off[(size_t)b + 1] += off[(size_t)b];
+    std::vector<unsigned long long> kv((size_t)std::max<long long>(A.nnz, 1));  // key << 32 | entry index
+    {
+        std::vector<long long> next(off.begin(), off.end() - 1);
+        for (int r = 0; r < m; ++r)
+            for (int e = rp[r]; e < rp[r + 1]; ++e) {
+                const int c = hcol[e];
+                const unsigned jc = (unsigned)((((long long)(c >> wlog) >> 3) << wlog) | (c & ((1 << wlog) - 1)));
+                const unsigned kk = (jc << rbits) | (unsigned)(r % R);
+                kv[(size_t)next[(size_t)bucket(r, c)]++] = ((unsigned long long)kk << 32) | (unsigned)e;
+            }
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int b = 0; b < nbk; ++b) std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
+    std::vector<unsigned> hkey((size_t)std::max<long long>(A.nnz, 1));
+    std::vector<double> hv((size_t)std::max<long long>(A.nnz, 1));
+#pragma omp parallel for schedule(static)
+    for (long long e = 0; e < A.nnz; ++e) {
+        hkey[(size_t)e] = (unsigned)(kv[(size_t)e] >> 32);
+        hv[(size_t)e] = hval[(size_t)(kv[(size_t)e] & 0xffffffffu)];
+    }
+    SBLAS_HIP(hipMalloc(&P.ct_key, sizeof(unsigned) * hkey.size()));
+    SBLAS_HIP(hipMalloc(&P.ct_val, sizeof(double) * hv.size()));
+    SBLAS_HIP(hipMalloc(&P.ct_off, sizeof(long long) * off.size()));
+    SBLAS_HIP(hipMemcpy(P.ct_key, hkey.data(), sizeof(unsigned) * hkey.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(P.ct_val, hv.data(), sizeof(double) * hv.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(P.ct_off, off.data(), sizeof(long long) * off.size(), hipMemcpyHostToDevice));
+    P.ct_ns = ns;
+    P.ct_nrb = nrb;
+    P.ct_R = R;
+    P.ct_rbits = rbits;
+    P.ct_wlog = wlog;
+    return SBLAS_OK;
+}
+
 int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.mm.ready) return SBLAS_OK;
@@ -395,6 +560,15 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     if (const char *e = getenv("SBLAS_SPMM_L2SLICE")) l2 = atoi(e) != 0 && P.nmfma == 0 && m > 0 && rw <= kL2MaxRows;
     int W = 8192;
     if (const char *e = getenv("SBLAS_SPMM_L2W")) W = std::max(1, std::min(65536, atoi(e)));
+    // the C-tile form replaces the L2-slice form where that one applies
+    // (SBLAS_SPMM_CTILE=0 keeps the L2-slice form, =1 forces C tiles)
+    bool ct = l2;
+    if (const char *e = getenv("SBLAS_SPMM_CTILE")) ct = atoi(e) != 0 && P.nmfma == 0 && m > 0;
+    if (ct) {
+        const int rc = build_ctile(A, rp, hcol, hval);
+        if (rc == SBLAS_OK) l2 = false;
+        else if (rc != SBLAS_ERR_UNSUPPORTED) return rc;
+    }
     if (l2) SBLAS_TRY(build_l2slice(A, rp, hcol, hval, W));
     (void)s;
     P.ready = true;
@@ -413,6 +587,9 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.l2_col);
     (void)hipFree(P.l2_val);
     (void)hipFree(P.l2_part);
+    (void)hipFree(P.ct_key);
+    (void)hipFree(P.ct_val);
+    (void)hipFree(P.ct_off);
     A.mm = SpmmPlan{};
 }
 
@@ -439,6 +616,7 @@ struct SpmmScratch {
     size_t bytes = 0;
 };
 static thread_local SpmmScratch g_scratch[64];
+static thread_local SpmmScratch g_ctpart[64];  // C-tile partials per device
 
 int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int ldb,
                 int b_layout, double beta, double *C, int ldc, hipStream_t s)
@@ -465,6 +643,39 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     }
     const SpmmPlan &P = A.mm;
     const int nslab = (n + 63) / 64;
+    if (P.ready && P.ct_nrb > 0) {
+        const int ncg = (n + kCtCols - 1) / kCtCols;
+        const int nslot = 8 * P.ct_ns;
+        SpmmScratch &S = g_ctpart[A.device & 63];
+        const size_t need = sizeof(double) * (size_t)nslot * (size_t)n * (size_t)A.m;
+        if (S.bytes < need) {
+            (void)hipFree(S.bt);
+            S.bt = nullptr;
+            S.bytes = 0;
+            SBLAS_HIP(hipMalloc(&S.bt, need));
+            S.bytes = need;
+        }
+        const long long nwg = 8LL * P.ct_ns * P.ct_nrb * ncg;
+        const size_t lds = sizeof(double) * (size_t)P.ct_R * kCtPad;
+        static thread_local bool attr_set[64] = {};
+        if (!attr_set[A.device & 63]) {  // > 64 KiB of dynamic LDS
+            SBLAS_HIP(hipFuncSetAttribute((const void *)k_spmm_ctile, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)(sizeof(double) * kCtMaxRows * kCtPad)));
+            attr_set[A.device & 63] = true;
+        }
+        hipLaunchKernelGGL(k_spmm_ctile, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val,
+                           P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr, n,
+                           A.m, S.bt);
+        const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,
+                               beta, C, (long long)ldc);
+        else
+            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,
+                               beta, C, (long long)ldc);
+        SBLAS_HIP(hipGetLastError());
+        return SBLAS_OK;
+    }
     if (P.ready && P.l2_S > 0) {
         const int rw = (A.m + kL2WgPerXcd * 4 - 1) / (kL2WgPerXcd * 4);
         for (int sl = 0; sl < nslab; ++sl) {

@@ -48,6 +48,15 @@ struct sblas_trsv_s {
     double *left = nullptr;    // push: left sums
     unsigned *ctl = nullptr;   // [0] ticket, [kAbort] timeout flag (kCtlBytes block)
     int nlevels = -1;
+    // level-set executor (algo 2), built on its first solve: rows in level
+    // order (stable by row), the CSR rows copied into that order, level
+    // pointers, and the launch schedule (runs of narrow levels -> one
+    // workgroup with barriers; each wide level -> one grid launch)
+    int *lrow = nullptr, *lrp = nullptr, *lcol = nullptr;
+    double *lval = nullptr;
+    int *lptr_d = nullptr;
+    std::vector<int> lptr;                  // host copy [nlevels + 1]
+    std::vector<std::pair<int, int>> lsched;  // (first level, end level); end < 0: wide level
 };
 
 namespace sblas {
@@ -490,6 +499,52 @@ static void launch_trsm(const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t 
     }
 }
 
+// ---- level-set executor (algo 2; findlevel.h:71-147's level sets) --------
+// Rows are solved level by level: every row of level l depends only on rows
+// of levels < l, so no ready flags are needed -- a level boundary is a kernel
+// boundary (wide levels) or a workgroup barrier (a run of narrow levels in
+// one workgroup).  Sums in CSR column order, as the pull executor: the two
+// give bit-identical x.  The comparison baseline for the sync-free
+// executors: one synchronisation per level, whatever the dependencies.
+__device__ __forceinline__ void level_row(const int *__restrict__ lrp, const int *__restrict__ lcol,
+                                          const double *__restrict__ lval, const int *__restrict__ lrow,
+                                          int k, int backward, const double *__restrict__ b, double *x)
+{
+    const int i = lrow[k];
+    const int a = lrp[k], e = lrp[k + 1];
+    const double diag = backward ? lval[a] : lval[e - 1];
+    const int j0 = backward ? a + 1 : a, j1 = backward ? e : e - 1;
+    double sum = 0.0;
+    for (int j = j0; j < j1; ++j) sum += lval[j] * ld_sc1_f64(x + lcol[j]);
+    __hip_atomic_store(x + i, (b[i] - sum) / diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_trsv_level(const int *__restrict__ lrp, const int *__restrict__ lcol,
+                                                    const double *__restrict__ lval, const int *__restrict__ lrow,
+                                                    int p0, int p1, int backward, const double *__restrict__ b,
+                                                    double *x)
+{
+    const int k = p0 + (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k < p1) level_row(lrp, lcol, lval, lrow, k, backward, b, x);
+}
+
+constexpr int kLevelWG = 1024;         // threads of the narrow-run workgroup
+constexpr int kLevelNarrow = 2 * kLevelWG;  // a level with <= this many rows is narrow
+
+__global__ __launch_bounds__(kLevelWG) void k_trsv_level_run(
+    const int *__restrict__ lrp, const int *__restrict__ lcol, const double *__restrict__ lval,
+    const int *__restrict__ lrow, const int *__restrict__ lptr, int l0, int l1, int backward,
+    const double *__restrict__ b, double *x)
+{
+    for (int l = l0; l < l1; ++l) {
+        for (int k = lptr[l] + (int)threadIdx.x; k < lptr[l + 1]; k += kLevelWG)
+            level_row(lrp, lcol, lval, lrow, k, backward, b, x);
+        // this level's x stores (agent scope) complete before any wave reads them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
 static int grid_for(int dev)
 {
     hipDeviceProp_t p;
@@ -567,12 +622,109 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz, const int *d_
     return SBLAS_OK;
 }
 
+// level sets of the solve (rows of level l depend only on levels < l), as
+// findlevel.h:71-147 computes them: level(i) = 1 + max level of i's
+// dependencies, walking columns in solve order
+static void host_levels(const sblas_trsv_s *T, const std::vector<int> &cp, const std::vector<int> &ri,
+                        std::vector<int> &lev, int &nl)
+{
+    lev.assign((size_t)T->n, 0);
+    nl = 0;
+    for (int k = 0; k < T->n; ++k) {
+        const int i = T->substitution ? T->n - 1 - k : k;
+        const int li = lev[(size_t)i];
+        nl = std::max(nl, li + 1);
+        for (int j = cp[(size_t)i]; j < cp[(size_t)i + 1]; ++j)
+            if (ri[(size_t)j] != i) lev[(size_t)ri[(size_t)j]] = std::max(lev[(size_t)ri[(size_t)j]], li + 1);
+    }
+}
+
+static int build_levelset(sblas_trsv_s *T, hipStream_t s)
+{
+    if (T->lrow) return SBLAS_OK;
+    const int n = T->n, nnz = T->nnz;
+    std::vector<int> cp((size_t)n + 1), ri((size_t)nnz);
+    SBLAS_HIP(hipStreamSynchronize(s));
+    SBLAS_HIP(hipMemcpy(cp.data(), T->colptr, sizeof(int) * cp.size(), hipMemcpyDeviceToHost));
+    if (nnz) SBLAS_HIP(hipMemcpy(ri.data(), T->rowidx, sizeof(int) * ri.size(), hipMemcpyDeviceToHost));
+    std::vector<int> lev;
+    int nl = 0;
+    host_levels(T, cp, ri, lev, nl);
+    T->nlevels = nl;
+    // counting sort of the rows by level (stable: ascending row in a level)
+    T->lptr.assign((size_t)nl + 1, 0);
+    for (int i = 0; i < n; ++i) T->lptr[(size_t)lev[(size_t)i] + 1]++;
+    for (int l = 0; l < nl; ++l) T->lptr[(size_t)l + 1] += T->lptr[(size_t)l];
+    std::vector<int> lrow((size_t)std::max(n, 1)), next(T->lptr.begin(), T->lptr.end() - 1);
+    for (int i = 0; i < n; ++i) lrow[(size_t)next[(size_t)lev[(size_t)i]]++] = i;
+    // CSR rows (the pull executor's device CSR) copied into level order
+    std::vector<int> rrp((size_t)n + 1), rc((size_t)std::max(nnz, 1));
+    std::vector<double> rv((size_t)std::max(nnz, 1));
+    SBLAS_HIP(hipMemcpy(rrp.data(), T->rrowptr, sizeof(int) * rrp.size(), hipMemcpyDeviceToHost));
+    if (nnz) {
+        SBLAS_HIP(hipMemcpy(rc.data(), T->rcol, sizeof(int) * nnz, hipMemcpyDeviceToHost));
+        SBLAS_HIP(hipMemcpy(rv.data(), T->rval, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+    }
+    std::vector<int> lrp((size_t)n + 1, 0), lc((size_t)std::max(nnz, 1));
+    std::vector<double> lv((size_t)std::max(nnz, 1));
+    for (int k = 0; k < n; ++k) {
+        const int i = lrow[(size_t)k];
+        const int len = rrp[(size_t)i + 1] - rrp[(size_t)i];
+        std::copy(rc.begin() + rrp[(size_t)i], rc.begin() + rrp[(size_t)i + 1], lc.begin() + lrp[(size_t)k]);
+        std::copy(rv.begin() + rrp[(size_t)i], rv.begin() + rrp[(size_t)i + 1], lv.begin() + lrp[(size_t)k]);
+        lrp[(size_t)k + 1] = lrp[(size_t)k] + len;
+    }
+    // schedule: maximal runs of narrow levels, single wide levels
+    T->lsched.clear();
+    for (int l = 0; l < nl;) {
+        if (T->lptr[(size_t)l + 1] - T->lptr[(size_t)l] > kLevelNarrow) {
+            T->lsched.push_back({l, -1});
+            ++l;
+            continue;
+        }
+        int e = l;
+        while (e < nl && T->lptr[(size_t)e + 1] - T->lptr[(size_t)e] <= kLevelNarrow) ++e;
+        T->lsched.push_back({l, e});
+        l = e;
+    }
+    SBLAS_HIP(hipMalloc(&T->lrow, sizeof(int) * lrow.size()));
+    SBLAS_HIP(hipMalloc(&T->lrp, sizeof(int) * lrp.size()));
+    SBLAS_HIP(hipMalloc(&T->lcol, sizeof(int) * lc.size()));
+    SBLAS_HIP(hipMalloc(&T->lval, sizeof(double) * lv.size()));
+    SBLAS_HIP(hipMalloc(&T->lptr_d, sizeof(int) * T->lptr.size()));
+    SBLAS_HIP(hipMemcpy(T->lrow, lrow.data(), sizeof(int) * lrow.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(T->lrp, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(T->lcol, lc.data(), sizeof(int) * lc.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(T->lval, lv.data(), sizeof(double) * lv.size(), hipMemcpyHostToDevice));
+    SBLAS_HIP(hipMemcpy(T->lptr_d, T->lptr.data(), sizeof(int) * T->lptr.size(), hipMemcpyHostToDevice));
+    return SBLAS_OK;
+}
+
+static int solve_levelset(sblas_trsv_s *T, const double *b, double *x, hipStream_t s)
+{
+    SBLAS_TRY(build_levelset(T, s));
+    for (const auto &seg : T->lsched) {
+        if (seg.second < 0) {
+            const int p0 = T->lptr[(size_t)seg.first], p1 = T->lptr[(size_t)seg.first + 1];
+            hipLaunchKernelGGL(k_trsv_level, dim3((unsigned)((p1 - p0 + 255) / 256)), dim3(256), 0, s, T->lrp,
+                               T->lcol, T->lval, T->lrow, p0, p1, T->substitution, b, x);
+        } else {
+            hipLaunchKernelGGL(k_trsv_level_run, dim3(1), dim3(kLevelWG), 0, s, T->lrp, T->lcol, T->lval, T->lrow,
+                               T->lptr_d, seg.first, seg.second, T->substitution, b, x);
+        }
+    }
+    SBLAS_HIP(hipGetLastError());
+    SBLAS_HIP(hipStreamSynchronize(s));
+    return SBLAS_OK;
+}
+
 int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, void *stream)
 {
-    if (!T || !d_b || !d_x || (algo != 0 && algo != 1)) return SBLAS_ERR_INVALID;
+    if (!T || !d_b || !d_x || algo < 0 || algo > 2) return SBLAS_ERR_INVALID;
     if (T->n == 0) return SBLAS_OK;
     DeviceGuard g(T->device);
     hipStream_t s = (hipStream_t)stream;
+    if (algo == 2) return solve_levelset(T, d_b, d_x, s);
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     const int grid = grid_for(T->device);
     if (algo == 0) {
@@ -627,15 +779,9 @@ int sblas_trsv_levels(sblas_trsv T, int *nlevel)
         std::vector<int> cp((size_t)T->n + 1), ri((size_t)T->nnz);
         SBLAS_HIP(hipMemcpy(cp.data(), T->colptr, sizeof(int) * cp.size(), hipMemcpyDeviceToHost));
         if (T->nnz) SBLAS_HIP(hipMemcpy(ri.data(), T->rowidx, sizeof(int) * ri.size(), hipMemcpyDeviceToHost));
-        std::vector<int> lev((size_t)T->n, 0);
+        std::vector<int> lev;
         int nl = 0;
-        for (int k = 0; k < T->n; ++k) {
-            const int i = T->substitution ? T->n - 1 - k : k;
-            const int li = lev[(size_t)i];
-            nl = std::max(nl, li + 1);
-            for (int j = cp[(size_t)i]; j < cp[(size_t)i + 1]; ++j)
-                if (ri[(size_t)j] != i) lev[(size_t)ri[(size_t)j]] = std::max(lev[(size_t)ri[(size_t)j]], li + 1);
-        }
+        host_levels(T, cp, ri, lev, nl);
         T->nlevels = nl;
     }
     *nlevel = T->nlevels;
@@ -657,6 +803,11 @@ int sblas_trsv_destroy(sblas_trsv T)
         (void)hipFree(T->done);
         (void)hipFree(T->left);
         (void)hipFree(T->ctl);
+        (void)hipFree(T->lrow);
+        (void)hipFree(T->lrp);
+        (void)hipFree(T->lcol);
+        (void)hipFree(T->lval);
+        (void)hipFree(T->lptr_d);
     }
     delete T;
     return SBLAS_OK;

@@ -701,9 +701,19 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // second round for a few items would double the kernel's tail)
     double cap = narrow_cost((double)nnz) / (double)slots;
     if (const char *e = getenv("SBLAS_XS_WSTAR")) cap = std::max(1.0, atof(e));
-    for (int it = 0; it < 400; ++it) {
+    // Ranges hold at most rows_cap rows, so once ceil(m / rows_cap) exceeds
+    // the slots no cap can fit them: stop there (and after 50 growth steps
+    // without fewer sub-items) instead of 400 O(m) passes.  Leftover
+    // sub-items are still correct: the grid claims them in a second round.
+    const long long min_ranges = ((long long)m + rows_cap - 1) / rows_cap;
+    long long best_subs = -1;
+    for (int it = 0, flat = 0; it < 400; ++it) {
         build_ranges(cap);
-        if (count_subs() <= slots || getenv("SBLAS_XS_WSTAR")) break;
+        const long long subs = count_subs();
+        if (subs <= slots || getenv("SBLAS_XS_WSTAR") || min_ranges > slots) break;
+        flat = (best_subs >= 0 && subs >= best_subs) ? flat + 1 : 0;
+        if (flat >= 50) break;
+        if (best_subs < 0 || subs < best_subs) best_subs = subs;
         cap *= 1.02;
     }
     const int I = (int)ranges.size();

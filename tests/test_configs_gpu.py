@@ -118,12 +118,15 @@ def cfg4(orc):
                 want=want, bound=bound)
 
 
-@pytest.mark.parametrize("layout", ["row", "col"])
-def test_config4_spmm_full_size(torch_cuda, sb, cfg4, layout):
+@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "l2slice")])
+def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form):
     """BASELINE configs[3]: C = -0.7 A B + 0.8 C on the rail4284-shaped matrix,
     all 4284 x 64 entries of C checked (B row-major as resident in HBM, and
-    the reference's column-major host layout)."""
+    the reference's column-major host layout), with the default column-sorted
+    C-tile form and the L2-slice form it replaced."""
     torch = torch_cuda
+    if form == "l2slice":
+        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     c = cfg4
     m, k, n = c["m"], c["k"], c["n"]
     A = sb.DeviceCSR.upload(0, k, c["rp"], c["col"], c["val"])
@@ -165,7 +168,7 @@ def test_config5_kat_serial_oracle(orc, cfg5):
     assert orc.levels_lower(c["cp"], c["ri"]) > 100
 
 
-@pytest.mark.parametrize("algo", [1, 0], ids=["pull", "push"])
+@pytest.mark.parametrize("algo", [1, 0, 2], ids=["pull", "push", "levelset"])
 def test_config5_single_device_exact(torch_cuda, sb, cfg5, algo):
     torch = torch_cuda
     c = cfg5

@@ -33,22 +33,31 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w"])
+@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     """Both row kernels: wave per row and workgroup per row (split over its
-    nonzeros; picked automatically for long rows) and the L2-slice form
-    (forced: "l2" = 3 slices of 2048 columns, "l2w" = 79 slices of 64)."""
+    nonzeros; picked automatically for long rows), the L2-slice form
+    (forced: "l2" = 3 slices of 2048 columns, "l2w" = 79 slices of 64) and
+    the column-sorted C-tile form (forced: "ct" = 3 slabs of 2048 columns,
+    one slab set; "ctw" = 313 slabs of 16 columns in 3 sets per XCD;
+    "ctrows" = 2,500 rows, i.e. 3 row blocks of 834)."""
     torch = torch_cuda
     if splitk in ("0", "1"):
         monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
     if splitk.startswith("l2"):
         monkeypatch.setenv("SBLAS_SPMM_L2SLICE", "1")
+        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
         if splitk == "l2w":
             monkeypatch.setenv("SBLAS_SPMM_L2W", "64")
+    if splitk.startswith("ct"):
+        monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
+        if splitk == "ctw":
+            monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
+            monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
     rng = np.random.default_rng(ncols + 10 * layout)
-    m, k = 700, 5000
+    m, k = (2500 if splitk == "ctrows" else 700), 5000
     rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
     B = rng.standard_normal((k, ncols))
     C0 = rng.standard_normal((m, ncols))
@@ -163,7 +172,7 @@ def test_sptrans_reference_api(torch_cuda, sb, orc, capfd):
 # -------------------------------------------------------------- SpTRSV ----
 @pytest.mark.parametrize("name", ["qh768", "ash85"])
 @pytest.mark.parametrize("sub", ["fwd", "bwd"])
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 2])
 def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     torch = torch_cuda
     g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
@@ -183,7 +192,7 @@ def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     T.close()
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 2])
 def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     """Random lower-triangular with long chains and a long column/row."""
     torch = torch_cuda
@@ -211,6 +220,55 @@ def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     x = xd.cpu().numpy()
     rel = np.abs(x - want).sum() / np.abs(want).sum()
     assert rel <= 1e-12, rel
+    if algo == 2:  # level-set sums in the pull executor's order: bit-identical
+        xp = torch.zeros(n, dtype=torch.float64, device="cuda")
+        T.solve(1, d[3].data_ptr(), xp.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xp.cpu().numpy(), x)
+    T.close()
+
+
+@pytest.mark.parametrize("sub", [0, 1])
+@pytest.mark.parametrize("shape", ["chain", "wide"])
+def test_sptrsv_levelset_schedule(torch_cuda, sb, orc, sub, shape):
+    """Level-set executor over both schedule kinds: "chain" = a bidiagonal
+    system (n levels of one row: one narrow run in one workgroup), "wide" = a
+    diagonal-heavy system with a few long dependency columns (levels of more
+    than 2,048 rows: one grid launch per level), forward and backward; exact
+    integer KATs (x integer, values small integers)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(17 + sub)
+    n = 5000 if shape == "chain" else 60000
+    cols, rows = [], []
+    for c in range(n):
+        deps = []
+        if shape == "chain":
+            if (sub == 0 and c + 1 < n) or (sub == 1 and c > 0):
+                deps = [c + 1 if sub == 0 else c - 1]
+        else:
+            lo, hi = (c + 1, min(n, c + 4000)) if sub == 0 else (max(0, c - 4000), c)
+            if hi > lo and rng.random() < 0.3:
+                deps = sorted(set(rng.integers(lo, hi, 2).tolist()))
+        rr = [c] + deps if sub == 0 else deps + [c]
+        rows.append(rr)
+    cp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ri = np.concatenate(rows).astype(np.int32)
+    cv = rng.integers(1, 4, len(ri)).astype(np.float64)
+    diag_pos = cp[:-1] if sub == 0 else cp[1:] - 1
+    cv[diag_pos] = 1.0
+    xref = rng.integers(-3, 4, n).astype(np.float64)
+    colidx = np.repeat(np.arange(n), np.diff(cp))
+    b = np.bincount(ri, weights=cv * xref[colidx], minlength=n)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
+    T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sub)
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    for _ in range(2):  # second solve reuses the level schedule
+        xd.zero_()
+        T.solve(2, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xd.cpu().numpy(), xref)
+    if shape == "chain":
+        assert T.levels() == n
     T.close()
 
 
