@@ -81,6 +81,14 @@ int sblas_csrmm_mgpu(int m, int n, int k, const double *alpha, int nnz_A,
                      const double *beta, double *B_dense, double *C_dense,
                      int ngpu);
 
+/* Same operation with the reference's own partition (dspmm_mgpu_baseline.cu
+ * :147-150): A replicated, B and C split by columns, device d owning columns
+ * [floor(d*n/ngpu), floor((d+1)*n/ngpu)).  Comparison mode; no exchange. */
+int sblas_csrmm_mgpu_colsplit(int m, int n, int k, const double *alpha, int nnz_A,
+                              int *csrRowPtr_A, int *csrColIndex_A, double *csrVal_A,
+                              const double *beta, double *B_dense, double *C_dense,
+                              int ngpu);
+
 /* Sync-free triangular solve, CSC input, x output; validates against x_ref
  * when x_ref != NULL (rel-L1, prints like the reference) and reports gflops.
  * substitution 0 forward (lower), 1 backward (upper). rhs must be 1. */

@@ -264,6 +264,48 @@ int sblas_csrmm_mgpu(int m, int n, int k, const double *alpha, int nnz_A, int *c
     return SBLAS_OK;
 }
 
+// The reference's own partition of cusparse_mgpu_csrmm[_omp]
+// (spmm/src/dspmm_mgpu_baseline.cu:147-150, :291-293): A replicated on every
+// device, B and C split by COLUMNS -- device d takes columns
+// [floor(d*n/g), floor((d+1)*n/g)), i.e. the contiguous column-major slices
+// at B + floor(d*n/g)*k and C + floor(d*n/g)*m.  No exchange; kept as the
+// comparison mode beside the north star's row partition.
+int sblas_csrmm_mgpu_colsplit(int m, int n, int k, const double *alpha, int nnz_A, int *csrRowPtr_A,
+                              int *csrColIndex_A, double *csrVal_A, const double *beta, double *B_dense,
+                              double *C_dense, int ngpu)
+{
+    if (m < 0 || n < 0 || k < 0 || nnz_A < 0 || ngpu <= 0 || !alpha || !beta) return SBLAS_ERR_INVALID;
+    int count;
+    if (sblas_device_count(&count) != SBLAS_OK || count == 0) return SBLAS_ERR_NODEV;
+    std::vector<long long> rp64((size_t)m + 1);
+    for (int i = 0; i <= m; ++i) rp64[(size_t)i] = csrRowPtr_A[i];
+    for (int d = 0; d < ngpu; ++d) {
+        const long long c0 = (long long)d * n / ngpu, c1 = (long long)(d + 1) * n / ngpu;
+        const int dn = (int)(c1 - c0);
+        if (dn <= 0 || m == 0) continue;
+        CsrHold A;
+        SBLAS_TRY(sblas_csr_upload_slice(&A.A, d, k, rp64.data(), csrColIndex_A, csrVal_A, 0, m, 0,
+                                         rp64[(size_t)m], nullptr));
+        const int phys = A.A->device;
+        DeviceGuard g(phys);
+        DevBuf dB, dC;
+        dB.dev = dC.dev = phys;
+        SBLAS_HIP(hipMalloc(&dB.p, sizeof(double) * std::max<size_t>((size_t)k * dn, 1)));
+        SBLAS_HIP(hipMalloc(&dC.p, sizeof(double) * (size_t)m * dn));
+        if ((size_t)k * dn)
+            SBLAS_HIP(hipMemcpy(dB.p, B_dense + (size_t)c0 * k, sizeof(double) * (size_t)k * dn,
+                                hipMemcpyHostToDevice));
+        if (*beta != 0.0)
+            SBLAS_HIP(hipMemcpy(dC.p, C_dense + (size_t)c0 * m, sizeof(double) * (size_t)m * dn,
+                                hipMemcpyHostToDevice));
+        SBLAS_TRY(sblas_spmm(A.A, dn, *alpha, (const double *)dB.p, std::max(k, 1), 0, *beta,
+                             (double *)dC.p, m, nullptr));
+        SBLAS_HIP(hipMemcpy(C_dense + (size_t)c0 * m, dC.p, sizeof(double) * (size_t)m * dn,
+                            hipMemcpyDeviceToHost));
+    }
+    return SBLAS_OK;
+}
+
 // Single-device solve for sblas_sptrsv_syncfree: upload, analyse, one warm-up
 // and one timed solve (the reference times exactly one executor run).
 static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int n,

@@ -70,6 +70,7 @@ _sig("sblas_get_row_from_index", _i, _i, _p, _ll)
 _sig("sblas_get_time", _d)
 _sig("sblas_get_gpu_availble_mem", _d, _i)
 _sig("sblas_csrmm_mgpu", _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _i)
+_sig("sblas_csrmm_mgpu_colsplit", _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _p, _i)
 _sig("sblas_sptrsv_syncfree", _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i)
 _sig("sblas_csr_upload_slice", _i, _p, _i, _i, _p, _p, _p, _i, _i, _ll, _ll, _p)
 _sig("sblas_csr_from_device", _i, _p, _i, _i, _i, _i, _p, _p, _p, _p)

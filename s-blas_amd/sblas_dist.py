@@ -277,13 +277,23 @@ def row_blocks_by_nnz(rowptr: np.ndarray, world: int) -> np.ndarray:
 
 class DistSpMM:
     """One rank's share of C = alpha*A*B + beta*C (B row-major k x ncols on
-    every rank; C column-major m x ncols, kept as a (ncols, m) tensor)."""
+    every rank; C column-major m x ncols, kept as a (ncols, m) tensor).
+
+    split "rows" (default, the north star's partition): whole-row blocks of A
+    by nnz, C row slices all-gathered.  split "cols" (the reference's own,
+    dspmm_mgpu_baseline.cu:147-150): A replicated, rank d owns C/B columns
+    [floor(d*n/g), floor((d+1)*n/g)) -- its C slice is a contiguous block of
+    the (ncols, m) tensor -- and the column slices are all-gathered."""
 
     def __init__(self, rowptr, col, val, k: int, ncols: int, world: int, rank: int, device: int,
-                 torch, dist=None):
+                 torch, dist=None, split: str = "rows"):
         self.torch, self.dist, self.world, self.rank = torch, dist, world, rank
         rp = np.ascontiguousarray(rowptr, np.int64)
         self.m, self.ncols = len(rp) - 1, ncols
+        self.split = split
+        if split == "cols":
+            self._init_cols(rp, col, val, k, device)
+            return
         self.rb = row_blocks_by_nnz(rp, world)
         r0, r1 = int(self.rb[rank]), int(self.rb[rank + 1])
         i0, i1 = int(rp[r0]), int(rp[r1])
@@ -297,18 +307,54 @@ class DistSpMM:
         self.gathered = torch.zeros((world, ncols, self.stride), dtype=f64, device=dev)
         self.c_full = torch.zeros((ncols, self.m), dtype=f64, device=dev)
 
+    def _init_cols(self, rp, col, val, k, device):
+        torch, m, n, g = self.torch, self.m, self.ncols, self.world
+        self.cb = [d * n // g for d in range(g + 1)]
+        self.c0, self.c1 = self.cb[self.rank], self.cb[self.rank + 1]
+        self.A = sblas.DeviceCSR.upload_slice(device, k, rp, np.ascontiguousarray(col, np.int32),
+                                              np.ascontiguousarray(val, np.float64), 0, m, 0, int(rp[-1]))
+        self.wmax = max(self.cb[d + 1] - self.cb[d] for d in range(g))
+        dev = torch.device("cuda", device)
+        f64 = torch.float64
+        self.c_local = torch.zeros((max(self.wmax, 1), m), dtype=f64, device=dev)
+        self.gathered = torch.zeros((g, max(self.wmax, 1), m), dtype=f64, device=dev)
+        self.c_full = torch.zeros((n, m), dtype=f64, device=dev)
+        self.stride = m
+
     def load_c(self, c_full) -> None:
         """Set C (a (ncols, m) device tensor) as the next call's input."""
         self.c_full.copy_(c_full)
+        if self.split == "cols":
+            self.c_local[: self.c1 - self.c0].copy_(self.c_full[self.c0:self.c1])
+            return
         self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[:, self.r0:self.r1])
 
     def kernel(self, alpha: float, B, beta: float, stream=None) -> None:
+        if self.split == "cols":
+            dn = self.c1 - self.c0
+            if dn > 0 and self.m > 0:  # B[:, c0:c1] row-major with ld = ncols
+                self.A.spmm(dn, alpha, B.data_ptr() + 8 * self.c0, self.ncols, 1, beta,
+                            self.c_local.data_ptr(), self.m, stream)
+            return
         if self.r1 > self.r0:
             self.A.spmm(self.ncols, alpha, B.data_ptr(), self.ncols, 1, beta,
                         self.c_local.data_ptr(), self.stride, stream)
 
     def exchange(self) -> None:
         if self.world == 1:
+            return
+        if self.split == "cols":
+            if self.dist.get_backend() == "nccl":
+                self.dist.all_gather_into_tensor(self.gathered.view(-1), self.c_local.reshape(-1))
+            else:  # gloo rehearsal (CPU staging)
+                parts = [torch_zeros_like_cpu(self.c_local) for _ in range(self.world)]
+                self.dist.all_gather(parts, self.c_local.cpu())
+                self.gathered.copy_(self.torch.stack(parts).to(self.gathered.device))
+            for d in range(self.world):
+                a, b = self.cb[d], self.cb[d + 1]
+                if b > a:
+                    self.c_full[a:b].copy_(self.gathered[d, : b - a])
+            self.c_local[: self.c1 - self.c0].copy_(self.c_full[self.c0:self.c1])
             return
         if self.dist.get_backend() == "nccl":
             self.dist.all_gather_into_tensor(self.gathered.view(-1), self.c_local.reshape(-1))
@@ -324,7 +370,7 @@ class DistSpMM:
 
     def result(self):
         if self.world == 1:
-            return self.c_local[:, : self.m]
+            return self.c_local[: self.ncols] if self.split == "cols" else self.c_local[:, : self.m]
         return self.c_full
 
     def close(self) -> None:

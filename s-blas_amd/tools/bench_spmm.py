@@ -71,6 +71,9 @@ def main():
                     help="instead of the rail4284 shape: 16-row blocks each dense (~90%%) over "
                          "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--split", choices=["rows", "cols"], default="rows",
+                    help="rows: whole-row blocks of A by nnz (north star); cols: A replicated, "
+                         "B/C columns split (the reference's dspmm_mgpu_baseline.cu:147-150)")
     args = ap.parse_args()
     import torch
     import sblas
@@ -105,7 +108,7 @@ def main():
         Bd, ldb, lay = B.t().contiguous(), k, 0
     else:
         Bd, ldb, lay = B, n, 1
-    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist)
+    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist, split=args.split)
 
     def step(ev=None):
         if ev is not None:
@@ -171,8 +174,10 @@ def main():
                        "b_layout": "row" if lay == 1 else "col",
                        "structure": f"blocky{args.blocky}" if args.blocky
                        else "rail4284-shaped uniform random",
-                       "partition": "whole-row blocks by nnz, B replicated, C all-gathered"
-                       if world > 1 else "single GPU",
+                       "partition": ("single GPU" if world == 1 else
+                                     "whole-row blocks by nnz, B replicated, C all-gathered"
+                                     if args.split == "rows" else
+                                     "A replicated, B/C column slices, C all-gathered"),
                        "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.25")},
             "roofline": {"bound": "hbm", "achieved": round(abytes / kern_max / 1e6, 1), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(abytes / kern_max / 1e6 / 8000.0, 4)},

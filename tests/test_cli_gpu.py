@@ -197,3 +197,19 @@ def test_config3_two_ranks(extra):
     out = bench_2rank(extra)
     assert out["n_gpus"] == 2 and out["check_vs_oracle"] is True, out
     assert out["config"]["nnz"] == 39_750_000
+
+
+@pytest.mark.parametrize("split", ["rows", "cols"])
+def test_spmm_two_ranks(split):
+    """sblas_dist.DistSpMM on 2 ranks (torchrun children, gloo exchange, HIP
+    kernels): the north star's row blocks and the reference's column split;
+    rank 0 checks 32 rows of C against a host fp64 product."""
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+            os.path.join(ROOT, "s-blas_amd", "tools", "bench_spmm.py"), "--mrows", "1000",
+            "--kcols", "200000", "--nnz", "600000", "--ncols", "40", "--steps", "2", "--warmup", "1",
+            "--dist-backend", "gloo", "--split", split]
+    rc, out, err = run(args, timeout=110)
+    assert rc == 0, out[-3000:] + err[-3000:]
+    res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["max_rel_err_32_rows"] < 1e-12, res

@@ -78,9 +78,12 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     A.close()
 
 
+@pytest.mark.parametrize("split", ["rows", "cols"])
 @pytest.mark.parametrize("ngpu", [1, 2, 3])
-def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu):
-    """cusparse_mgpu_csrmm drop-in on qh768 x 128 (run_test.py's spmm case)."""
+def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
+    """cusparse_mgpu_csrmm drop-in on qh768 x 128 (run_test.py's spmm case),
+    with the north star's row partition and the reference's own column split
+    (A replicated, B/C split by columns, dspmm_mgpu_baseline.cu:147-150)."""
     path = os.path.join(GOLDEN, "qh768.mtx")
     m, k, rp, col, val = sb.mm_read(path, 0)
     ncols = 128
@@ -91,8 +94,9 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu):
     Bf = np.asfortranarray(B)
     rp32 = rp.astype(np.int32)
     a = np.array([-0.7]); b = np.array([0.8])
-    rc = sb.lib.sblas_csrmm_mgpu(m, ncols, k, sb.ptr(a), int(rp[-1]), sb.ptr(rp32), sb.ptr(col),
-                                 sb.ptr(val), sb.ptr(b), Bf.ctypes.data, Cf.ctypes.data, ngpu)
+    fn = sb.lib.sblas_csrmm_mgpu if split == "rows" else sb.lib.sblas_csrmm_mgpu_colsplit
+    rc = fn(m, ncols, k, sb.ptr(a), int(rp[-1]), sb.ptr(rp32), sb.ptr(col),
+            sb.ptr(val), sb.ptr(b), Bf.ctypes.data, Cf.ctypes.data, ngpu)
     assert rc == 0
     want = orc.spmm(m, ncols, k, -0.7, rp32, col, val, B, 0.8, C0)
     assert np.all(np.abs(Cf - want) <= spmm_bound(rp, col, val, B, -0.7, 0.8, C0))
