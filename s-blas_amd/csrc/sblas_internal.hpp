@@ -124,6 +124,7 @@ struct SpmmPlan {
     // workgroup accumulates one (row block x 16 C columns) tile in LDS and
     // writes it to its (XCD, set) partial; a reduce adds the partials.
     int ct_ns = 0, ct_nrb = 0, ct_R = 0, ct_rbits = 0, ct_wlog = 0;
+    bool ct_direct = false;              // keys hold the global column
     unsigned *ct_key = nullptr;
     double *ct_val = nullptr;
     long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets

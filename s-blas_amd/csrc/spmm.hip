@@ -343,11 +343,40 @@ static int build_l2slice(sblas_csr_s &A, const std::vector<int> &rp, const std::
 // slabs are split into ns sets, and each (set, row block, column group) is
 // one workgroup writing an alpha-free partial, added in slot order after.
 constexpr int kCtCols = 16;      // C columns per tile (one 128-B B segment)
-constexpr int kCtPad = 17;       // LDS row stride in doubles (bank spread)
+constexpr int kCtPad = 17;       // LDS row stride in doubles (bank spread; col 16 = pad sink)
 constexpr int kCtThreads = 1024;
-constexpr int kCtU = 8;          // 4-entry steps in flight per wave
 constexpr int kCtMaxRows = 163840 / (kCtPad * 8);  // 1204: one tile per CU
 
+// DPP row_newbcast:s (gfx90a+): every 16-lane row reads lane s of that row
+template <int kS>
+__device__ __forceinline__ unsigned dpp_rowbcast(unsigned v)
+{
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + kS, 0xf, 0xf, false);
+}
+
+// Step T's value for this lane: lanes 0-7 of each 16-lane DPP row (banks 0-1)
+// take lane T of the row, lanes 8-15 (banks 2-3) lane 8 + T -- two bank-masked
+// row_newbcast moves, no select.  Must run with every lane active (a
+// broadcast from an inactive lane returns `old`), so no branch encloses it.
+template <int kT>
+__device__ __forceinline__ unsigned ct_bcast(unsigned v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)v, 0x150 + kT, 0xf, 0x3, false);
+    return (unsigned)__builtin_amdgcn_update_dpp(lo, (int)v, 0x150 + 8 + kT, 0xf, 0xc, false);
+}
+
+// Inner loop: per 64 entries ONE coalesced key load and ONE value load; lane
+// L = 16g + 8h + T holds entry 8T + 2g + h of the 64 (g = DPP row, h = half
+// row), so step T's 8 entries (entry 8T + 2g + h for the lanes of half-row
+// (g, h)) come from row broadcasts, no memory instruction.  An entry's 16 C
+// columns are 8 lanes x 2 doubles: one 16-B B load per lane and two
+// ds_add_f64.  kDirect: keys hold the global column (j << rbits | row);
+// otherwise the XCD-local column of the slab layout.  kFast: B rows 16-B
+// aligned, n % 16 == 0 and B < 4 GiB (32-bit byte offsets); else per-column
+// guards and scalar loads.  Full 64-entry iterations run without checks;
+// the one partial iteration per item routes dead lanes' +0.0 into the row's
+// padding column.
+template <bool kDirect, bool kFast>
 __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     const unsigned *__restrict__ key, const double *__restrict__ val,
     const long long *__restrict__ off, int ns, int nrb, int R, int rbits, int wlog, int ncg,
@@ -365,35 +394,67 @@ __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     __syncthreads();
     const long long e0 = off[(long long)slot * nrb + rb], e1 = off[(long long)slot * nrb + rb + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int sub = lane >> 4, cl = lane & 15;
-    const int col = cg * kCtCols + cl;
-    const bool live_c = col < n;
-    const int cc = live_c ? col : 0;
+    const int g = lane >> 4, h = (lane >> 3) & 1, q = lane & 7;
+    const int myoff = 8 * (lane & 7) + 2 * g + h;
+    const int mypos = 2 * g + h;  // this lane's entry within a step
+    const int c0 = cg * kCtCols + 2 * q;
+    const bool live0 = kFast || c0 < n, live1 = kFast || c0 + 1 < n;
     const unsigned rmask = (1u << rbits) - 1;
     const unsigned wmask = (1u << wlog) - 1;
-    // XCD-local column jc -> global column: slab (jc >> wlog) * 8 + x
-    auto gcol = [&](unsigned jc) -> long long {
+    const int cq0 = live0 ? c0 : 0, cq1 = live1 ? c0 + 1 : cq0;
+    const unsigned ldb8 = (unsigned)(ldb * 8);
+    const char *Bc = reinterpret_cast<const char *>(B) + (size_t)cq0 * 8;
+    typedef double v2d_t __attribute__((ext_vector_type(2)));
+    auto brow = [&](unsigned kt) -> long long {
+        const unsigned jc = kt >> rbits;
+        if constexpr (kDirect) return (long long)jc;
         return ((long long)(jc >> wlog) << (wlog + 3)) | ((long long)x << wlog) | (jc & wmask);
     };
-    constexpr long long kStride = (long long)(kCtThreads / 64) * 4 * kCtU;
-    for (long long it = e0 + (long long)wv * 4 * kCtU; it < e1; it += kStride) {
-        unsigned k[kCtU];
-        double v[kCtU], b[kCtU];
+    constexpr long long kStride = (long long)(kCtThreads / 64) * 64;
+    auto body = [&](long long it, bool tail) {
+        const long long e = it + myoff;
+        const long long ec = e < e1 ? e : e1 - 1;
+        const unsigned kk = key[ec];
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(val[ec]);
+        const unsigned vlo = (unsigned)vb, vhi = (unsigned)(vb >> 32);
+        unsigned kt[8];
+        kt[0] = ct_bcast<0>(kk); kt[1] = ct_bcast<1>(kk); kt[2] = ct_bcast<2>(kk); kt[3] = ct_bcast<3>(kk);
+        kt[4] = ct_bcast<4>(kk); kt[5] = ct_bcast<5>(kk); kt[6] = ct_bcast<6>(kk); kt[7] = ct_bcast<7>(kk);
+        double b0[8], b1[8];
 #pragma unroll
-        for (int u = 0; u < kCtU; ++u) {
-            const long long e = it + 4 * u + sub;
-            const long long ec = e < e1 ? e : e1 - 1;
-            k[u] = key[ec];
-            v[u] = e < e1 ? val[ec] : 0.0;
+        for (int t = 0; t < 8; ++t) {
+            if constexpr (kFast) {
+                const v2d_t bb = *reinterpret_cast<const v2d_t *>(Bc + (unsigned)brow(kt[t]) * ldb8);
+                b0[t] = bb.x;
+                b1[t] = bb.y;
+            } else {
+                const double *br = B + brow(kt[t]) * ldb;
+                b0[t] = br[cq0];
+                b1[t] = br[cq1];
+            }
         }
+        unsigned lo[8], hi[8];
+        lo[0] = ct_bcast<0>(vlo); lo[1] = ct_bcast<1>(vlo); lo[2] = ct_bcast<2>(vlo); lo[3] = ct_bcast<3>(vlo);
+        lo[4] = ct_bcast<4>(vlo); lo[5] = ct_bcast<5>(vlo); lo[6] = ct_bcast<6>(vlo); lo[7] = ct_bcast<7>(vlo);
+        hi[0] = ct_bcast<0>(vhi); hi[1] = ct_bcast<1>(vhi); hi[2] = ct_bcast<2>(vhi); hi[3] = ct_bcast<3>(vhi);
+        hi[4] = ct_bcast<4>(vhi); hi[5] = ct_bcast<5>(vhi); hi[6] = ct_bcast<6>(vhi); hi[7] = ct_bcast<7>(vhi);
 #pragma unroll
-        for (int u = 0; u < kCtU; ++u) b[u] = B[gcol(k[u] >> rbits) * ldb + cc];
-#pragma unroll
-        for (int u = 0; u < kCtU; ++u) {
-            const long long e = it + 4 * u + sub;
-            if (live_c && e < e1) atomicAdd(&tile[(k[u] & rmask) * kCtPad + cl], v[u] * b[u]);
+        for (int t = 0; t < 8; ++t) {
+            const double vt = __longlong_as_double((long long)(((unsigned long long)hi[t] << 32) | lo[t]));
+            double *row_p = &tile[(kt[t] & rmask) * kCtPad];
+            if (!tail && kFast) {
+                atomicAdd(row_p + 2 * q, vt * b0[t]);
+                atomicAdd(row_p + 2 * q + 1, vt * b1[t]);
+            } else {  // dead lanes add +0.0 into the padding column
+                const bool ok = it + 8 * t + mypos < e1;
+                atomicAdd(row_p + ((ok && live0) ? 2 * q : kCtCols), (ok && live0) ? vt * b0[t] : 0.0);
+                atomicAdd(row_p + ((ok && live1) ? 2 * q + 1 : kCtCols), (ok && live1) ? vt * b1[t] : 0.0);
+            }
         }
-    }
+    };
+    long long it = e0 + (long long)wv * 64;
+    for (; it + 64 <= e1; it += kStride) body(it, false);
+    if (it < e1) body(it, true);  // uniform: this wave's partial iteration
     __syncthreads();
     // partial [slot][column][row] (column-major like C): coalesced over rows
     const int ncol = min(kCtCols, n - cg * kCtCols);
@@ -460,13 +521,18 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     for (int r = 0; r < m; ++r)
         for (int e = rp[r]; e < rp[r + 1]; ++e) off[(size_t)bucket(r, hcol[e]) + 1]++;
     for (int b = 0; b < nbk; ++b) off[(size_t)b + 1] += off[(size_t)b];
+    // direct keys (global column << rbits | row) when the column fits: the
+    // kernel then needs no slab arithmetic; sorting is the same order
+    const bool direct = (long long)k <= (1LL << (32 - rbits)) && !(getenv("SBLAS_SPMM_CTDIRECT") &&
+                                                                     atoi(getenv("SBLAS_SPMM_CTDIRECT")) == 0);
     std::vector<unsigned long long> kv((size_t)std::max<long long>(A.nnz, 1));  // key << 32 | entry index
     {
         std::vector<long long> next(off.begin(), off.end() - 1);
         for (int r = 0; r < m; ++r)
             for (int e = rp[r]; e < rp[r + 1]; ++e) {
                 const int c = hcol[e];
-                const unsigned jc = (unsigned)((((long long)(c >> wlog) >> 3) << wlog) | (c & ((1 << wlog) - 1)));
+                const unsigned jc = direct ? (unsigned)c
+                                           : (unsigned)((((long long)(c >> wlog) >> 3) << wlog) | (c & ((1 << wlog) - 1)));
                 const unsigned kk = (jc << rbits) | (unsigned)(r % R);
                 kv[(size_t)next[(size_t)bucket(r, c)]++] = ((unsigned long long)kk << 32) | (unsigned)e;
             }
@@ -491,6 +557,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     P.ct_R = R;
     P.ct_rbits = rbits;
     P.ct_wlog = wlog;
+    P.ct_direct = direct;
     return SBLAS_OK;
 }
 
@@ -659,13 +726,21 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         const size_t lds = sizeof(double) * (size_t)P.ct_R * kCtPad;
         static thread_local bool attr_set[64] = {};
         if (!attr_set[A.device & 63]) {  // > 64 KiB of dynamic LDS
-            SBLAS_HIP(hipFuncSetAttribute((const void *)k_spmm_ctile, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)(sizeof(double) * kCtMaxRows * kCtPad)));
+            const void *ks[4] = {(const void *)k_spmm_ctile<true, false>, (const void *)k_spmm_ctile<true, true>,
+                                 (const void *)k_spmm_ctile<false, false>, (const void *)k_spmm_ctile<false, true>};
+            for (const void *kf : ks)
+                SBLAS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)(sizeof(double) * kCtMaxRows * kCtPad)));
             attr_set[A.device & 63] = true;
         }
-        hipLaunchKernelGGL(k_spmm_ctile, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val,
-                           P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr, n,
-                           A.m, S.bt);
+        const bool fast = (ldr % 2 == 0) && (n % kCtCols == 0) && (((uintptr_t)Brow & 15) == 0) &&
+                          (unsigned long long)A.n * (unsigned long long)ldr * 8ULL < (1ULL << 32);
+        using K = void (*)(const unsigned *, const double *, const long long *, int, int, int, int, int, int,
+                           const double *, long long, int, int, double *);
+        K kern = P.ct_direct ? (fast ? k_spmm_ctile<true, true> : k_spmm_ctile<true, false>)
+                             : (fast ? k_spmm_ctile<false, true> : k_spmm_ctile<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_off,
+                           P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr, n, A.m, S.bt);
         const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
         if (beta != 0.0)
             hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,

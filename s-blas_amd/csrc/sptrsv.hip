@@ -55,6 +55,7 @@ struct sblas_trsv_s {
     int *lrow = nullptr, *lrp = nullptr, *lcol = nullptr;
     double *lval = nullptr;
     int *lptr_d = nullptr;
+    unsigned *larrive = nullptr;            // grid barrier: arrival epoch per workgroup
     std::vector<int> lptr;                  // host copy [nlevels + 1]
     std::vector<std::pair<int, int>> lsched;  // (first level, end level); end < 0: wide level
 };
@@ -530,6 +531,7 @@ __global__ __launch_bounds__(256) void k_trsv_level(const int *__restrict__ lrp,
 
 constexpr int kLevelWG = 1024;         // threads of the narrow-run workgroup
 constexpr int kLevelNarrow = 2 * kLevelWG;  // a level with <= this many rows is narrow
+constexpr int kLevelMaxWG = 1024;           // grid-barrier workgroups (arrival words)
 
 __global__ __launch_bounds__(kLevelWG) void k_trsv_level_run(
     const int *__restrict__ lrp, const int *__restrict__ lcol, const double *__restrict__ lval,
@@ -542,6 +544,69 @@ __global__ __launch_bounds__(kLevelWG) void k_trsv_level_run(
         // this level's x stores (agent scope) complete before any wave reads them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+    }
+}
+
+// A run of wide levels in ONE launch: a persistent grid (every workgroup
+// resident) strides over each level's rows, then meets at a grid barrier.
+// The barrier avoids one hot counter (256 RMWs on one address serialise at
+// the memory side: ~19 us per level, measured): workgroup w stores its
+// arrival epoch into its own word arrive[w]; workgroup 0's first wave reads
+// all of them (64 per load) and then publishes the epoch in a release word
+// that everyone polls.  Plain agent-scope (sc1) loads/stores, no fences: x
+// itself travels through agent-scope stores and sc1 loads, and every wave's
+// x stores drained (vmcnt(0)) before its workgroup's barrier.  Bounded
+// spins; the abort word voids the solve as in the sync-free executors.
+__global__ __launch_bounds__(1024) void k_trsv_level_grid(
+    const int *__restrict__ lrp, const int *__restrict__ lcol, const double *__restrict__ lval,
+    const int *__restrict__ lrow, const int *__restrict__ lptr, int l0, int l1, int backward,
+    const double *__restrict__ b, double *x, unsigned *ctl, unsigned *arrive)
+{
+    const unsigned nwg = gridDim.x;
+    unsigned *release = &ctl[1];
+    for (int l = l0; l < l1; ++l) {
+        const int p1 = lptr[l + 1];
+        for (int k = lptr[l] + (int)(blockIdx.x * blockDim.x + threadIdx.x); k < p1;
+             k += (int)(nwg * blockDim.x))
+            level_row(lrp, lcol, lval, lrow, k, backward, b, x);
+        if (l + 1 == l1) break;
+        const unsigned epoch = (unsigned)(l - l0 + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&arrive[blockIdx.x], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool bail = false;
+        if (blockIdx.x == 0 && threadIdx.x < 64) {  // the master wave gathers every arrival
+            unsigned spins = 0;
+            for (;;) {
+                bool all = true;
+                for (unsigned w = threadIdx.x; w < nwg; w += 64)
+                    all &= __hip_atomic_load(&arrive[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+                if (__all(all)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 255u) == 0 &&
+                    (spins > kSpinLimit || __hip_atomic_load(&ctl[kAbort], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                    bail = true;
+                    break;
+                }
+            }
+            if (threadIdx.x == 0) {
+                if (bail) atomicOr(&ctl[kAbort], 1u);
+                else __hip_atomic_store(release, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 1023u) == 0 &&
+                    (spins > kSpinLimit || __hip_atomic_load(&ctl[kAbort], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                    atomicOr(&ctl[kAbort], 1u);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (__hip_atomic_load(&ctl[kAbort], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     }
 }
 
@@ -674,17 +739,16 @@ static int build_levelset(sblas_trsv_s *T, hipStream_t s)
         std::copy(rv.begin() + rrp[(size_t)i], rv.begin() + rrp[(size_t)i + 1], lv.begin() + lrp[(size_t)k]);
         lrp[(size_t)k + 1] = lrp[(size_t)k] + len;
     }
-    // schedule: maximal runs of narrow levels, single wide levels
+    // schedule: maximal runs of narrow levels (one workgroup, workgroup
+    // barriers) and of wide levels (persistent grid, grid barriers), encoded
+    // (l0, l1) narrow / (l0, -l1) wide
     T->lsched.clear();
+    auto narrow = [&](int l) { return T->lptr[(size_t)l + 1] - T->lptr[(size_t)l] <= kLevelNarrow; };
     for (int l = 0; l < nl;) {
-        if (T->lptr[(size_t)l + 1] - T->lptr[(size_t)l] > kLevelNarrow) {
-            T->lsched.push_back({l, -1});
-            ++l;
-            continue;
-        }
+        const bool nw = narrow(l);
         int e = l;
-        while (e < nl && T->lptr[(size_t)e + 1] - T->lptr[(size_t)e] <= kLevelNarrow) ++e;
-        T->lsched.push_back({l, e});
+        while (e < nl && narrow(e) == nw) ++e;
+        T->lsched.push_back({l, nw ? e : -e});
         l = e;
     }
     SBLAS_HIP(hipMalloc(&T->lrow, sizeof(int) * lrow.size()));
@@ -692,6 +756,7 @@ static int build_levelset(sblas_trsv_s *T, hipStream_t s)
     SBLAS_HIP(hipMalloc(&T->lcol, sizeof(int) * lc.size()));
     SBLAS_HIP(hipMalloc(&T->lval, sizeof(double) * lv.size()));
     SBLAS_HIP(hipMalloc(&T->lptr_d, sizeof(int) * T->lptr.size()));
+    SBLAS_HIP(hipMalloc(&T->larrive, sizeof(unsigned) * kLevelMaxWG));
     SBLAS_HIP(hipMemcpy(T->lrow, lrow.data(), sizeof(int) * lrow.size(), hipMemcpyHostToDevice));
     SBLAS_HIP(hipMemcpy(T->lrp, lrp.data(), sizeof(int) * lrp.size(), hipMemcpyHostToDevice));
     SBLAS_HIP(hipMemcpy(T->lcol, lc.data(), sizeof(int) * lc.size(), hipMemcpyHostToDevice));
@@ -703,18 +768,41 @@ static int build_levelset(sblas_trsv_s *T, hipStream_t s)
 static int solve_levelset(sblas_trsv_s *T, const double *b, double *x, hipStream_t s)
 {
     SBLAS_TRY(build_levelset(T, s));
+    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
+    int ncu = 0;
+    SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, T->device));
+    static const int per_level = [] {  // experiments: one launch per wide level
+        const char *e = getenv("SBLAS_TRSV_LEVEL_LAUNCH");
+        return e ? atoi(e) : 0;
+    }();
     for (const auto &seg : T->lsched) {
-        if (seg.second < 0) {
-            const int p0 = T->lptr[(size_t)seg.first], p1 = T->lptr[(size_t)seg.first + 1];
-            hipLaunchKernelGGL(k_trsv_level, dim3((unsigned)((p1 - p0 + 255) / 256)), dim3(256), 0, s, T->lrp,
-                               T->lcol, T->lval, T->lrow, p0, p1, T->substitution, b, x);
+        if (seg.second < 0 && per_level) {
+            for (int l = seg.first; l < -seg.second; ++l) {
+                const int p0 = T->lptr[(size_t)l], p1 = T->lptr[(size_t)l + 1];
+                hipLaunchKernelGGL(k_trsv_level, dim3((unsigned)((p1 - p0 + 255) / 256)), dim3(256), 0, s, T->lrp,
+                                   T->lcol, T->lval, T->lrow, p0, p1, T->substitution, b, x);
+            }
+        } else if (seg.second < 0) {
+            // one 1024-thread workgroup per CU: all resident (the barrier's premise)
+            const int nwg = std::max(1, std::min(ncu, kLevelMaxWG));
+            SBLAS_HIP(hipMemsetAsync(T->ctl, 0, 8, s));
+            SBLAS_HIP(hipMemsetAsync(T->larrive, 0, sizeof(unsigned) * kLevelMaxWG, s));
+            hipLaunchKernelGGL(k_trsv_level_grid, dim3((unsigned)nwg), dim3(1024), 0, s, T->lrp, T->lcol, T->lval,
+                               T->lrow, T->lptr_d, seg.first, -seg.second, T->substitution, b, x, T->ctl,
+                               T->larrive);
         } else {
             hipLaunchKernelGGL(k_trsv_level_run, dim3(1), dim3(kLevelWG), 0, s, T->lrp, T->lcol, T->lval, T->lrow,
                                T->lptr_d, seg.first, seg.second, T->substitution, b, x);
         }
     }
     SBLAS_HIP(hipGetLastError());
+    unsigned h[kCtlBytes / 4] = {0};
+    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, kCtlBytes, hipMemcpyDeviceToHost, s));
     SBLAS_HIP(hipStreamSynchronize(s));
+    if (h[kAbort]) {
+        set_error("sptrsv level-set: grid barrier spin limit exceeded");
+        return SBLAS_ERR_HIP;
+    }
     return SBLAS_OK;
 }
 
@@ -808,6 +896,7 @@ int sblas_trsv_destroy(sblas_trsv T)
         (void)hipFree(T->lcol);
         (void)hipFree(T->lval);
         (void)hipFree(T->lptr_d);
+        (void)hipFree(T->larrive);
     }
     delete T;
     return SBLAS_OK;

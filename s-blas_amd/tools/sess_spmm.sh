@@ -3,8 +3,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python -u -m pytest tests/test_kernels_gpu.py -k "spmm or sptrsv" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_spmm.log 2>&1 || { tail -30 gpurun_out/t_spmm.log; exit 1; }
+$T 600 python -u -m pytest tests/test_kernels_gpu.py -k "spmm or sptrsv or csrmm" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_spmm.log 2>&1 || { tail -30 gpurun_out/t_spmm.log; exit 1; }
 tail -2 gpurun_out/t_spmm.log
+$T 400 python -u -m pytest tests/test_cli_gpu.py -k "spmm_two_ranks" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_2r.log 2>&1 || { tail -30 gpurun_out/t_2r.log; exit 1; }
 $T 400 python -u -m pytest tests/test_configs_gpu.py -k "config4 or config5_single" -x -q --timeout 250 --timeout-method thread > gpurun_out/t_cfg4.log 2>&1 || { tail -30 gpurun_out/t_cfg4.log; exit 1; }
 tail -2 gpurun_out/t_cfg4.log
 for w in 11 10 12 9; do
