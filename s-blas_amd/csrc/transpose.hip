@@ -10,6 +10,7 @@
 // sorted keys.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -209,6 +210,188 @@ __global__ __launch_bounds__(kRxThreads, 2) void k_rx_scatter(
     }
 }
 
+// ---- wide-digit variant (default): up to 11-bit digits, 2 passes for n <=
+// 4M columns instead of 3.  Workgroup b sorts the contiguous tiles
+// [b*S, (b+1)*S) in order, so (i) the count matrix is digits x workgroups,
+// not digits x tiles, and (ii) a digit's output run of tile t+1 continues
+// exactly where tile t's ended: the same CU appends to the same lines, which
+// its XCD's L2 merges before write-back (with 2,048 digits a tile's runs are
+// only ~2 entries long).  Ranking per 256-element batch: RB wave ballots give
+// the in-wave rank; the first lane of each (wave, digit) group posts the
+// group's size, so LDS work per element is O(waves), not O(digits).
+constexpr int kRx2MaxDigits = 2048;
+constexpr int kRx2CountSplit = 8;  // count workgroups per scatter workgroup segment
+
+// counts[d][wg] of each scatter workgroup's segment: kRx2CountSplit small
+// workgroups per segment (8 KiB LDS each, many per CU), 16 keys in flight per
+// thread, histograms merged with global atomics (counts zeroed first).
+__global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict__ keys, long long nnz,
+                                                          int shift, int rb, int S, int nwg,
+                                                          int *__restrict__ counts)
+{
+    __shared__ int h[kRx2MaxDigits];
+    const int D = 1 << rb;
+    for (int d = threadIdx.x; d < D; d += kRxThreads) h[d] = 0;
+    __syncthreads();
+    const int wg = (int)blockIdx.x / kRx2CountSplit, part = (int)blockIdx.x % kRx2CountSplit;
+    const long long seg0 = (long long)wg * S * kRxTile;
+    const long long seg1 = min(nnz, seg0 + (long long)S * kRxTile);
+    const long long len = max(0LL, seg1 - seg0);
+    const long long p0 = seg0 + len * part / kRx2CountSplit, p1 = seg0 + len * (part + 1) / kRx2CountSplit;
+    constexpr int kU = 16;
+    for (long long i0 = p0; i0 < p1; i0 += (long long)kU * kRxThreads) {
+        int d[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const long long i = i0 + (long long)u * kRxThreads + threadIdx.x;
+            d[u] = i < p1 ? ((keys[i] >> shift) & (D - 1)) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (d[u] >= 0) atomicAdd(&h[d[u]], 1);
+    }
+    __syncthreads();
+    for (int dd = threadIdx.x; dd < D; dd += kRxThreads)
+        if (h[dd]) atomicAdd(&counts[(size_t)dd * nwg + wg], h[dd]);
+}
+
+// Scatter: workgroup b sorts tiles [b*S, (b+1)*S) in order.  Wave w ranks
+// the contiguous quarter [w*1024, (w+1)*1024) of a tile in 16 batches of 64
+// with WAVE-PRIVATE digit counters (a wave's LDS operations retire in
+// program order, so no barrier per batch): rank = wcnt[w][d] + in-batch rank
+// from RB ballots.  Two barriers per tile then turn the per-wave counts into
+// the tile's digit offsets.  The next tile's (key, row, value) are loaded
+// into registers while the current one is ranked and written.
+template <int kMaxD>
+__global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
+    const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
+    int shift, int rb, int S, int nwg, const int *__restrict__ incl, int *__restrict__ kout,
+    int *__restrict__ rout, double *__restrict__ vout)
+{
+    __shared__ int wcnt[kRxWaves][kMaxD];  // per-wave counts, then per-wave starts
+    __shared__ int lstart[kMaxD], gbase[kMaxD];
+    __shared__ int wtot[kRxWaves];
+    __shared__ int skey[kRxTile], srow[kRxTile];
+    __shared__ double sval[kRxTile];
+    constexpr int kQ = kRxTile / kRxWaves;  // elements per wave per tile (1024)
+    constexpr int kB = kQ / 64;             // batches per wave (16)
+    static_assert(kB == kRxItems, "one register slot per batch");
+    const int D = 1 << rb, dm = D - 1;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int d = t; d < D; d += kRxThreads) {
+        const size_t idx = (size_t)d * nwg + blockIdx.x;
+        gbase[d] = idx ? incl[idx - 1] : 0;  // exclusive start of this workgroup's run of d
+#pragma unroll
+        for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] = 0;
+    }
+    int kk[kB], rr[kB];
+    double vv[kB];
+    auto load_tile = [&](long long base, int valid) {
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            const int li = w * kQ + j * 64 + lane;
+            const bool ok = li < valid;
+            const long long gi = ok ? base + li : 0;
+            kk[j] = ok ? kin[gi] : -1;  // top digit, ranked after every real element
+            rr[j] = ok ? rin[gi] : 0;
+            vv[j] = ok ? vin[gi] : 0.0;
+        }
+    };
+    long long base = (long long)blockIdx.x * S * kRxTile;
+    int valid = base < nnz ? (int)min((long long)kRxTile, nnz - base) : 0;
+    if (valid > 0) load_tile(base, valid);
+    __syncthreads();
+    for (int st = 0; st < S && valid > 0; ++st) {  // valid: workgroup-uniform
+        int lp[kB];
+        // 1. wave-private ranking
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            const int d = (kk[j] >> shift) & dm;
+            unsigned long long mm = ~0ull;
+            for (int b = 0; b < rb; ++b) {
+                const unsigned long long bal = __ballot((d >> b) & 1);
+                mm &= ((d >> b) & 1) ? bal : ~bal;
+            }
+            const int rank = __popcll(mm & lt);
+            lp[j] = wcnt[w][d] + rank;
+            if (rank == 0) wcnt[w][d] += __popcll(mm);
+        }
+        // padding (top digit, after every real element) is not part of the output
+        if (t == kRxThreads - 1 && valid < kRxTile) wcnt[kRxWaves - 1][dm] -= kRxTile - valid;
+        __syncthreads();
+        // 2. digit totals, per-wave starts inside each digit, exclusive scan
+        constexpr int kPer = (kMaxD + kRxThreads - 1) / kRxThreads;
+        int tot[kPer];
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int d = t * kPer + k;
+            int c = 0;
+            if (d < D) {
+#pragma unroll
+                for (int q = 0; q < kRxWaves; ++q) {
+                    const int v = wcnt[q][d];
+                    wcnt[q][d] = c;  // this wave's start within digit d
+                    c += v;
+                }
+            }
+            tot[k] = c;
+            sum += c;
+        }
+        const int inc = wave_incl_scan(sum);
+        if (lane == 63) wtot[w] = inc;
+        __syncthreads();
+        int ex = inc - sum;
+        for (int q = 0; q < w; ++q) ex += wtot[q];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int d = t * kPer + k;
+            if (d < D) {
+                lstart[d] = ex;
+#pragma unroll
+                for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] += ex;  // absolute tile position
+            }
+            ex += tot[k];
+        }
+        __syncthreads();
+        // 3. stage in digit order
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            if (w * kQ + j * 64 + lane < valid) {
+                const int pos = wcnt[w][(kk[j] >> shift) & dm] + lp[j];
+                skey[pos] = kk[j];
+                srow[pos] = rr[j];
+                sval[pos] = vv[j];
+            }
+        }
+        __syncthreads();
+        // 4. prefetch the next tile, write this one out as per-digit runs
+        const long long nbase = base + kRxTile;
+        const int nvalid = (st + 1 < S && nbase < nnz) ? (int)min((long long)kRxTile, nnz - nbase) : 0;
+        if (nvalid > 0) load_tile(nbase, nvalid);
+        for (int li = t; li < valid; li += kRxThreads) {
+            const int k = skey[li];
+            const int d = (k >> shift) & dm;
+            const long long g = (long long)gbase[d] + (li - lstart[d]);
+            kout[g] = k;
+            rout[g] = srow[li];
+            vout[g] = sval[li];
+        }
+        __syncthreads();
+        // 5. the next tile appends after this one; counters restart
+        for (int d = t; d < D; d += kRxThreads) {
+            const int nxt = d < dm ? lstart[d + 1] : valid;
+            gbase[d] += nxt - lstart[d];
+#pragma unroll
+            for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] = 0;
+        }
+        __syncthreads();
+        base = nbase;
+        valid = nvalid;
+    }
+}
+
 // colptr from the sorted keys: colptr[c] = first position whose key >= c
 __global__ void k_colptr_sorted(const int *__restrict__ keys, long long nnz, int n, int *__restrict__ colptr)
 {
@@ -238,9 +421,33 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     }
     int nbits = 0;
     while (nbits < 31 && (n - 1) >> nbits) ++nbits;
-    const int passes = std::max(1, (nbits + 7) / 8);
+    // wide digits (default; SBLAS_TRANSPOSE_RB=8 selects the 8-bit path)
+    // SBLAS_TRANSPOSE_RB=8 selects the one-tile-per-workgroup 8-bit path;
+    // otherwise digits of at most SBLAS_TRANSPOSE_RBMAX bits (default 8: a
+    // workgroup's partially written digit runs -- 2^rb per array -- must fit
+    // its share of the XCD's L2 until they merge; 11-bit digits measured
+    // 0.85 ms per pass against ~0.3 ms), spread evenly over the passes
+    const char *rb_e = getenv("SBLAS_TRANSPOSE_RB");
+    const int rb_env = rb_e ? atoi(rb_e) : 0;
+    const char *rbm_e = getenv("SBLAS_TRANSPOSE_RBMAX");
+    const int rbmax = std::max(1, std::min(11, rbm_e ? atoi(rbm_e) : 8));
+    const bool wide = rb_env != 8;
+    const int passes = wide ? std::max(1, (nbits + rbmax - 1) / rbmax) : std::max(1, (nbits + 7) / 8);
+    const int rb = wide ? std::max(1, (nbits + passes - 1) / passes) : 8;
     const int ntiles = (int)((nnz + kRxTile - 1) / kRxTile);
-    const long long ncnt = 256LL * ntiles;
+    int ncu = 256;
+    {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    }
+    // tiles per workgroup: one round of resident workgroups (2 per CU for
+    // <= 8-bit digits, 1 per CU above); SBLAS_TRANSPOSE_WGCU overrides
+    const char *wgcu_e = getenv("SBLAS_TRANSPOSE_WGCU");
+    const int wgcu = wgcu_e ? std::max(1, atoi(wgcu_e)) : 2;
+    const int S_t = wide ? std::max(1, (ntiles + ncu * wgcu - 1) / (ncu * wgcu)) : 1;
+    const int nwg = (ntiles + S_t - 1) / S_t;
+    const long long ncnt = wide ? (long long)(1 << rb) * nwg : 256LL * ntiles;
     const size_t scan_ints = (size_t)(ncnt / kScanTile + 64) * 2;
     // scratch: keysA rowsA valsA | keysB rowsB valsB | counts | scan (+ outputs when null)
     const size_t z = (size_t)nnz;
@@ -276,10 +483,24 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         int *ko = (ps & 1) ? keysB : keysA;
         int *ro = last ? rout_final : ((ps & 1) ? rowsB : rowsA);
         double *vo = last ? vout_final : ((ps & 1) ? valsB : valsA);
-        hipLaunchKernelGGL(k_rx_count, dim3(ntiles), dim3(kRxThreads), 0, s, kin, nnz, shift, ntiles, counts);
-        SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
-        hipLaunchKernelGGL(k_rx_scatter, dim3(ntiles), dim3(kRxThreads), 0, s, kin, rin, vin, nnz, shift,
-                           ntiles, counts, ko, ro, vo);
+        if (wide) {
+            const int sh = rb * ps;
+            SBLAS_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)ncnt, s));
+            hipLaunchKernelGGL(k_rx2_count, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s, kin, nnz,
+                               sh, rb, S_t, nwg, counts);
+            SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
+            if (rb <= 8)  // 71 KiB of LDS: two workgroups per CU
+                hipLaunchKernelGGL(k_rx2_scatter<256>, dim3(nwg), dim3(kRxThreads), 0, s, kin, rin, vin, nnz, sh, rb,
+                                   S_t, nwg, counts, ko, ro, vo);
+            else
+                hipLaunchKernelGGL(k_rx2_scatter<kRx2MaxDigits>, dim3(nwg), dim3(kRxThreads), 0, s, kin, rin, vin, nnz,
+                                   sh, rb, S_t, nwg, counts, ko, ro, vo);
+        } else {
+            hipLaunchKernelGGL(k_rx_count, dim3(ntiles), dim3(kRxThreads), 0, s, kin, nnz, shift, ntiles, counts);
+            SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
+            hipLaunchKernelGGL(k_rx_scatter, dim3(ntiles), dim3(kRxThreads), 0, s, kin, rin, vin, nnz, shift,
+                               ntiles, counts, ko, ro, vo);
+        }
         kin = ko;
         rin = ro;
         vin = vo;

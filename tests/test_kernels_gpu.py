@@ -108,15 +108,29 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols"])
-def test_transpose_bit_exact(torch_cuda, sb, orc, case):
+@pytest.mark.parametrize("digits", ["default", "rb11", "rb8"])
+@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "big"])
+def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
+    """Stable radix transpose: tiles-per-workgroup path with <= 8-bit digits
+    (default; "big" = 3 passes of 8 bits at n = 3M, 2 tiles per workgroup),
+    the same with 11-bit digits, and the one-tile 8-bit path."""
     torch = torch_cuda
+    if digits == "rb8":
+        monkeypatch.setenv("SBLAS_TRANSPOSE_RB", "8")
+    if digits == "rb11":
+        monkeypatch.setenv("SBLAS_TRANSPOSE_RBMAX", "11")
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
     elif case == "random":
         m, n = 3000, 2500
         rp, col, val = rand_csr(rng, m, n, 30)
+    elif case == "big":  # 2.2M nonzeros over 3M columns: 2 passes x 11 bits, 2 tiles per workgroup
+        m, n = 110000, 3_000_000
+        lens = rng.integers(0, 40, m)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
     else:  # columns longer than 32 / 4096 (medium and big sort paths)
         m, n = 9000, 40
         rp, col, val = rand_csr(rng, m, n, 40, empty_frac=0.2)
