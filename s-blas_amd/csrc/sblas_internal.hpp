@@ -171,7 +171,7 @@ struct XsArgs {
     int qstride;
     int G, q, Wg;
     int use_xcc;
-    int kstride, vstride;   // chunk strides in 16-B units (keys, values)
+    int kstride, vstride;   // chunk strides in 16-B units (keys, values); K24: the chunk size
     long long *trace;       // debugging aid (SBLAS_XS_TRACE), else null
 };
 
@@ -184,6 +184,7 @@ struct XsPlan {
     uint32_t *key = nullptr;     // owns the chunk storage (keys and values)
     double *val = nullptr;       // values inside it (interleaved per chunk by default)
     int kstride = 64, vstride = 128;
+    bool k24 = false;            // 24-bit keys, 320-entry chunks (xsort.hip "K24 chunks")
     int *qitems = nullptr;
     long long *xrec = nullptr;   // item records (see XsArgs)
     int *qhead = nullptr;        // [2][16]: claim heads per launch parity

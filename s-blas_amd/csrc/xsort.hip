@@ -60,6 +60,20 @@ constexpr int kXsChunk = 256;      // entries per chunk: one wave, 4 per lane
 constexpr int kXsUnroll = 2;       // chunks per wave per pipeline stage
 constexpr uint32_t kXsPad = ((1u << kXsColBits) - 1) << kXsRowBits;  // column all ones, row 0
 constexpr int kXsTrace = 6;        // longs per trace row
+// K24 chunks (opt-in, SBLAS_XS_K24; measured slower, see the planner): 320 entries = 5 sub-chunks of
+// 64; a key is 24 bits, (column - sub-chunk base) << 13 | local row, the base
+// being the group-local column of the sub-chunk's first entry; a sub-chunk
+// ends early rather than span more than kK24Span columns.  Lane l's 16-B key
+// load holds the keys of entries l, 64+l, ..., 256+l (5 x 24 bits); values
+// {l, 64+l} and {128+l, 192+l} as two 16-B loads and 256+l as one 8-B load;
+// the 5 bases sit in a 32-B header read with scalar loads.  11.1 B per entry
+// on config 2's narrow blocks against 12 for the 32-bit keys.
+constexpr int kK24RowBits = 13;
+constexpr uint32_t kK24Mask = (1u << 24) - 1;
+constexpr uint32_t kK24Pad = kK24Mask;  // column offset all ones, row all ones
+constexpr int kK24Span = (1 << (24 - kK24RowBits)) - 2;  // largest column offset (2046)
+constexpr int kK24Bytes = 1024 + 2560 + 32;              // keys | values | header
+static_assert(kK24Bytes % 16 == 0, "16-B aligned chunks");
 static_assert(kXsRowBits + kXsColBits == 32, "packed key is 32 bits");
 static_assert(kXsRows <= (1 << kXsRowBits), "local row must fit the key");
 
@@ -281,6 +295,111 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
     }
 }
 
+// K24 form of xs_stream_dyn (same claims, same pipeline): per chunk one 16-B
+// key load, two 16-B and one 8-B value loads, a 32-B scalar header.
+template <int kMode, int U = kXsUnroll>
+__device__ __forceinline__ void xs_stream_dyn24(const unsigned char *__restrict__ base, int *ctr, long long c0,
+                                                long long c1, const long long *bnd, int gb, int Wg,
+                                                const double *__restrict__ x, double *acc)
+{
+    if (c1 <= c0) return;  // uniform
+    if (__builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= c1 - c0)
+        return;
+    const int lane = threadIdx.x & 63;
+    int gi = 0;
+    long long nb = bnd[1];
+    auto claim = [&]() -> long long {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(ctr, U);
+        return c0 + __builtin_amdgcn_readfirstlane(v);
+    };
+    struct Ch {
+        v4u k;
+        v2d va, vb;
+        double vc;
+        uint32_t b[5];
+        int xo;
+    };
+    auto load = [&](long long cb, Ch *ch) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long c = cb + u;
+            const bool live = c < c1;
+            const long long ci = live ? c : c1 - 1;
+            const unsigned char *cp = base + ci * kK24Bytes;
+            const int l = live ? lane : 0;
+            ch[u].k = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(cp) + l);
+            ch[u].va = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cp + 1024) + l);
+            ch[u].vb = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cp + 2048) + l);
+            ch[u].vc = __builtin_nontemporal_load(reinterpret_cast<const double *>(cp + 3072) + l);
+            const uint32_t *h = reinterpret_cast<const uint32_t *>(cp + 3584);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) ch[u].b[j] = __builtin_amdgcn_readfirstlane(h[j]);
+            while (ci >= nb) nb = bnd[++gi + 1];
+            ch[u].xo = (gb + gi) * Wg;
+        }
+    };
+    auto keys = [&](const v4u &k, uint32_t *e) {
+        e[0] = k.x & kK24Mask;
+        e[1] = __builtin_amdgcn_alignbit(k.y, k.x, 24) & kK24Mask;
+        e[2] = __builtin_amdgcn_alignbit(k.z, k.y, 16) & kK24Mask;
+        e[3] = k.z >> 8;
+        e[4] = k.w & kK24Mask;
+    };
+    auto gather = [&](const Ch *ch, double (*xx)[5]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t e[5];
+            keys(ch[u].k, e);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int idx = e[j] == kK24Pad ? ch[u].xo : ch[u].xo + (int)ch[u].b[j] + (int)(e[j] >> kK24RowBits);
+                xx[u][j] = x[(kMode & 2) ? 0 : idx];
+            }
+        }
+    };
+    auto accumulate = [&](long long cb, const Ch *ch, double (*xx)[5]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool live = cb + u < c1;
+            uint32_t e[5];
+            keys(ch[u].k, e);
+            const double v[5] = {ch[u].va.x, ch[u].va.y, ch[u].vb.x, ch[u].vb.y, ch[u].vc};
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const double p = (live && e[j] != kK24Pad) ? v[j] * xx[u][j] : 0.0;
+                double *slot = &acc[e[j] & ((1u << kK24RowBits) - 1)];
+                if (kMode & 1) *slot = p;
+                else atomicAdd(slot, p);
+            }
+        }
+    };
+    Ch a[U], b[U];
+    double xa[U][5], xb[U][5];
+    long long ca = claim();
+    if (ca >= c1) return;
+    load(ca, a);
+    for (;;) {
+        gather(a, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        const long long cb = claim();
+        load(cb, b);
+        __builtin_amdgcn_sched_barrier(0);
+        accumulate(ca, a, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        if (cb >= c1) break;
+        gather(b, xb);
+        __builtin_amdgcn_sched_barrier(0);
+        ca = claim();
+        load(ca, a);
+        __builtin_amdgcn_sched_barrier(0);
+        accumulate(cb, b, xb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ca >= c1) break;
+    }
+}
+
 // Fused reduce of the wide ranges (replaces k_xsort_reduce when a.fused):
 // after its last item a workgroup claims reduce tasks (a wide range's rows
 // [r0, r0 + blockDim)) from a global head, waits until all 8 sub-items of
@@ -333,7 +452,7 @@ __device__ void xs_reduce_phase(const XsArgs &a, double alpha, double beta, doub
 // kDyn (pairs only): the chunks of both sub-items are claimed dynamically
 // (xs_stream_dyn); a team drains its own streams, then its partner's.
 template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false,
-          bool kDyn = false, int kU = kXsUnroll>
+          bool kDyn = false, int kU = kXsUnroll, bool kK24 = false>
 __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     const double *__restrict__ x,
                                                     double alpha, double beta,
@@ -464,8 +583,12 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                 if (hs < 0 || (seg && (hk1 || hg0 == 0))) continue;  // uniform
                 const long long *hb = s_bnd_all[h] + (seg ? 128 : 0);
                 const int hn = seg ? hg0 : hn1;
-                xs_stream_dyn<kMode, kU>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], hb[0], hb[hn], hb, seg ? 0 : hg0,
-                                     a.Wg, x, acc_all + h * kXsHalfRows);
+                if constexpr (kK24)
+                    xs_stream_dyn24<kMode, kU>(reinterpret_cast<const unsigned char *>(a.key), &s_ctr[h][seg], hb[0],
+                                               hb[hn], hb, seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
+                else
+                    xs_stream_dyn<kMode, kU>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], hb[0], hb[hn], hb,
+                                             seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
             }
         } else if (sub >= 0) {
             if (SA == SB || half == 0) {  // one inlined copy when the teams are equal
@@ -730,84 +853,154 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMemcpy(hval.data(), A.val, sizeof(double) * nnz, hipMemcpyDeviceToHost));
     }
 
-    // pass 1: entries per (range, group) -> whole chunks per block
-    std::vector<long long> cnt((size_t)I * G, 0);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int i = 0; i < I; ++i) {
-        long long *c = cnt.data() + (size_t)i * G;
-        for (int e = rp[ranges[i].row0]; e < rp[ranges[i].row0 + ranges[i].nrows]; ++e) {
-            const int col = hcol[e];
-            if (col >= 0 && col < n) ++c[col / Wg];
-        }
-    }
-    std::vector<long long> blk((size_t)I * G + 1, 0);  // chunk offsets
-    for (size_t k = 0; k < cnt.size(); ++k) blk[k + 1] = blk[k] + (cnt[k] + kXsChunk - 1) / kXsChunk;
-    const long long nchunks = blk.back();
-
-    // pass 2: fill each block, sort it by (column, row), pad it to whole
-    // chunks and store every chunk lane-transposed (header comment)
-    // one allocation: interleaved (default) = per chunk 1 KiB of keys then
-    // 2 KiB of values, so a chunk is ONE 3-KiB run in HBM; split
-    // (SBLAS_XS_KV=0) = all keys, then all values
-    const bool kv = !(getenv("SBLAS_XS_KV") && atoi(getenv("SBLAS_XS_KV")) == 0);
-    const size_t cbytes = (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
-    std::vector<unsigned char> hbuf((size_t)std::max<long long>(nchunks, 1) * cbytes);
-    auto chunk_keys = [&](long long c) {
-        return (uint32_t *)(hbuf.data() + (kv ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
-    };
-    auto chunk_vals = [&](long long c) {
-        return (double *)(hbuf.data() + (kv ? (size_t)c * cbytes + kXsChunk * sizeof(uint32_t)
-                                            : (size_t)std::max<long long>(nchunks, 1) * kXsChunk * sizeof(uint32_t) +
-                                                  (size_t)c * kXsChunk * sizeof(double)));
-    };
-    P.kstride = kv ? (int)(cbytes / 16) : kXsChunk * 4 / 16;
-    P.vstride = kv ? (int)(cbytes / 16) : kXsChunk * 8 / 16;
+    // pass 1: every block (range, group) bucketed and sorted by (column, row)
+    // once, kept for the fill (both key formats are sized from it)
+    const size_t nblk = (size_t)I * G;
+    std::vector<std::vector<std::pair<uint32_t, double>>> bk(nblk);
     bool bad = false;
-#pragma omp parallel
-    {
-        std::vector<std::vector<std::pair<uint32_t, double>>> bucket(G);
-#pragma omp for schedule(dynamic, 16) reduction(|| : bad)
-        for (int i = 0; i < I; ++i) {
-            const XsRange &R = ranges[i];
-            for (int g = 0; g < G; ++g) bucket[g].clear();
-            for (int r = R.row0; r < R.row0 + R.nrows; ++r) {
-                for (int e = rp[r]; e < rp[r + 1]; ++e) {
-                    const int c = hcol[e];
-                    if (c < 0 || c >= n) {
-                        bad = true;
-                        continue;
-                    }
-                    const int g = c / Wg;
-                    const uint32_t cp = (uint32_t)(c - g * Wg), lr = (uint32_t)(r - R.row0);
-                    if ((long long)cp >= wmax || lr >= (uint32_t)rows_cap) bad = true;
-                    bucket[g].push_back({(cp << kXsRowBits) | lr, hval[e]});
+#pragma omp parallel for schedule(dynamic, 16) reduction(|| : bad)
+    for (int i = 0; i < I; ++i) {
+        const XsRange &R = ranges[i];
+        for (int r = R.row0; r < R.row0 + R.nrows; ++r) {
+            for (int e = rp[r]; e < rp[r + 1]; ++e) {
+                const int c = hcol[e];
+                if (c < 0 || c >= n) {
+                    bad = true;
+                    continue;
                 }
+                const int g = c / Wg;
+                const uint32_t cp = (uint32_t)(c - g * Wg), lr = (uint32_t)(r - R.row0);
+                if ((long long)cp >= wmax || lr >= (uint32_t)rows_cap) bad = true;
+                bk[(size_t)i * G + g].push_back({(cp << kXsRowBits) | lr, hval[e]});
             }
-            for (int g = 0; g < G; ++g) {
-                auto &b = bucket[g];
-                if (!nosort)
-                    std::stable_sort(b.begin(), b.end(),
-                                     [](const std::pair<uint32_t, double> &u,
-                                        const std::pair<uint32_t, double> &v) { return u.first < v.first; });
-                const long long c0 = blk[(size_t)i * G + g], c1 = blk[(size_t)i * G + g + 1];
-                for (long long c = c0; c < c1; ++c) {
-                    uint32_t *kc = chunk_keys(c);
-                    double *vc = chunk_vals(c);
-                    for (int p = 0; p < kXsChunk; ++p) {
-                        const long long src = (c - c0) * kXsChunk + p;
-                        const bool in = src < (long long)b.size();
-                        const int l = p & 63, j = p >> 6;
-                        kc[4 * l + j] = in ? b[src].first : kXsPad;
-                        vc[(j < 2 ? 0 : 128) + 2 * l + (j & 1)] = in ? b[src].second : 0.0;
-                    }
-                }
-            }
+        }
+        for (int g = 0; g < G; ++g) {
+            auto &bb = bk[(size_t)i * G + g];
+            if (!nosort)
+                std::stable_sort(bb.begin(), bb.end(),
+                                 [](const std::pair<uint32_t, double> &u,
+                                    const std::pair<uint32_t, double> &v) { return u.first < v.first; });
         }
     }
     if (bad) {
         set_error("xsort: column index out of [0, n) or key overflow");
         return SBLAS_ERR_INVALID;
     }
+    // K24 sub-chunks of a block: <= 64 entries spanning <= kK24Span columns
+    auto k24_subs = [&](const std::vector<std::pair<uint32_t, double>> &bb, std::vector<int> *starts) {
+        long long subs = 0;
+        for (size_t i0 = 0; i0 < bb.size();) {
+            const uint32_t base = bb[i0].first >> kXsRowBits;
+            size_t j = i0;
+            while (j < bb.size() && j - i0 < 64 && (bb[j].first >> kXsRowBits) - base <= (uint32_t)kK24Span) ++j;
+            if (starts) starts->push_back((int)i0);
+            ++subs;
+            i0 = j;
+        }
+        return subs;
+    };
+    // format: K24 needs the paired dynamic kernel (8192-row teams) and wins
+    // when its chunks hold fewer bytes (dense-enough blocks); SBLAS_XS_K24=0/1
+    std::vector<long long> n32(nblk), n24(nblk);
+    long long b32 = 0, b24 = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : b32, b24)
+    for (long long k = 0; k < (long long)nblk; ++k) {
+        n32[(size_t)k] = ((long long)bk[(size_t)k].size() + kXsChunk - 1) / kXsChunk;
+        n24[(size_t)k] = (k24_subs(bk[(size_t)k], nullptr) + 4) / 5;
+        b32 += n32[(size_t)k] * (long long)kXsChunk * 12;
+        b24 += n24[(size_t)k] * (long long)kK24Bytes;
+    }
+    // opt-in: on config 2 K24 moves 7% fewer bytes but runs 144 us against
+    // 137.7 us (the header's scalar load sits on every claim's dependency
+    // chain, and one 320-entry chunk per claim -- two spill -- keeps fewer
+    // loads in flight than two 256-entry chunks); SBLAS_XS_K24=1 selects it
+    // (only where its chunks are smaller, unless forced with =2)
+    bool k24 = false;
+    if (const char *e = getenv("SBLAS_XS_K24"))
+        k24 = P.dyn && rows_cap <= (1 << kK24RowBits) && (atoi(e) == 2 || (atoi(e) == 1 && b24 < b32));
+    P.k24 = k24;
+    std::vector<long long> blk(nblk + 1, 0);  // chunk offsets
+    for (size_t k = 0; k < nblk; ++k) blk[k + 1] = blk[k] + (k24 ? n24[k] : n32[k]);
+    const long long nchunks = blk.back();
+
+    // pass 2: fill every chunk (lane-transposed, header comment / K24 notes)
+    // 32-bit keys, interleaved (default): per chunk 1 KiB of keys then 2 KiB
+    // of values, ONE 3-KiB run in HBM; split (SBLAS_XS_KV=0): all keys, then
+    // all values.  K24: 3616-B chunks, keys | values | header.
+    const bool kv = !(getenv("SBLAS_XS_KV") && atoi(getenv("SBLAS_XS_KV")) == 0);
+    const size_t cbytes = k24 ? (size_t)kK24Bytes : (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
+    std::vector<unsigned char> hbuf((size_t)std::max<long long>(nchunks, 1) * cbytes);
+    auto chunk_keys = [&](long long c) {
+        return (uint32_t *)(hbuf.data() + ((kv || k24) ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
+    };
+    auto chunk_vals = [&](long long c) {
+        return (double *)(hbuf.data() + ((kv || k24) ? (size_t)c * cbytes + (k24 ? 1024 : kXsChunk * sizeof(uint32_t))
+                                                     : (size_t)std::max<long long>(nchunks, 1) * kXsChunk * sizeof(uint32_t) +
+                                                           (size_t)c * kXsChunk * sizeof(double)));
+    };
+    P.kstride = k24 ? kK24Bytes / 16 : kv ? (int)(cbytes / 16) : kXsChunk * 4 / 16;
+    P.vstride = k24 ? kK24Bytes / 16 : kv ? (int)(cbytes / 16) : kXsChunk * 8 / 16;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long long k = 0; k < (long long)nblk; ++k) {
+        const auto &bb = bk[(size_t)k];
+        const long long c0 = blk[(size_t)k], c1 = blk[(size_t)k + 1];
+        if (!k24) {
+            for (long long c = c0; c < c1; ++c) {
+                uint32_t *kc = chunk_keys(c);
+                double *vc = chunk_vals(c);
+                for (int p = 0; p < kXsChunk; ++p) {
+                    const long long src = (c - c0) * kXsChunk + p;
+                    const bool in = src < (long long)bb.size();
+                    const int l = p & 63, j = p >> 6;
+                    kc[4 * l + j] = in ? bb[src].first : kXsPad;
+                    vc[(j < 2 ? 0 : 128) + 2 * l + (j & 1)] = in ? bb[src].second : 0.0;
+                }
+            }
+            continue;
+        }
+        std::vector<int> starts;
+        k24_subs(bb, &starts);
+        starts.push_back((int)bb.size());
+        const long long nsub = (long long)starts.size() - 1;
+        for (long long c = c0; c < c1; ++c) {
+            unsigned char *cp = hbuf.data() + (size_t)c * cbytes;
+            uint32_t *kw = (uint32_t *)cp;          // 64 lanes x 4 words
+            double *vw = (double *)(cp + 1024);     // 320 values
+            uint32_t *hd = (uint32_t *)(cp + 3584); // 8 words
+            std::memset(cp, 0, cbytes);
+            for (int sb = 0; sb < 5; ++sb) {
+                const long long si = (c - c0) * 5 + sb;
+                uint32_t base = 0;
+                int a0 = 0, a1 = 0;
+                if (si < nsub) {
+                    a0 = starts[(size_t)si];
+                    a1 = starts[(size_t)si + 1];
+                    base = bb[(size_t)a0].first >> kXsRowBits;
+                }
+                hd[sb] = base;
+                for (int l = 0; l < 64; ++l) {
+                    const int src = a0 + l;
+                    uint32_t key = kK24Pad;
+                    double v = 0.0;
+                    if (src < a1) {
+                        const uint32_t col = bb[(size_t)src].first >> kXsRowBits;
+                        const uint32_t row = bb[(size_t)src].first & ((1u << kXsRowBits) - 1);
+                        key = ((col - base) << kK24RowBits) | row;
+                        v = bb[(size_t)src].second;
+                    }
+                    // lane l's 120 key bits: slot sb at bit 24*sb
+                    const int bit = 24 * sb, w = bit >> 5, o = bit & 31;
+                    kw[4 * l + w] |= key << o;
+                    if (o > 8) kw[4 * l + w + 1] |= key >> (32 - o);
+                    // values: slots 0,1 -> {l, 64+l} pair, 2,3 -> second pair, 4 -> single
+                    if (sb < 2) vw[2 * l + sb] = v;
+                    else if (sb < 4) vw[128 + 2 * l + (sb - 2)] = v;
+                    else vw[256 + l] = v;
+                }
+            }
+        }
+    }
+    { std::vector<std::vector<std::pair<uint32_t, double>>>().swap(bk); }
 
     // sub-items, wide partial slots, then items (pairs) in XCD queues
     std::vector<int> wide, nsub;
@@ -1027,9 +1220,24 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else kern = mm == 4 ? XS_DYN(4, 2) : XS_DYN(6, 2);
 #undef XS_DYN
     }
+    if (P.k24) {  // 24-bit keys: the paired dynamic kernel only (planner)
+#define XS_K24(M, U) k_spmv_xsort<true, M, W, true, 8, false, true, U, true>
+        const int mm = mode & 2;
+        // one 320-entry chunk per claim by default (U = 2 spills at the
+        // 128-VGPR cap of 16 waves per CU); SBLAS_XS_U=2 for experiments
+        const char *ue = getenv("SBLAS_XS_U");
+        const int u24 = ue ? atoi(ue) : 1;
+        if (!b) kern = k_spmv_xsort<false, 0, W, true, 8, false, true, 1, true>;
+        else if (u24 == 2) kern = mm ? XS_K24(2, 2) : XS_K24(0, 2);
+        else kern = mm ? XS_K24(2, 1) : XS_K24(0, 1);
+#undef XS_K24
+    }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
     if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
         if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
+        else if (P.pair && P.dyn && P.k24)
+            kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1, true>
+                     : k_spmv_xsort<false, 0, W, true, 8, true, true, 1, true>;
         else if (P.pair && P.dyn) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true> : k_spmv_xsort<false, 0, W, true, 8, true, true>;
         else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;

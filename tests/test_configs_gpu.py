@@ -74,8 +74,10 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
 
 @pytest.mark.parametrize("algo,env", [
     (1, {}), (2, {}), (3, {}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
-    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"})],
-    ids=["rowsplit", "csr5", "csr5_alt", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused"])
+    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_K24": "0"}),
+    (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2"})],
+    ids=["rowsplit", "csr5", "csr5_alt", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused",
+         "xsort_k32", "xsort_k24_u2"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
     for k, v in env.items():

@@ -31,10 +31,14 @@ ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANE
          (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_Q": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_Q": "3"}),
          (5, {"SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_FUSE": "1", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"})]
+         (5, {"SBLAS_XS_FUSE": "1", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_K24": "2"}), (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K24": "0"})]
 ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
-            "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50"]
+            "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
+            "xsort_k24", "xsort_k24_w50", "xsort_k24_q3_w50", "xsort_k24_u2_w50", "xsort_k32"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
@@ -157,7 +161,8 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
 
 
 @pytest.mark.parametrize("env", [{}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"},
-                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}])
+                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"},
+                                 {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}])
 def test_xsort_relaunch(torch_cuda, sb, orc, monkeypatch, env):
     """The column-sorted kernel's work queues re-arm themselves at the end of
     each launch (no memset): five launches on one plan, each checked."""
