@@ -537,8 +537,34 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
                 kv[(size_t)next[(size_t)bucket(r, c)]++] = ((unsigned long long)kk << 32) | (unsigned)e;
             }
     }
+    // LDS banks: the entries 2g and 2g+1 of a kernel step share one 16-lane
+    // group of the ds_add_f64 (b64: 32 banks of dwords); with the 17-double
+    // row stride their dwords are disjoint exactly when the two rows differ
+    // in parity.  So inside each aligned 8-entry step, odd rows go to the even
+    // slots and even rows to the odd slots as far as the step allows (the
+    // order inside a step does not change which products are summed).
+    const bool pair_rows = !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int b = 0; b < nbk; ++b) std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
+    for (int b = 0; b < nbk; ++b) {
+        std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
+        if (!pair_rows) continue;
+        const unsigned rm = (1u << rbits) - 1;
+        for (long long w = off[(size_t)b]; w + 8 <= off[(size_t)b + 1]; w += 8) {
+            unsigned long long odd[8], even[8];
+            int no = 0, ne = 0;
+            for (int i = 0; i < 8; ++i) {
+                const unsigned long long e = kv[(size_t)(w + i)];
+                if (((unsigned)(e >> 32) & rm) & 1u) odd[no++] = e;
+                else even[ne++] = e;
+            }
+            int io = 0, ie = 0;
+            for (int i = 0; i < 8; ++i) {  // even slot: odd row first; odd slot: even row first
+                const bool want_odd = (i & 1) == 0;
+                if ((want_odd && io < no) || (!want_odd && ie >= ne)) kv[(size_t)(w + i)] = odd[io++];
+                else kv[(size_t)(w + i)] = even[ie++];
+            }
+        }
+    }
     std::vector<unsigned> hkey((size_t)std::max<long long>(A.nnz, 1));
     std::vector<double> hv((size_t)std::max<long long>(A.nnz, 1));
 #pragma omp parallel for schedule(static)
