@@ -125,6 +125,9 @@ struct SpmmPlan {
     // writes it to its (XCD, set) partial; a reduce adds the partials.
     int ct_ns = 0, ct_nrb = 0, ct_R = 0, ct_rbits = 0, ct_wlog = 0;
     bool ct_direct = false;              // keys hold the global column
+    bool ct_slots = false;               // units are column-run slots of <= 2 entries
+    unsigned *ct_key2 = nullptr;         // slots: second entry's local row, ~0 if none
+    double *ct_val2 = nullptr;
     unsigned *ct_key = nullptr;
     double *ct_val = nullptr;
     long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets

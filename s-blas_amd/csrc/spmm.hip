@@ -376,9 +376,15 @@ __device__ __forceinline__ unsigned ct_bcast(unsigned v)
 // guards and scalar loads.  Full 64-entry iterations run without checks;
 // the one partial iteration per item routes dead lanes' +0.0 into the row's
 // padding column.
-template <bool kDirect, bool kFast>
+// kSlots: the item's units are column-run SLOTS of up to two entries of one
+// column (key2 = second row or ~0, val2 its value): one B segment feeds both,
+// so ~41% fewer B bytes cross L1 -> lanes on rail4284 (runs average 2.7
+// entries per tile); a single-entry slot's second adds go to the padding
+// column.
+template <bool kDirect, bool kFast, bool kSlots>
 __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     const unsigned *__restrict__ key, const double *__restrict__ val,
+    const unsigned *__restrict__ key2, const double *__restrict__ val2,
     const long long *__restrict__ off, int ns, int nrb, int R, int rbits, int wlog, int ncg,
     const double *__restrict__ B, long long ldb, int n, int m, double *__restrict__ part)
 {
@@ -449,6 +455,30 @@ __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
                 const bool ok = it + 8 * t + mypos < e1;
                 atomicAdd(row_p + ((ok && live0) ? 2 * q : kCtCols), (ok && live0) ? vt * b0[t] : 0.0);
                 atomicAdd(row_p + ((ok && live1) ? 2 * q + 1 : kCtCols), (ok && live1) ? vt * b1[t] : 0.0);
+            }
+        }
+        if constexpr (kSlots) {  // the slots' second entries (same B segments)
+            const unsigned k2 = key2[ec];
+            const unsigned long long wb = (unsigned long long)__double_as_longlong(val2[ec]);
+            const unsigned wlo = (unsigned)wb, whi = (unsigned)(wb >> 32);
+            unsigned r2[8];
+            r2[0] = ct_bcast<0>(k2); r2[1] = ct_bcast<1>(k2); r2[2] = ct_bcast<2>(k2); r2[3] = ct_bcast<3>(k2);
+            r2[4] = ct_bcast<4>(k2); r2[5] = ct_bcast<5>(k2); r2[6] = ct_bcast<6>(k2); r2[7] = ct_bcast<7>(k2);
+            lo[0] = ct_bcast<0>(wlo); lo[1] = ct_bcast<1>(wlo); lo[2] = ct_bcast<2>(wlo); lo[3] = ct_bcast<3>(wlo);
+            lo[4] = ct_bcast<4>(wlo); lo[5] = ct_bcast<5>(wlo); lo[6] = ct_bcast<6>(wlo); lo[7] = ct_bcast<7>(wlo);
+            hi[0] = ct_bcast<0>(whi); hi[1] = ct_bcast<1>(whi); hi[2] = ct_bcast<2>(whi); hi[3] = ct_bcast<3>(whi);
+            hi[4] = ct_bcast<4>(whi); hi[5] = ct_bcast<5>(whi); hi[6] = ct_bcast<6>(whi); hi[7] = ct_bcast<7>(whi);
+            // predicated, not routed to the padding column: the 8 lanes of a
+            // single-entry slot would all hit ONE address there, and
+            // same-address LDS atomics serialise (measured 4x slower).  Every
+            // row broadcast above already ran with all lanes active.
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const double vt = __longlong_as_double((long long)(((unsigned long long)hi[t] << 32) | lo[t]));
+                const bool has2 = r2[t] != ~0u && (!tail || it + 8 * t + mypos < e1);
+                double *row_p = &tile[(r2[t] & rmask) * kCtPad];
+                if (has2 && live0) atomicAdd(row_p + 2 * q, vt * b0[t]);
+                if (has2 && live1) atomicAdd(row_p + 2 * q + 1, vt * b1[t]);
             }
         }
     };
@@ -565,13 +595,92 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
             }
         }
     }
-    std::vector<unsigned> hkey((size_t)std::max<long long>(A.nnz, 1));
-    std::vector<double> hv((size_t)std::max<long long>(A.nnz, 1));
-#pragma omp parallel for schedule(static)
-    for (long long e = 0; e < A.nnz; ++e) {
-        hkey[(size_t)e] = (unsigned)(kv[(size_t)e] >> 32);
-        hv[(size_t)e] = hval[(size_t)(kv[(size_t)e] & 0xffffffffu)];
+    // Column-run slots (opt-in, SBLAS_SPMM_CTSLOT=1): consecutive entries of
+    // one column are paired into slots of two so one B segment feeds both
+    // (rail4284: 0.59 slots per entry).  Measured slower on config 4: 0.435
+    // against 0.362 ms -- L2 misses 10.0M against 6.0M per launch and more TD
+    // stall cycles (the second key/value arrays), so entries stay the unit.
+    std::vector<long long> soff((size_t)nbk + 1, 0);
+    for (int b = 0; b < nbk; ++b) {
+        long long ns_b = 0;
+        for (long long e = off[(size_t)b]; e < off[(size_t)b + 1];) {
+            long long f = e;
+            const unsigned col = (unsigned)(kv[(size_t)e] >> 32) >> rbits;
+            while (f < off[(size_t)b + 1] && ((unsigned)(kv[(size_t)f] >> 32) >> rbits) == col) ++f;
+            ns_b += (f - e + 1) / 2;
+            e = f;
+        }
+        soff[(size_t)b + 1] = soff[(size_t)b] + ns_b;
     }
+    bool slots = false;
+    if (const char *e = getenv("SBLAS_SPMM_CTSLOT")) slots = atoi(e) != 0 && A.nnz > 0;
+    const long long nunits = slots ? soff.back() : A.nnz;
+    std::vector<unsigned> hkey((size_t)std::max<long long>(nunits, 1)), hkey2;
+    std::vector<double> hv((size_t)std::max<long long>(nunits, 1)), hv2;
+    if (!slots) {
+#pragma omp parallel for schedule(static)
+        for (long long e = 0; e < A.nnz; ++e) {
+            hkey[(size_t)e] = (unsigned)(kv[(size_t)e] >> 32);
+            hv[(size_t)e] = hval[(size_t)(kv[(size_t)e] & 0xffffffffu)];
+        }
+    } else {
+        hkey2.assign(hkey.size(), ~0u);
+        hv2.assign(hv.size(), 0.0);
+        const unsigned rm = (1u << rbits) - 1;
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int b = 0; b < nbk; ++b) {
+            // entries were parity-shuffled inside steps above: re-sort the
+            // bucket so runs are contiguous, then pair each run's rows
+            std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
+            long long o = soff[(size_t)b];
+            for (long long e = off[(size_t)b]; e < off[(size_t)b + 1];) {
+                long long f = e;
+                const unsigned col = (unsigned)(kv[(size_t)e] >> 32) >> rbits;
+                while (f < off[(size_t)b + 1] && ((unsigned)(kv[(size_t)f] >> 32) >> rbits) == col) ++f;
+                for (long long i = e; i < f; i += 2, ++o) {
+                    hkey[(size_t)o] = (unsigned)(kv[(size_t)i] >> 32);
+                    hv[(size_t)o] = hval[(size_t)(kv[(size_t)i] & 0xffffffffu)];
+                    if (i + 1 < f) {
+                        hkey2[(size_t)o] = (unsigned)(kv[(size_t)i + 1] >> 32) & rm;
+                        hv2[(size_t)o] = hval[(size_t)(kv[(size_t)i + 1] & 0xffffffffu)];
+                    }
+                }
+                e = f;
+            }
+            // LDS banks: opposite-parity first rows in each 16-lane pair of a step
+            if (!pair_rows) continue;
+            for (long long w = soff[(size_t)b]; w + 8 <= soff[(size_t)b + 1]; w += 8) {
+                int odd[8], even[8], no = 0, ne = 0;
+                for (int i = 0; i < 8; ++i) {
+                    if ((hkey[(size_t)(w + i)] & rm) & 1u) odd[no++] = i;
+                    else even[ne++] = i;
+                }
+                unsigned tk[8], tk2[8];
+                double tv[8], tv2[8];
+                int io = 0, ie = 0;
+                for (int i = 0; i < 8; ++i) {
+                    const bool want_odd = (i & 1) == 0;
+                    const int src = ((want_odd && io < no) || (!want_odd && ie >= ne)) ? odd[io++] : even[ie++];
+                    tk[i] = hkey[(size_t)(w + src)];
+                    tk2[i] = hkey2[(size_t)(w + src)];
+                    tv[i] = hv[(size_t)(w + src)];
+                    tv2[i] = hv2[(size_t)(w + src)];
+                }
+                for (int i = 0; i < 8; ++i) {
+                    hkey[(size_t)(w + i)] = tk[i];
+                    hkey2[(size_t)(w + i)] = tk2[i];
+                    hv[(size_t)(w + i)] = tv[i];
+                    hv2[(size_t)(w + i)] = tv2[i];
+                }
+            }
+        }
+        off = soff;
+        SBLAS_HIP(hipMalloc(&P.ct_key2, sizeof(unsigned) * hkey2.size()));
+        SBLAS_HIP(hipMalloc(&P.ct_val2, sizeof(double) * hv2.size()));
+        SBLAS_HIP(hipMemcpy(P.ct_key2, hkey2.data(), sizeof(unsigned) * hkey2.size(), hipMemcpyHostToDevice));
+        SBLAS_HIP(hipMemcpy(P.ct_val2, hv2.data(), sizeof(double) * hv2.size(), hipMemcpyHostToDevice));
+    }
+    P.ct_slots = slots;
     SBLAS_HIP(hipMalloc(&P.ct_key, sizeof(unsigned) * hkey.size()));
     SBLAS_HIP(hipMalloc(&P.ct_val, sizeof(double) * hv.size()));
     SBLAS_HIP(hipMalloc(&P.ct_off, sizeof(long long) * off.size()));
@@ -683,6 +792,8 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.ct_key);
     (void)hipFree(P.ct_val);
     (void)hipFree(P.ct_off);
+    (void)hipFree(P.ct_key2);
+    (void)hipFree(P.ct_val2);
     A.mm = SpmmPlan{};
 }
 
@@ -752,8 +863,11 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         const size_t lds = sizeof(double) * (size_t)P.ct_R * kCtPad;
         static thread_local bool attr_set[64] = {};
         if (!attr_set[A.device & 63]) {  // > 64 KiB of dynamic LDS
-            const void *ks[4] = {(const void *)k_spmm_ctile<true, false>, (const void *)k_spmm_ctile<true, true>,
-                                 (const void *)k_spmm_ctile<false, false>, (const void *)k_spmm_ctile<false, true>};
+            const void *ks[8] = {
+                (const void *)k_spmm_ctile<true, false, false>, (const void *)k_spmm_ctile<true, true, false>,
+                (const void *)k_spmm_ctile<false, false, false>, (const void *)k_spmm_ctile<false, true, false>,
+                (const void *)k_spmm_ctile<true, false, true>, (const void *)k_spmm_ctile<true, true, true>,
+                (const void *)k_spmm_ctile<false, false, true>, (const void *)k_spmm_ctile<false, true, true>};
             for (const void *kf : ks)
                 SBLAS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)(sizeof(double) * kCtMaxRows * kCtPad)));
@@ -761,12 +875,18 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         }
         const bool fast = (ldr % 2 == 0) && (n % kCtCols == 0) && (((uintptr_t)Brow & 15) == 0) &&
                           (unsigned long long)A.n * (unsigned long long)ldr * 8ULL < (1ULL << 32);
-        using K = void (*)(const unsigned *, const double *, const long long *, int, int, int, int, int, int,
-                           const double *, long long, int, int, double *);
-        K kern = P.ct_direct ? (fast ? k_spmm_ctile<true, true> : k_spmm_ctile<true, false>)
-                             : (fast ? k_spmm_ctile<false, true> : k_spmm_ctile<false, false>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_off,
-                           P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr, n, A.m, S.bt);
+        using K = void (*)(const unsigned *, const double *, const unsigned *, const double *, const long long *,
+                           int, int, int, int, int, int, const double *, long long, int, int, double *);
+        K kern;
+        if (P.ct_slots)
+            kern = P.ct_direct ? (fast ? k_spmm_ctile<true, true, true> : k_spmm_ctile<true, false, true>)
+                               : (fast ? k_spmm_ctile<false, true, true> : k_spmm_ctile<false, false, true>);
+        else
+            kern = P.ct_direct ? (fast ? k_spmm_ctile<true, true, false> : k_spmm_ctile<true, false, false>)
+                               : (fast ? k_spmm_ctile<false, true, false> : k_spmm_ctile<false, false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_key2,
+                           P.ct_val2, P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr,
+                           n, A.m, S.bt);
         const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
         if (beta != 0.0)
             hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,

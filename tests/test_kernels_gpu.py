@@ -33,7 +33,7 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows", "ctslab"])
+@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows", "ctslab", "ctslot"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
@@ -55,6 +55,8 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
         monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
         if splitk == "ctslab":  # XCD-local slab keys instead of global columns
             monkeypatch.setenv("SBLAS_SPMM_CTDIRECT", "0")
+        if splitk == "ctslot":  # column-run slots of two entries (opt-in form)
+            monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
         if splitk == "ctw":
             monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
             monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
