@@ -287,13 +287,35 @@ def main() -> int:
         # same command reads ~12 us less than unpadded events did).
         # The host wall clock around each cold step is measured in a second,
         # spin-free pass and kept beside (wall_el).
+        # At N = 1 the step is the SpMV call alone (no exchange): its device
+        # span is read from events the runtime stamps at the call's first
+        # kernel start and last kernel end (sblas_spmv_timed), which excludes
+        # the remaining dispatch / event-record gaps of stream events
+        # (~5 us on config 2; rocprofv3's kernel trace agrees with the span).
         evs = events()
+        span_ms = []
         for k in range(args.steps):
             evict()  # 1 GiB sweep: evicts MALL (256 MB) and L2
             sync_barrier()
-            torch.cuda._sleep(500_000)
-            step(evs[k])
+            if world == 1 and op.dm > 0:
+                span_ms.append(op.A.spmv_timed(op.algo, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp))
+            else:
+                torch.cuda._sleep(500_000)
+                step(evs[k])
             sync_barrier()
+        if span_ms:
+            run_cold.wall_el = 0.0
+            run_cold.xch = 0.0
+            wall_el = 0.0
+            for k in range(args.steps):
+                evict()
+                sync_barrier()
+                t0 = time.perf_counter()
+                step()
+                sync_barrier()
+                wall_el += time.perf_counter() - t0
+            run_cold.wall_el = wall_el
+            return float(np.sum(span_ms)) * 1e-3, float(np.mean(span_ms))
         wall_el = 0.0
         for k in range(args.steps):
             evict()
@@ -332,14 +354,9 @@ def main() -> int:
             for _ in range(args.steps):
                 evict()
                 torch.cuda.synchronize()
-                torch.cuda._sleep(500_000)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                op.A.spmv(sblas.ROWSPLIT, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp)
-                e1.record(stream)
-                rs.append((e0, e1))
+                rs.append(op.A.spmv_timed(sblas.ROWSPLIT, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp))
             torch.cuda.synchronize()
-        rk = float(np.mean([a.elapsed_time(b) for a, b in rs]))
+        rk = float(np.mean(rs))
         rowsplit_beside = {"kernel_ms": round(rk, 5),
                            "gflops": round(2.0 * nnz / (rk * 1e-3) / 1e9, 3),
                            "roofline_frac": round(local_bytes / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -430,8 +447,11 @@ def main() -> int:
                      "device_bytes_rank0": int(op.A.plan_bytes(algo)),
                      "csr_device_bytes_rank0": int(12 * local_nnz + 4 * (op.A.info()[0] + 1))},
             "exchange_ms_max_over_ranks": round(xch_max, 5),
-            "timing": ("cold steps: device time, HIP events on the launch stream from before the "
-                       "kernel to after exchange + merge, max over ranks; host wall clock beside"
+            "timing": (("cold steps: device span of the SpMV call (events stamped by the runtime at "
+                        "its first kernel's start and last kernel's end, sblas_spmv_timed); host wall "
+                        "clock beside" if world == 1 else
+                        "cold steps: device time, HIP events on the launch stream from before the "
+                        "kernel to after exchange + merge, max over ranks; host wall clock beside")
                        if args.cache == "cold" else "warm: host wall clock over K back-to-back steps"),
             "cache": args.cache,
             "scrub": args.scrub,

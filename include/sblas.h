@@ -142,6 +142,12 @@ int sblas_csr_analyse(sblas_csr A, int algo, void *stream);
  * (even of the same matrix) are independent. */
 int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x,
                double beta, double *d_y, void *stream);
+/* sblas_spmv that also measures the call's device span: ms = time from the
+ * first kernel's start to the last kernel's end (events stamped by the
+ * runtime at the kernels themselves, hipExtLaunchKernelGGL), excluding the
+ * host's launch latency and event-record gaps.  Waits for the call. */
+int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
+                     double beta, double *d_y, void *stream, float *ms);
 /* Device bytes held by the analysis of `algo` (free memory before - after
  * sblas_csr_analyse; 0 if not analysed): the layout's cost beside the CSR. */
 long long sblas_csr_plan_bytes(sblas_csr A, int algo);

@@ -34,6 +34,14 @@ static int alloc_padded(sblas_csr_s &A, long long nnz)
 
 using namespace sblas;
 
+namespace sblas {
+LaunchTimer &launch_timer()
+{
+    static thread_local LaunchTimer t;
+    return t;
+}
+}  // namespace sblas
+
 extern "C" {
 
 const char *sblas_status_string(int s)
@@ -233,6 +241,55 @@ int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x, double be
         return launch_spmv_xsort(*A, alpha, d_x, beta, d_y, s);
     default: return SBLAS_ERR_INVALID;
     }
+}
+
+// y = alpha*A*x + beta*y with the call's device span measured: every kernel
+// of the call goes through hipExtLaunchKernelGGL with events stamped at the
+// first kernel's start and at the last kernel's end (SBLAS_LAUNCH), then the
+// call waits for the stop event.  ms = 0 when the call launches nothing.
+int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x, double beta, double *d_y,
+                     void *stream, float *ms)
+{
+    if (!A || !ms) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    // build any plan first, untimed (the plan build launches its own kernels)
+    hipStream_t s = (hipStream_t)stream;
+    switch (algo) {
+    case SBLAS_SPMV_ROWSPLIT: if (!A->rs.ready) SBLAS_TRY(build_rowsplit_plan(*A, s)); break;
+    case SBLAS_SPMV_CSR5:
+    case SBLAS_SPMV_CSR5_ALT: if (!A->c5.ready) SBLAS_TRY(build_csr5_plan(*A, s)); break;
+    case SBLAS_SPMV_PANEL: if (!A->pn.ready) SBLAS_TRY(build_panel_plan(*A, s)); break;
+    case SBLAS_SPMV_XSORT: if (!A->xs.ready) SBLAS_TRY(build_xsort_plan(*A, s)); break;
+    default: return SBLAS_ERR_INVALID;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    SBLAS_HIP(hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        set_error("sblas_spmv_timed: hipEventCreate failed");
+        return SBLAS_ERR_HIP;
+    }
+    LaunchTimer &lt = launch_timer();
+    lt.start = e0;
+    lt.stop = e1;
+    lt.pending_start = true;
+    int rc = sblas_spmv(A, algo, alpha, d_x, beta, d_y, stream);
+    const bool launched = !lt.pending_start;
+    lt = LaunchTimer{};
+    *ms = 0.0f;
+    hipError_t e = hipSuccess;
+    if (rc == SBLAS_OK && launched) {
+        e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc != SBLAS_OK) return rc;
+    if (e != hipSuccess) {
+        set_error("sblas_spmv_timed: %s", hipGetErrorString(e));
+        return SBLAS_ERR_HIP;
+    }
+    return SBLAS_OK;
 }
 
 // Compulsory traffic: each array touched once.

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -13,6 +14,28 @@
 namespace sblas {
 
 void set_error(const char *fmt, ...);
+
+// Kernel-span timing of one library call (sblas_spmv_timed): while `stop` is
+// set, SBLAS_LAUNCH launches through hipExtLaunchKernelGGL so the runtime
+// stamps `start` as the call's FIRST kernel begins and `stop` as each kernel
+// ends (the last one wins): the call's device span without the dispatch and
+// event-record gaps that stream events around the call include.
+struct LaunchTimer {
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool pending_start = false;
+};
+LaunchTimer &launch_timer();
+#define SBLAS_LAUNCH(kern, grid, block, shmem, stream, ...)                                        \
+    do {                                                                                          \
+        ::sblas::LaunchTimer &lt_ = ::sblas::launch_timer();                                      \
+        if (lt_.stop) {                                                                           \
+            hipExtLaunchKernelGGL(kern, grid, block, shmem, stream,                              \
+                                  lt_.pending_start ? lt_.start : nullptr, lt_.stop, 0, __VA_ARGS__); \
+            lt_.pending_start = false;                                                            \
+        } else {                                                                                  \
+            hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                    \
+        }                                                                                         \
+    } while (0)
 
 #define SBLAS_HIP(expr)                                                        \
     do {                                                                       \

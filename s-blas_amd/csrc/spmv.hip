@@ -245,16 +245,16 @@ int launch_rowsplit_raw(const int *rowptr, const int *col, const double *val, co
 {
     if (nblocks == 0) return SBLAS_OK;
     if (beta != 0.0) {
-        hipLaunchKernelGGL(k_spmv_rowsplit<true>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
+        SBLAS_LAUNCH(k_spmv_rowsplit<true>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
                            x, blocks, alpha, beta, y, partial);
         if (nlong)
-            hipLaunchKernelGGL(k_spmv_long_finalize<true>, dim3((nlong + 63) / 64), dim3(64), 0, s,
+            SBLAS_LAUNCH(k_spmv_long_finalize<true>, dim3((nlong + 63) / 64), dim3(64), 0, s,
                                long_rows, nlong, partial, alpha, beta, y);
     } else {
-        hipLaunchKernelGGL(k_spmv_rowsplit<false>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
+        SBLAS_LAUNCH(k_spmv_rowsplit<false>, dim3(nblocks), dim3(kRsThreads), 0, s, rowptr, col, val,
                            x, blocks, alpha, beta, y, partial);
         if (nlong)
-            hipLaunchKernelGGL(k_spmv_long_finalize<false>, dim3((nlong + 63) / 64), dim3(64), 0, s,
+            SBLAS_LAUNCH(k_spmv_long_finalize<false>, dim3((nlong + 63) / 64), dim3(64), 0, s,
                                long_rows, nlong, partial, alpha, beta, y);
     }
     SBLAS_HIP(hipGetLastError());
@@ -267,16 +267,16 @@ int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
     if (!A.rs.ready) return SBLAS_ERR_INVALID;
     if (A.rs.nblocks == 0) return SBLAS_OK;
     if (beta != 0.0) {
-        hipLaunchKernelGGL(k_spmv_rowsplit<true>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+        SBLAS_LAUNCH(k_spmv_rowsplit<true>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
                            A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
         if (A.rs.nlong)
-            hipLaunchKernelGGL(k_spmv_long_finalize<true>, dim3((A.rs.nlong + 63) / 64), dim3(64),
+            SBLAS_LAUNCH(k_spmv_long_finalize<true>, dim3((A.rs.nlong + 63) / 64), dim3(64),
                                0, s, A.rs.long_rows, A.rs.nlong, A.rs.partial, alpha, beta, y);
     } else {
-        hipLaunchKernelGGL(k_spmv_rowsplit<false>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+        SBLAS_LAUNCH(k_spmv_rowsplit<false>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
                            A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
         if (A.rs.nlong)
-            hipLaunchKernelGGL(k_spmv_long_finalize<false>, dim3((A.rs.nlong + 63) / 64), dim3(64),
+            SBLAS_LAUNCH(k_spmv_long_finalize<false>, dim3((A.rs.nlong + 63) / 64), dim3(64),
                                0, s, A.rs.long_rows, A.rs.nlong, A.rs.partial, alpha, beta, y);
     }
     SBLAS_HIP(hipGetLastError());
@@ -513,22 +513,22 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
         if (beta != 0.0)
-            hipLaunchKernelGGL(k_spmv_csr5<true>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
+            SBLAS_LAUNCH(k_spmv_csr5<true>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
                                P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
                                beta, y, P.carry);
         else
-            hipLaunchKernelGGL(k_spmv_csr5<false>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
+            SBLAS_LAUNCH(k_spmv_csr5<false>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
                                P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
                                beta, y, P.carry);
-        hipLaunchKernelGGL(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
+        SBLAS_LAUNCH(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
                            0, s, P.tile_row, P.flags, P.carry, P.ntiles, alpha, y);
     }
     if (P.nempty) {
         if (beta != 0.0)
-            hipLaunchKernelGGL(k_empty_rows<true>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
+            SBLAS_LAUNCH(k_empty_rows<true>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
                                P.empty_rows, P.nempty, beta, y);
         else
-            hipLaunchKernelGGL(k_empty_rows<false>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
+            SBLAS_LAUNCH(k_empty_rows<false>, dim3((P.nempty + 255) / 256), dim3(256), 0, s,
                                P.empty_rows, P.nempty, beta, y);
     }
     SBLAS_HIP(hipGetLastError());
@@ -741,21 +741,21 @@ int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x, doubl
     }();
     if (grid > 0) {
         if (sc1)
-            hipLaunchKernelGGL(k_spmv_panel<true>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
+            SBLAS_LAUNCH(k_spmv_panel<true>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
                                Q.desc, Q.P, x, alpha);
         else
-            hipLaunchKernelGGL(k_spmv_panel<false>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
+            SBLAS_LAUNCH(k_spmv_panel<false>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,
                                Q.desc, Q.P, x, alpha);
     }
     if (Q.nlong)
-        hipLaunchKernelGGL(k_panel_long_finalize, dim3((Q.nlong + 63) / 64), dim3(64), 0, s,
+        SBLAS_LAUNCH(k_panel_long_finalize, dim3((Q.nlong + 63) / 64), dim3(64), 0, s,
                            Q.long_rows, Q.nlong, Q.partial, alpha, Q.ypart, (long long)A.m);
     const unsigned rb = (unsigned)((A.m + 255) / 256);
     if (beta != 0.0)
-        hipLaunchKernelGGL(k_panel_reduce<true>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
+        SBLAS_LAUNCH(k_panel_reduce<true>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
                            (long long)A.m, beta, y);
     else
-        hipLaunchKernelGGL(k_panel_reduce<false>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
+        SBLAS_LAUNCH(k_panel_reduce<false>, dim3(rb), dim3(256), 0, s, Q.ypart, Q.P,
                            (long long)A.m, beta, y);
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;

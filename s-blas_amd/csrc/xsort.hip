@@ -1249,7 +1249,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         SBLAS_HIP(hipMemsetAsync(a.trace, 0, sizeof(long long) * len, s));
         htrace.resize(len);
     }
-    hipLaunchKernelGGL(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
+    SBLAS_LAUNCH(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
     if (trace_path) {  // debugging aid: rows {subA, subB, block<<4|xcc, t0, endA, endB}
         SBLAS_HIP(hipMemcpyAsync(htrace.data(), a.trace, sizeof(long long) * htrace.size(),
                                  hipMemcpyDeviceToHost, s));
@@ -1267,11 +1267,11 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     if (P.nwide && !P.fused) {
         const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
         if (b)
-            hipLaunchKernelGGL(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide,
-                               P.partial, alpha, beta, y);
+            SBLAS_LAUNCH(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide, P.partial, alpha, beta,
+                         y);
         else
-            hipLaunchKernelGGL(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.ranges, P.wide,
-                               P.partial, alpha, beta, y);
+            SBLAS_LAUNCH(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.ranges, P.wide, P.partial, alpha, beta,
+                         y);
     }
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;

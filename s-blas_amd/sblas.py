@@ -78,6 +78,7 @@ _sig("sblas_csr_destroy", _i, _p)
 _sig("sblas_csr_info", _i, _p, _p, _p, _p)
 _sig("sblas_csr_analyse", _i, _p, _i, _p)
 _sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
+_sig("sblas_spmv_timed", _i, _p, _i, C.c_double, _p, C.c_double, _p, _p, _p)
 _sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
 _sig("sblas_csr_plan_bytes", _ll, _p, _i)
 _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
@@ -385,6 +386,15 @@ class DeviceCSR:
     def spmv(self, algo: int, alpha: float, x_ptr: int, beta: float, y_ptr: int,
              stream=None) -> None:
         check(lib.sblas_spmv(self.h, algo, alpha, x_ptr, beta, y_ptr, stream), "spmv")
+
+    def spmv_timed(self, algo: int, alpha: float, x_ptr: int, beta: float, y_ptr: int,
+                   stream=None) -> float:
+        """sblas_spmv_timed: runs the SpMV, waits, returns its device span in
+        ms (first kernel start .. last kernel end)."""
+        ms = C.c_float(0.0)
+        check(lib.sblas_spmv_timed(self.h, algo, alpha, x_ptr, beta, y_ptr, stream, C.byref(ms)),
+              "spmv_timed")
+        return float(ms.value)
 
     def spmm(self, ncols: int, alpha: float, b_ptr: int, ldb: int, b_layout: int, beta: float,
              c_ptr: int, ldc: int, stream=None) -> None:
