@@ -519,7 +519,9 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     const int m = A.m, k = A.n;
     int wlog = 11;  // 2048 B rows = 1 MiB of B per slab at n = 64
     if (const char *e = getenv("SBLAS_SPMM_CTW")) wlog = std::max(4, std::min(20, atoi(e)));
-    const int nrb = (m + kCtMaxRows - 1) / kCtMaxRows;
+    int rmax = kCtMaxRows;  // experiments: SBLAS_SPMM_CTR caps the tile rows
+    if (const char *e = getenv("SBLAS_SPMM_CTR")) rmax = std::max(16, std::min(kCtMaxRows, atoi(e)));
+    const int nrb = (m + rmax - 1) / rmax;
     const int R = (m + nrb - 1) / nrb;
     int rbits = 1;
     while ((1 << rbits) < R) ++rbits;
