@@ -174,7 +174,8 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz,
 /* algo 0 = sync-free CSC push (reference algorithm), 1 = CSR pull with ready
  * flags (deterministic sums), 2 = level-set (rows grouped by level,
  * findlevel.h:71-147; one synchronisation per level; built on the first
- * algo-2 solve; x bit-identical to algo 1). */
+ * algo-2 solve; x bit-identical to algo 1), 3 = the pull executor with its
+ * tickets in level order (same analysis; x bit-identical to algo 1). */
 int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x,
                      void *stream);
 int sblas_trsv_levels(sblas_trsv T, int *nlevel);

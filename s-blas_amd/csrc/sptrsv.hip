@@ -179,10 +179,15 @@ __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long lon
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// kLevel (algo 3): tickets walk the level-ordered CSR of the level-set
+// analysis (position t holds row lrow[t]; rows of one level are contiguous),
+// so the 64 rows of a wave belong to one level and become ready together
+// instead of a wave waiting on its latest level.  Same sums, same order.
+template <bool kLevel>
 __global__ __launch_bounds__(256) void k_trsv_pull(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, int n, int backward, const double *__restrict__ b,
-    unsigned long long *xbits, unsigned *ctl)
+    unsigned long long *xbits, unsigned *ctl, const int *__restrict__ lrow)
 {
     constexpr int kBatch = 8;
     const int lane = threadIdx.x & 63;
@@ -193,11 +198,12 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
         if (t0 >= n) return;  // done, or another wave timed out: the solve is void
         const int t = t0 + lane;
         const bool live = t < n;
-        const int i = live ? (backward ? n - 1 - t : t) : 0;
+        const int i = live ? (kLevel ? lrow[t] : (backward ? n - 1 - t : t)) : 0;
+        const int ri = kLevel ? t : i;  // CSR row index of this row
         int j = 0, jend = 0;
         double diag = 1.0, sum = 0.0;
         if (live) {
-            const int a = rowptr[i], e = rowptr[i + 1];
+            const int a = rowptr[ri], e = rowptr[ri + 1];
             if (backward) {
                 diag = val[a];
                 j = a + 1;
@@ -808,22 +814,27 @@ static int solve_levelset(sblas_trsv_s *T, const double *b, double *x, hipStream
 
 int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, void *stream)
 {
-    if (!T || !d_b || !d_x || algo < 0 || algo > 2) return SBLAS_ERR_INVALID;
+    if (!T || !d_b || !d_x || algo < 0 || algo > 3) return SBLAS_ERR_INVALID;
     if (T->n == 0) return SBLAS_OK;
     DeviceGuard g(T->device);
     hipStream_t s = (hipStream_t)stream;
     if (algo == 2) return solve_levelset(T, d_b, d_x, s);
+    if (algo == 3) SBLAS_TRY(build_levelset(T, s));
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     const int grid = grid_for(T->device);
-    if (algo == 0) {
+    if (algo == 3) {  // sync-free pull, tickets in level order
+        fill_pending((unsigned long long *)d_x, T->n, s);
+        hipLaunchKernelGGL(k_trsv_pull<true>, dim3(grid), dim3(256), 0, s, T->lrp, T->lcol, T->lval, T->n,
+                           T->substitution, d_b, (unsigned long long *)d_x, T->ctl, T->lrow);
+    } else if (algo == 0) {
         SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
         SBLAS_HIP(hipMemsetAsync(T->left, 0, sizeof(double) * T->n, s));
         hipLaunchKernelGGL(k_trsv_push, dim3(grid), dim3(256), 0, s, T->colptr, T->rowidx, T->val,
                            T->in_degree, T->n, T->substitution, d_b, d_x, T->done, T->left, T->ctl);
     } else {
         fill_pending((unsigned long long *)d_x, T->n, s);
-        hipLaunchKernelGGL(k_trsv_pull, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
-                           T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl);
+        hipLaunchKernelGGL(k_trsv_pull<false>, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
+                           T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl, nullptr);
     }
     SBLAS_HIP(hipGetLastError());
     unsigned h[kCtlBytes / 4] = {0};

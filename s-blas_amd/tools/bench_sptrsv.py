@@ -58,7 +58,7 @@ def main():
     abytes = 12 * nnz + 4 * (n + 1) + 16 * n
     res = {}
     s = torch.cuda.Stream(device=dev)
-    for algo, name in ((1, "pull_csr"), (0, "push_csc"), (2, "levelset_csr")):
+    for algo, name in ((1, "pull_csr"), (3, "pull_level_order"), (0, "push_csc"), (2, "levelset_csr")):
         with torch.cuda.stream(s):
             T.solve(algo, db.data_ptr(), dx.data_ptr(), s.cuda_stream)  # warm-up
             torch.cuda.synchronize()

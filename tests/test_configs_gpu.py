@@ -173,7 +173,7 @@ def test_config5_kat_serial_oracle(orc, cfg5):
     assert orc.levels_lower(c["cp"], c["ri"]) > 100
 
 
-@pytest.mark.parametrize("algo", [1, 0, 2], ids=["pull", "push", "levelset"])
+@pytest.mark.parametrize("algo", [1, 0, 2, 3], ids=["pull", "push", "levelset", "pull_level_order"])
 def test_config5_single_device_exact(torch_cuda, sb, cfg5, algo):
     torch = torch_cuda
     c = cfg5

@@ -194,7 +194,7 @@ def test_sptrans_reference_api(torch_cuda, sb, orc, capfd):
 # -------------------------------------------------------------- SpTRSV ----
 @pytest.mark.parametrize("name", ["qh768", "ash85"])
 @pytest.mark.parametrize("sub", ["fwd", "bwd"])
-@pytest.mark.parametrize("algo", [0, 1, 2])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     torch = torch_cuda
     g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
@@ -214,7 +214,7 @@ def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     T.close()
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     """Random lower-triangular with long chains and a long column/row."""
     torch = torch_cuda
@@ -242,7 +242,7 @@ def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     x = xd.cpu().numpy()
     rel = np.abs(x - want).sum() / np.abs(want).sum()
     assert rel <= 1e-12, rel
-    if algo == 2:  # level-set sums in the pull executor's order: bit-identical
+    if algo in (2, 3):  # level-set / level-ordered pull sum in the pull executor's order: bit-identical
         xp = torch.zeros(n, dtype=torch.float64, device="cuda")
         T.solve(1, d[3].data_ptr(), xp.data_ptr())
         torch.cuda.synchronize()
