@@ -57,6 +57,56 @@ def blocky(m, k, width, seed):
     return rp, np.concatenate(rows).astype(np.int32)
 
 
+def cpu_baseline_spmm(m, n, rp, col, val, B, C0, budget_s=10.0):
+    """The oracle's csrmm restatement (orc_spmm_omp, OpenMP over rows; test
+    infrastructure, only this leg touches oracle/) on this host's cores."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle", "liboracle.so"))
+    f = lib.orc_spmm_omp
+    f.restype = None
+    f.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                  C.c_int, C.c_double, C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    rp32 = np.ascontiguousarray(rp, np.int32)
+    Cw = np.array(C0, np.float64, copy=True, order="F")
+    args = (m, n, -0.7, rp32.ctypes.data, col.ctypes.data, val.ctypes.data, B.ctypes.data, n, 1, 0.8,
+            Cw.ctypes.data, m, None, threads)
+    f(*args)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        f(*args)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or reps >= 50:
+            break
+    t = el / reps
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nnz = int(rp[-1])
+    return {"value": round(2.0 * nnz * n / t / 1e9, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+            "cpu_model": model,
+            "sample": f"full config-4 product, orc_spmm_omp (OpenMP over rows, B row-major) x{reps} reps, "
+                      f"{t * 1e3:.1f} ms per call"}
+
+
+def pmc_traffic_spmm():
+    """Fabric bytes per call of the C-tile kernels from a committed
+    rocprofv3 FETCH/WRITE summary (profiles/pmc_spmm_ctile.json), or None."""
+    p = os.path.join(os.path.dirname(os.path.dirname(HERE)), "profiles", "pmc_spmm_ctile.json")
+    try:
+        with open(p) as fh:
+            return float(json.load(fh)["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mrows", type=int, default=4284)
@@ -71,6 +121,7 @@ def main():
                     help="instead of the rail4284 shape: 16-row blocks each dense (~90%%) over "
                          "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", choices=["rows", "cols"], default="rows",
                     help="rows: whole-row blocks of A by nnz (north star); cols: A replicated, "
                          "B/C columns split (the reference's dspmm_mgpu_baseline.cu:147-150)")
@@ -184,6 +235,10 @@ def main():
             "gbps_brow": round(nnz * n * 8 / kern_max / 1e6 / max(world, 1), 1),
             "max_rel_err_32_rows": err,
         }
+        if world == 1 and not args.blocky and lay == 1:
+            out["roofline"]["traffic"] = pmc_traffic_spmm()
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_spmm(m, n, rp, col, val, Bh, C0h.T)
         if world > 1 and args.dist_backend != "nccl":
             out["note"] = f"rehearsal: {world} ranks over gloo"
         print(json.dumps(out), flush=True)
