@@ -187,6 +187,7 @@ struct XsArgs {
     int *qreset;            // the other parity's heads, re-armed to qstat by block 0
     int qstat[8];           // items per queue taken statically (block b: queue b%8, index b/8)
     int dynamic;            // items beyond the static share exist (claims needed)
+    int sc1part;            // experiments: agent-scope partial stores without the fused reduce
     int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
     int nrtasks;
     const int2 *rtasks;     // (range, first row) reduce tasks

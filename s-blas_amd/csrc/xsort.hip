@@ -631,12 +631,22 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
             if (k1) {
                 double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
-                // agent-scope (sc1) stores: the fused reduce may read them on
-                // another XCD, whose L2 is not coherent with this one
+                // agent-scope (sc1) stores when the fused reduce may read them
+                // on another XCD (whose L2 is not coherent with this one);
+                // plain stores otherwise: the kernel boundary before
+                // k_xsort_reduce publishes them (SBLAS_XS_SC1PART=1 keeps sc1)
+                if (a.fused || a.sc1part) {
 #pragma unroll
-                for (int e = 0; e < kEp; ++e) {
-                    const int r = ht + e * NT;
-                    if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        if (r < R.nrows) out[r] = acc[r];
+                    }
                 }
             } else {
                 double *yr = y + R.row0;
@@ -669,6 +679,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
 }
 
 // Wide ranges: y = alpha * sum_k partial[k] (+ beta*y), XCD slots in order.
+// All 8 partial loads (and y) of a row are issued before the first add.
 template <bool kBeta>
 __global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict__ ranges,
                                                       const int *__restrict__ wide,
@@ -679,11 +690,15 @@ __global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict_
     const XsRange R = ranges[wide[blockIdx.y]];
     for (int r = blockIdx.x * 256 + threadIdx.x; r < R.nrows; r += gridDim.x * 256) {
         const double *p = partial + R.pbase + r;
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(p + (long long)k * R.nrows);
+        double *yr = y + R.row0 + r;
+        const double y0 = kBeta ? *yr : 0.0;
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += p[(long long)k * R.nrows];
-        double *yr = y + R.row0 + r;
-        *yr = kBeta ? alpha * s + beta * *yr : alpha * s;
+        for (int k = 0; k < 8; ++k) s += v[k];
+        *yr = kBeta ? alpha * s + beta * y0 : alpha * s;
     }
 }
 
@@ -1186,6 +1201,11 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.q = P.q;
     a.Wg = P.Wg;
     a.use_xcc = use_xcc;
+    static const int sc1part = [] {
+        const char *e = getenv("SBLAS_XS_SC1PART");
+        return e ? atoi(e) : 0;
+    }();
+    a.sc1part = sc1part;
     using K = void (*)(const XsArgs, const double *, double, double, double *);
     K kern;
     const bool b = beta != 0.0;
