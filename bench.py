@@ -153,6 +153,9 @@ def main() -> int:
                          "pay) or read+write (add_, round 1's method)")
     ap.add_argument("--no-rowsplit-beside", action="store_true",
                     help="skip the row-split kernel's figure reported beside the headline")
+    ap.add_argument("--overlap", action="store_true",
+                    help="N>1 cyclic allgather: split each rank's chunks in two halves and "
+                         "all-gather the first while the kernel runs on the second")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -203,14 +206,18 @@ def main() -> int:
                                               prefix=prefix, seed=42))
         t_gen = time.perf_counter() - t_gen
         try:
-            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
+            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
+                                           overlap=args.overlap)
         except sblas.SblasError:
             if not (auto and algo == sblas.XSORT):
                 raise
             args.algo, algo = "panel", sblas.PANEL  # the layout does not apply: fall back
-            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist)
+            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
+                                           overlap=args.overlap)
         local_nnz = int(lrp[-1])
         partition = f"cyclic row chunks ({plan.chunk_rows} rows, {plan.nchunks} chunks)"
+        if op.overlap:
+            partition += ", two-half overlapped all-gather"
     else:
         plan = sblas_dist.make_plan(rowptr, n, world)
         r0, r1, i0, i1, _ = plan.local(rank)

@@ -199,6 +199,23 @@ def cyclic_local_csr(rowptr: np.ndarray, plan: CyclicPlan, rank: int, rows_fn):
     return lrp, np.ascontiguousarray(col), np.ascontiguousarray(val)
 
 
+def overlap_halves(plan: CyclicPlan):
+    """Two-half split of the cyclic deal for the overlapped exchange.
+
+    Each rank's first hA local chunks (global chunks < hA * world) form half A,
+    the rest half B; each half is dealt cyclically on its own, so each is
+    placed by one sblas_assemble_cyclic call.  Returns (hA, strideA, strideB,
+    rows_a): per-rank slice lengths of the halves and the global rows of
+    half A (half B starts at row rows_a)."""
+    R, g = plan.chunk_rows, plan.world
+    ncmax = -(-plan.nchunks // g)
+    hA = (ncmax + 1) // 2
+    strideA = hA * R
+    strideB = max(1, plan.stride - strideA)
+    rows_a = min(plan.m, hA * g * R)
+    return hA, strideA, strideB, rows_a
+
+
 class DistSpMVCyclic:
     """One rank's share of y = alpha*A*x + beta*y under the cyclic row-chunk
     distribution: the rank's rows are uploaded as one local CSR, y_local is
@@ -208,14 +225,15 @@ class DistSpMVCyclic:
     call's y input (whole rows), so nothing is copied back."""
 
     def __init__(self, plan: CyclicPlan, rank: int, device: int, local_rowptr, col, val,
-                 algo: int, torch, dist=None):
+                 algo: int, torch, dist=None, overlap: bool = False):
         self.plan, self.rank, self.algo = plan, rank, algo
         self.torch, self.dist = torch, dist
         self.dm = len(local_rowptr) - 1
         dev = torch.device("cuda", device)
-        self.A = sblas.DeviceCSR.upload(device, plan.n, np.ascontiguousarray(local_rowptr, np.int64),
-                                        np.ascontiguousarray(col, np.int32),
-                                        np.ascontiguousarray(val, np.float64))
+        lrp64 = np.ascontiguousarray(local_rowptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        self.A = sblas.DeviceCSR.upload(device, plan.n, lrp64, col, val)
         t0 = time.perf_counter()
         self.A.analyse(algo)
         self.plan_s = time.perf_counter() - t0
@@ -223,6 +241,25 @@ class DistSpMVCyclic:
         self.y_local = torch.zeros(plan.stride, dtype=f64, device=dev)
         self.y_full = torch.zeros(plan.m, dtype=f64, device=dev)
         self.gathered = torch.zeros(plan.world * plan.stride, dtype=f64, device=dev)
+        # overlap: the rank's chunks in two halves (the first hA local chunks
+        # of every rank, then the rest), each its own handle; the all-gather
+        # of half A runs while half B's kernel runs
+        # (needs two chunks per rank to split)
+        self.overlap = bool(overlap) and plan.world > 1 and plan.nchunks > plan.world
+        self._work = []
+        if self.overlap:
+            self.hA, self.strideA, self.strideB, self.rows_a = overlap_halves(plan)
+            rA = min(self.dm, self.strideA)
+            self.halves = []
+            for r0, r1 in ((0, rA), (rA, self.dm)):
+                H = None
+                if r1 > r0:
+                    H = sblas.DeviceCSR.upload_slice(device, plan.n, lrp64, col, val, r0, r1,
+                                                     int(lrp64[r0]), int(lrp64[r1]))
+                    H.analyse(algo)
+                self.halves.append((H, r0, r1))
+            self.gA = torch.zeros(plan.world * self.strideA, dtype=f64, device=dev)
+            self.gB = torch.zeros(plan.world * self.strideB, dtype=f64, device=dev)
 
     def load_y(self, y_full) -> None:
         self.y_full.copy_(y_full)
@@ -232,11 +269,45 @@ class DistSpMVCyclic:
             o += b - a
 
     def kernel(self, alpha: float, x, beta: float, stream=None) -> None:
+        if self.overlap:
+            (HA, a0, _), (HB, b0, _) = self.halves
+            if HA is not None:
+                HA.spmv(self.algo, alpha, x.data_ptr(), beta, self.y_local.data_ptr() + 8 * a0, stream)
+            if self.dist.get_backend() == "nccl":  # collective stream waits for half A only
+                self._work.append(self.dist.all_gather_into_tensor(
+                    self.gA, self.y_local[: self.strideA], async_op=True))
+            if HB is not None:
+                HB.spmv(self.algo, alpha, x.data_ptr(), beta, self.y_local.data_ptr() + 8 * b0, stream)
+            return
         if self.dm > 0:
             self.A.spmv(self.algo, alpha, x.data_ptr(), beta, self.y_local.data_ptr(), stream)
 
+    def _gather_gloo(self, out, inp):
+        chunks = [c.cpu() for c in out.chunk(self.plan.world)]
+        self.dist.all_gather(chunks, inp.cpu())
+        out.copy_(self.torch.cat(chunks).to(out.device))
+
     def exchange(self, stream=None) -> None:
         if self.plan.world == 1:
+            return
+        if self.overlap:
+            yB = self.y_local[self.strideA: self.strideA + self.strideB]
+            if self.dist.get_backend() == "nccl":
+                self._work.append(self.dist.all_gather_into_tensor(self.gB, yB, async_op=True))
+                for w in self._work:
+                    w.wait()
+                self._work = []
+            else:  # gloo rehearsal: same data flow, no overlap
+                self._gather_gloo(self.gA, self.y_local[: self.strideA])
+                self._gather_gloo(self.gB, yB)
+            p, R, g, rows_a = self.plan, self.plan.chunk_rows, self.plan.world, self.rows_a
+            sblas.check(sblas.lib.sblas_assemble_cyclic(
+                self.gA.data_ptr(), g, self.strideA, R, rows_a, self.y_full.data_ptr(), stream),
+                "assemble_cyclic")
+            if p.m > rows_a:
+                sblas.check(sblas.lib.sblas_assemble_cyclic(
+                    self.gB.data_ptr(), g, self.strideB, R, p.m - rows_a,
+                    self.y_full.data_ptr() + 8 * rows_a, stream), "assemble_cyclic")
             return
         if self.dist.get_backend() == "nccl":
             self.dist.all_gather_into_tensor(self.gathered, self.y_local)
@@ -255,6 +326,9 @@ class DistSpMVCyclic:
 
     def close(self):
         self.A.close()
+        for H, _, _ in getattr(self, "halves", []):
+            if H is not None:
+                H.close()
 
 
 # ---------------------------------------------------------------------------

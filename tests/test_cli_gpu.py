@@ -189,9 +189,10 @@ def bench_2rank(extra, nrows=2_000_000):
     ["--algo", "csr5", "--partition", "nnz", "--exchange", "allreduce"],
     ["--algo", "csr5"],
     ["--algo", "xsort"],
-    ["--algo", "panel", "--partition", "nnz"]],
+    ["--algo", "panel", "--partition", "nnz"],
+    ["--algo", "xsort", "--overlap"]],
     ids=["cfg3_csr5_nnz_allreduce", "csr5_cyclic_allgather", "xsort_cyclic_allgather",
-         "panel_nnz_allgather"])
+         "panel_nnz_allgather", "xsort_cyclic_overlap_halves"])
 def test_config3_two_ranks(extra):
     """BASELINE configs[2]'s dataflow on 2 ranks at full size, checked."""
     out = bench_2rank(extra)

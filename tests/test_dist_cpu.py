@@ -92,7 +92,7 @@ def assemble_cyclic(gathered, world, stride, R, m):
     return gathered[(j % world) * stride + (j // world) * R + (r - j * R)]
 
 
-def _cyclic_worker(rank, world, port, n, result_q):
+def _cyclic_worker(rank, world, port, n, result_q, halves=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import orc
@@ -109,9 +109,21 @@ def _cyclic_worker(rank, world, port, n, result_q):
     part = orc.csr_spmv(lrp, lcol, lval, x, a, b, yl)
     buf = torch.zeros(plan.stride, dtype=torch.float64)
     buf[:len(part)] = torch.from_numpy(part)
-    out = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf)
-    y = assemble_cyclic(torch.cat(out).numpy(), world, plan.stride, plan.chunk_rows, plan.m)
+    if halves:
+        # DistSpMVCyclic(overlap=True): the slice's first hA chunks and the
+        # rest are all-gathered separately and each half placed on its own
+        hA, sA, sB, rows_a = sblas_dist.overlap_halves(plan)
+        outA = [torch.zeros(sA, dtype=torch.float64) for _ in range(world)]
+        outB = [torch.zeros(sB, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(outA, buf[:sA].contiguous())
+        dist.all_gather(outB, buf[sA:sA + sB].contiguous())
+        y = np.concatenate([
+            assemble_cyclic(torch.cat(outA).numpy(), world, sA, plan.chunk_rows, rows_a),
+            assemble_cyclic(torch.cat(outB).numpy(), world, sB, plan.chunk_rows, plan.m - rows_a)])
+    else:
+        out = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        y = assemble_cyclic(torch.cat(out).numpy(), world, plan.stride, plan.chunk_rows, plan.m)
     want = orc.csr_spmv(rp, col, val, x, a, b, y0)
     ok = bool(np.all(np.abs(y - want) <= orc.spmv_bound(rp, col, val, x, a, b, y0)))
     # every rank holds the same number of rows (up to the last chunk) and
@@ -123,12 +135,13 @@ def _cyclic_worker(rank, world, port, n, result_q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("halves", [False, True], ids=["one_gather", "overlap_halves"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_gloo_cyclic_protocol(world):
+def test_gloo_cyclic_protocol(world, halves):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_cyclic_worker, args=(r, world, port, 1003, q))
+    procs = [ctx.Process(target=_cyclic_worker, args=(r, world, port, 1003, q, halves))
              for r in range(world)]
     for p in procs:
         p.start()

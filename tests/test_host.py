@@ -268,3 +268,34 @@ def test_cyclic_partition_matches_dist_plan(sb, m, g):
         total_rows += len(lrp) - 1
         total_nnz += int(lrp[-1])
     assert total_rows == m and total_nnz == int(rp[-1])
+
+
+@pytest.mark.parametrize("m,g", [(1, 2), (77, 5), (1003, 2), (1003, 3), (200_003, 8), (9, 4)])
+def test_overlap_halves_place_every_row_once(m, g):
+    """DistSpMVCyclic(overlap=True) splits each rank's slice at hA chunks
+    and places the halves with two assemble_cyclic calls (rows [0, rows_a)
+    and [rows_a, m)).  With each rank's slice filled by its global row ids,
+    the two placements reproduce 0..m-1 (ragged last chunk, ranks with fewer
+    chunks included)."""
+    import sblas_dist
+    rp = np.zeros(m + 1, np.int64)
+    plan = sblas_dist.make_cyclic_plan(rp, m, g)
+    hA, sA, sB, rows_a = sblas_dist.overlap_halves(plan)
+    assert sA + sB == plan.stride or (sA == plan.stride and sB == 1)
+    R = plan.chunk_rows
+    slices = []
+    for d in range(g):
+        ids = np.concatenate([np.arange(a, b) for a, b in plan.chunks(d)] or [np.zeros(0, np.int64)])
+        buf = np.full(plan.stride + 1, -1, np.int64)
+        buf[:len(ids)] = ids
+        slices.append(buf)
+
+    def place(gathered, stride, rows):
+        r = np.arange(rows)
+        j = r // R
+        return gathered[(j % g) * stride + (j // g) * R + (r - j * R)]
+
+    gA = np.concatenate([s[:sA] for s in slices])
+    gB = np.concatenate([s[sA:sA + sB] for s in slices])
+    y = np.concatenate([place(gA, sA, rows_a), place(gB, sB, m - rows_a)])
+    assert np.array_equal(y, np.arange(m))
