@@ -184,6 +184,15 @@ int sblas_trsv_destroy(sblas_trsv T);
  * sptrsv_v1/src/sptrsv_syncfree_cuda.h:170-282): d_b, d_x device n x rhs
  * row-major.  Pull executor; rhs == 1 is sblas_trsv_solve(T, 1, ...). */
 int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream);
+/* SpTRSM with the executor chosen: algo 1 = the pull executor above (opt
+ * ignored); algo 0 = the reference's push dataflow (CSC scatter of left sums
+ * with fp64 atomics, sptrsv_syncfree_cuda.h:170-282) with its lane mapping
+ * opt: 1 OPT_WARP_NNZ (lanes over a column's entries), 2 OPT_WARP_RHS (lanes
+ * over the right-hand sides), 3 OPT_WARP_AUTO (per column: rhs mapping when
+ * (len <= rhs || rhs > 16) && len < 2048).  rhs >= 1.  Push sums land in
+ * arrival order: within the fp64 bound, not bitwise repeatable. */
+int sblas_trsv_solve_rhs_opt(sblas_trsv T, int algo, int opt, int rhs, const double *d_b,
+                             double *d_x, void *stream);
 /* Out-of-core SpMV (the task pool + streams of spMV_mgpu_v2,
  * dspmv_mgpu_v2.cu:33-441).  HOST CSR (int64 rowptr), x and y: the matrix is
  * streamed through ngpu devices in nnz-balanced chunks of chunk_nnz, over

@@ -330,12 +330,16 @@ static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const d
     sblas_trsv T = nullptr;
     SBLAS_TRY(sblas_trsv_create(&T, 0, n, nnz, (const int *)dcp.p, (const int *)dri.p,
                                 (const double *)dv.p, substitution, nullptr));
-    // rhs == 1: opt 1 (OPT_WARP_NNZ) -> CSC push (reference algorithm), else
-    // CSR pull; rhs > 1: the SpTRSM pull executor
-    const int algo = opt == 1 ? 0 : 1;
+    // opt 1 (OPT_WARP_NNZ) / 2 (OPT_WARP_RHS): the reference's CSC push
+    // dataflow with that lane mapping (rhs == 1, opt 1: k_trsv_push); any
+    // other opt, OPT_WARP_AUTO included (the reference main's choice), picks
+    // the fastest executor: the CSR pull executor (SpTRSM pull for rhs > 1)
+    const bool push = opt == 1 || opt == 2;
     auto solve = [&]() {
-        return rhs == 1 ? sblas_trsv_solve(T, algo, (const double *)db.p, (double *)dx.p, nullptr)
-                        : sblas_trsv_solve_rhs(T, rhs, (const double *)db.p, (double *)dx.p, nullptr);
+        const double *bb = (const double *)db.p;
+        double *xx = (double *)dx.p;
+        if (rhs == 1 && opt != 2) return sblas_trsv_solve(T, push ? 0 : 1, bb, xx, nullptr);
+        return sblas_trsv_solve_rhs_opt(T, push ? 0 : 1, opt, rhs, bb, xx, nullptr);
     };
     int st = solve();  // warm-up
     const double t0 = sblas_get_time();
@@ -349,8 +353,8 @@ static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const d
 
 // sptrsv_syncfree_cuda (sptrsv_v1/src/sptrsv_syncfree_cuda.h:287-670).
 // Prints the reference's timing / validation lines.  opt selects the
-// executor: OPT_WARP_NNZ (1) -> CSC push (reference algorithm), otherwise
-// the CSR pull executor.  ngpu > 1 runs the multi-device pull executor
+// executor: OPT_WARP_NNZ (1) / OPT_WARP_RHS (2) -> CSC push (reference
+// algorithm, that lane mapping), otherwise the CSR pull executor.  ngpu > 1 runs the multi-device pull executor
 // (sblas_trsv_mgpu_solve: nnz-balanced blocks of the solve order, x pushed to
 // later blocks over xGMI), which is what sptrsv_v2/v3 distribute.
 int sblas_sptrsv_syncfree(const int *cscColPtr, const int *cscRowIdx, const double *cscVal, int m,

@@ -430,11 +430,133 @@ __global__ void k_empty_rows(const int *__restrict__ rows, int n, double beta,
     y[r] = kBeta ? beta * y[r] : 0.0;
 }
 
+// ---- CSR5 tile descriptors built on the device ----------------------------
+// (the reference builds its descriptors on the GPU too:
+// spmv/include/detail/cuda/format_cuda.h:21-300).  Same arrays as the host
+// builder below (kept as SBLAS_CSR5_HOSTPLAN=1): row-start bits, the row of
+// each tile's first element (bit 31: the tile holds empty rows), and for such
+// tiles the explicit list of rows starting in the tile.
+__global__ void k_c5_flags(const int *__restrict__ rp, int m, uint32_t *__restrict__ flags,
+                           int *__restrict__ empty, int *__restrict__ nempty)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const int a = rp[r];
+    if (a == rp[r + 1]) {
+        empty[atomicAdd(nempty, 1)] = r;
+        return;
+    }
+    const long long t = a / kC5Tile;
+    const int w = (int)(a - t * kC5Tile);
+    atomicOr(&flags[t * 64 + w / kC5Sigma], 1u << (w % kC5Sigma));
+}
+
+// last r in [0, m) with rp[r] <= e (e < nnz: that row holds element e)
+__device__ __forceinline__ int c5_row_of(const int *__restrict__ rp, int m, long long e)
+{
+    int lo = 0, hi = m;  // invariant rp[lo] <= e, answer in [lo, hi)
+    while (hi - lo > 1) {
+        const int mid = lo + (hi - lo) / 2;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_c5_tiles(const int *__restrict__ rp, int m, long long nnz, long long nt,
+                           const uint32_t *__restrict__ flags, int *__restrict__ trow,
+                           int *__restrict__ segcnt)
+{
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == nt) trow[nt] = m;
+    if (t >= nt) return;
+    const long long e = t * kC5Tile;
+    const long long elast = (nnz < e + kC5Tile ? nnz : e + kC5Tile) - 1;
+    const int rf = c5_row_of(rp, m, e), rl = c5_row_of(rp, m, elast);
+    int nstarts = 0;
+    for (int l = 0; l < 64; ++l) nstarts += __popc(flags[t * 64 + l]);
+    const int start0 = (int)(flags[t * 64] & 1u);
+    const bool holes = nstarts != rl - rf + start0;
+    trow[t] = holes ? (int)((unsigned)rf | 0x80000000u) : rf;
+    segcnt[t] = holes ? nstarts : 0;
+}
+
+__global__ void k_c5_segrows(const int *__restrict__ rp, int m, long long nnz, long long nt,
+                             const uint32_t *__restrict__ flags, const int *__restrict__ trow,
+                             const int *__restrict__ seg_end, int *__restrict__ seg_row)
+{
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt || trow[t] >= 0) return;
+    const long long e = t * kC5Tile;
+    const long long elast = (nnz < e + kC5Tile ? nnz : e + kC5Tile) - 1;
+    const int rf = trow[t] & 0x7fffffff, rl = c5_row_of(rp, m, elast);
+    int o = t ? seg_end[t - 1] : 0;
+    for (int q = (flags[t * 64] & 1u) ? rf : rf + 1; q <= rl; ++q)
+        if (rp[q + 1] > rp[q] && rp[q] >= e && rp[q] <= elast) seg_row[o++] = q;
+}
+
+static int build_csr5_plan_device(sblas_csr_s &A, hipStream_t s)
+{
+    Csr5Plan &P = A.c5;
+    const long long nnz = A.nnz, nt = P.ntiles;
+    const int m = A.m;
+    SBLAS_HIP(hipMalloc(&P.tile_row, sizeof(int) * (nt + 1)));
+    SBLAS_HIP(hipMalloc(&P.flags, sizeof(uint32_t) * std::max<long long>(nt * 64, 1)));
+    SBLAS_HIP(hipMalloc(&P.seg_off, sizeof(int) * (nt + 1)));
+    SBLAS_HIP(hipMalloc(&P.empty_rows, sizeof(int) * (std::max(m, 1) + 1)));
+    int *nempty = P.empty_rows + std::max(m, 1);  // counter word after the list
+    SBLAS_HIP(hipMemsetAsync(P.flags, 0, sizeof(uint32_t) * std::max<long long>(nt * 64, 1), s));
+    SBLAS_HIP(hipMemsetAsync(P.seg_off, 0, sizeof(int) * (nt + 1), s));
+    SBLAS_HIP(hipMemsetAsync(nempty, 0, sizeof(int), s));
+    if (m > 0)
+        hipLaunchKernelGGL(k_c5_flags, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+                           P.flags, P.empty_rows, nempty);
+    // seg_off[0] = 0, seg_off[1..nt] = inclusive scan of the per-tile counts
+    hipLaunchKernelGGL(k_c5_tiles, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+                       nnz, nt, P.flags, P.tile_row, P.seg_off + 1);
+    SBLAS_HIP(hipGetLastError());
+    int *scratch = nullptr;
+    SBLAS_HIP(hipMalloc(&scratch, sizeof(int) * (nt / 1024 + 256)));
+    const int st = scan_inclusive(P.seg_off + 1, nt, scratch, s);
+    int h[2] = {0, 0};
+    if (st == SBLAS_OK) {
+        SBLAS_HIP(hipMemcpyAsync(&h[0], P.seg_off + nt, sizeof(int), hipMemcpyDeviceToHost, s));
+        SBLAS_HIP(hipMemcpyAsync(&h[1], nempty, sizeof(int), hipMemcpyDeviceToHost, s));
+        SBLAS_HIP(hipStreamSynchronize(s));
+    }
+    (void)hipFree(scratch);
+    SBLAS_TRY(st);
+    P.nempty = h[1];
+    SBLAS_HIP(hipMalloc(&P.seg_row, sizeof(int) * std::max(h[0], 1)));
+    if (h[0] > 0)
+        hipLaunchKernelGGL(k_c5_segrows, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+                           nnz, nt, P.flags, P.tile_row, P.seg_off + 1, P.seg_row);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
 int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.c5.ready) return SBLAS_OK;
     DeviceGuard g(A.device);
     Csr5Plan &P = A.c5;
+    const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
+    if (!(hp && atoi(hp) == 1)) {
+        P.ntiles = (A.nnz + kC5Tile - 1) / kC5Tile;
+        SBLAS_TRY(build_csr5_plan_device(A, s));
+        const long long nt = P.ntiles, total = nt * kC5Tile;
+        SBLAS_HIP(hipMalloc(&P.tval, sizeof(double) * std::max<long long>(total, 1)));
+        SBLAS_HIP(hipMalloc(&P.tcol, sizeof(int) * std::max<long long>(total, 1)));
+        SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
+        if (total) {
+            hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                               A.col, A.val, A.nnz, total, P.tcol, P.tval);
+            SBLAS_HIP(hipGetLastError());
+        }
+        SBLAS_HIP(hipStreamSynchronize(s));
+        P.ready = true;
+        return SBLAS_OK;
+    }
     const long long nnz = A.nnz;
     const std::vector<int> &rp = A.h_rowptr;
     P.ntiles = (nnz + kC5Tile - 1) / kC5Tile;

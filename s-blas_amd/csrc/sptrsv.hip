@@ -46,6 +46,8 @@ struct sblas_trsv_s {
     // scratch
     int *done = nullptr;       // push: arrivals per row; pull: ready flags
     double *left = nullptr;    // push: left sums
+    double *left_rhs = nullptr;  // SpTRSM push: left sums n x rhs (grown on demand)
+    size_t left_rhs_cap = 0;
     unsigned *ctl = nullptr;   // [0] ticket, [kAbort] timeout flag (kCtlBytes block)
     int nlevels = -1;
     // level-set executor (algo 2), built on its first solve: rows in level
@@ -506,6 +508,82 @@ static void launch_trsm(const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t 
     }
 }
 
+// ---- SpTRSM push: the reference's dataflow with its lane mappings ---------
+// sptrsm_syncfree_cuda_executor (sptrsv_v1/src/sptrsv_syncfree_cuda.h:170-282):
+// one wave per column (monotone ticket, as k_trsv_push), the column's
+// contributions scattered into left sums n x rhs with fp64 atomics, then the
+// in-degree counters bumped.  The lane mapping is the reference's `opt`:
+//   kOptNnz  (OPT_WARP_NNZ, 1): lanes over the column's entries, each lane
+//            loops over the rhs;
+//   kOptRhs  (OPT_WARP_RHS, 2): lanes over the rhs, entries in sequence;
+//   kOptAuto (OPT_WARP_AUTO, 3): per column, the rhs mapping when
+//            (len <= rhs || rhs > 16) && len < 2048, else the nnz mapping.
+// Counters are bumped once per entry after all rhs of the entry have landed
+// (s_waitcnt vmcnt(0) orders the atomics, as in k_trsv_push).  Sums are added
+// in arrival order: within the fp64 bound, exact on integer systems.
+constexpr int kOptNnz = 1, kOptRhs = 2, kOptAuto = 3;
+
+template <int kOpt>
+__global__ __launch_bounds__(256) void k_trsm_push(
+    const int *__restrict__ colptr, const int *__restrict__ rowidx,
+    const double *__restrict__ val, const int *__restrict__ in_degree, int n, int backward,
+    int rhs, const double *__restrict__ b, double *x, int *done, double *left, unsigned *ctl)
+{
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = ld_sc1_i32((const int *)&ctl[kAbort]) ? n : (int)atomicAdd(&ctl[0], 1u);
+        t = __shfl(t, 0, 64);
+        if (t >= n) return;
+        const int i = backward ? n - 1 - t : t;
+        const int a = colptr[i], e = colptr[i + 1];
+        const double diag = val[backward ? e - 1 : a];
+        const int need = in_degree[i] - 1;
+        int bail = 0;
+        if (lane == 0) {
+            unsigned spins = 0;
+            while (ld_sc1_i32(&done[i]) != need) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 1023u) == 0) {
+                    if (spins > kSpinLimit) atomicOr(&ctl[kAbort], 1u);
+                    if (ld_sc1_i32((const int *)&ctl[kAbort])) {
+                        bail = 1;
+                        break;
+                    }
+                }
+            }
+        }
+        if (__shfl(bail, 0, 64)) return;
+        const int lo = backward ? a : a + 1, hi = backward ? e - 1 : e;
+        const int len = hi - lo;
+        const bool by_rhs = kOpt == kOptRhs ||
+                            (kOpt == kOptAuto && (len <= rhs || rhs > 16) && len < 2048);
+        const size_t xi = (size_t)i * rhs;
+        for (int kc = 0; kc < rhs; kc += 64) {
+            const int k = kc + lane;
+            if (k >= rhs) break;
+            const double xk = (b[xi + k] - ld_sc1_f64(&left[xi + k])) / diag;
+            __hip_atomic_store(&x[xi + k], xk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (by_rhs)
+                for (int j = lo; j < hi; ++j)
+                    (void)__hip_atomic_fetch_add(&left[(size_t)rowidx[j] * rhs + k], xk * val[j],
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!by_rhs)
+            for (int j = lo + lane; j < hi; j += 64) {
+                const size_t r = (size_t)rowidx[j] * rhs;
+                const double v = val[j];
+                for (int k = 0; k < rhs; ++k)
+                    (void)__hip_atomic_fetch_add(&left[r + k], ld_sc1_f64(&x[xi + k]) * v,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int j = lo + lane; j < hi; j += 64)
+            (void)__hip_atomic_fetch_add(&done[rowidx[j]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---- level-set executor (algo 2; findlevel.h:71-147's level sets) --------
 // Rows are solved level by level: every row of level l depends only on rows
 // of levels < l, so no ready flags are needed -- a level boundary is a kernel
@@ -870,6 +948,46 @@ int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, 
     return SBLAS_OK;
 }
 
+int sblas_trsv_solve_rhs_opt(sblas_trsv T, int algo, int opt, int rhs, const double *d_b,
+                             double *d_x, void *stream)
+{
+    if (!T || !d_b || !d_x || rhs <= 0 || algo < 0 || algo > 1) return SBLAS_ERR_INVALID;
+    if (algo == 1) return sblas_trsv_solve_rhs(T, rhs, d_b, d_x, stream);
+    if (opt < kOptNnz || opt > kOptAuto) return SBLAS_ERR_INVALID;
+    if (T->n == 0) return SBLAS_OK;
+    DeviceGuard g(T->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = (size_t)T->n * rhs;
+    if (need > T->left_rhs_cap) {
+        if (T->left_rhs) SBLAS_HIP(hipFree(T->left_rhs));
+        T->left_rhs = nullptr;
+        T->left_rhs_cap = 0;
+        SBLAS_HIP(hipMalloc(&T->left_rhs, sizeof(double) * need));
+        T->left_rhs_cap = need;
+    }
+    SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
+    SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
+    SBLAS_HIP(hipMemsetAsync(T->left_rhs, 0, sizeof(double) * need, s));
+    const int grid = grid_for(T->device);
+#define SBLAS_TRSM_PUSH(O)                                                                        \
+    hipLaunchKernelGGL(k_trsm_push<O>, dim3(grid), dim3(256), 0, s, T->colptr, T->rowidx, T->val, \
+                       T->in_degree, T->n, T->substitution, rhs, d_b, d_x, T->done, T->left_rhs,  \
+                       T->ctl)
+    if (opt == kOptNnz) SBLAS_TRSM_PUSH(kOptNnz);
+    else if (opt == kOptRhs) SBLAS_TRSM_PUSH(kOptRhs);
+    else SBLAS_TRSM_PUSH(kOptAuto);
+#undef SBLAS_TRSM_PUSH
+    SBLAS_HIP(hipGetLastError());
+    unsigned h[kCtlBytes / 4] = {0};
+    SBLAS_HIP(hipMemcpyAsync(h, T->ctl, kCtlBytes, hipMemcpyDeviceToHost, s));
+    SBLAS_HIP(hipStreamSynchronize(s));
+    if (h[kAbort]) {
+        set_error("sptrsm: spin limit exceeded (matrix not triangular or missing diagonal?)");
+        return SBLAS_ERR_HIP;
+    }
+    return SBLAS_OK;
+}
+
 int sblas_trsv_levels(sblas_trsv T, int *nlevel)
 {
     if (!T || !nlevel) return SBLAS_ERR_INVALID;
@@ -901,6 +1019,7 @@ int sblas_trsv_destroy(sblas_trsv T)
         (void)hipFree(T->rval);
         (void)hipFree(T->done);
         (void)hipFree(T->left);
+        (void)hipFree(T->left_rhs);
         (void)hipFree(T->ctl);
         (void)hipFree(T->lrow);
         (void)hipFree(T->lrp);

@@ -89,6 +89,7 @@ _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
 _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
 _sig("sblas_trsv_solve_rhs", _i, _p, _i, _p, _p, _p)
+_sig("sblas_trsv_solve_rhs_opt", _i, _p, _i, _i, _i, _p, _p, _p)
 _sig("sblas_trsv_mgpu_solve_tasks", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _i, _i, _p)
 _sig("sblas_sptrsv_syncfree_v3", _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _i)
 _sig("sblas_spmv_ooc", _i, _i, _i, _ll, _d, _p, _p, _p, _p, _d, _p, _i, _ll, _i, _p)
@@ -492,6 +493,12 @@ class DeviceTRSV:
     def solve_rhs(self, rhs: int, b_ptr: int, x_ptr: int, stream=None) -> None:
         """SpTRSM: b, x device n x rhs row-major."""
         check(lib.sblas_trsv_solve_rhs(self.h, rhs, b_ptr, x_ptr, stream), "trsv_solve_rhs")
+
+    def solve_rhs_opt(self, algo: int, opt: int, rhs: int, b_ptr: int, x_ptr: int, stream=None) -> None:
+        """algo 0: reference push dataflow with lane mapping opt (1 nnz, 2 rhs, 3 auto);
+        algo 1: pull executor."""
+        check(lib.sblas_trsv_solve_rhs_opt(self.h, algo, opt, rhs, b_ptr, x_ptr, stream),
+              "trsv_solve_rhs_opt")
 
     def levels(self) -> int:
         n = C.c_int()

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--algos", default="xsort,panel,rowsplit")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--floor", action="store_true",
+                    help="also time a cold streaming read of the slice's byte count")
     args = ap.parse_args()
 
     import torch
@@ -64,9 +66,42 @@ def main():
                         ts.append((e0, e1))
                     torch.cuda.synchronize()
                     out[mode + "_us"] = round(float(np.median([a.elapsed_time(b) for a, b in ts[2:]])) * 1e3, 1)
+                # cold as bench.py times it at N = 1: read-only 1 GiB sweep,
+                # then the call's device span (runtime events at the first
+                # kernel's start and the last kernel's end)
+                spans = []
+                for k in range(args.reps + 2):
+                    scrub.sum(dtype=torch.int64)
+                    torch.cuda.synchronize()
+                    spans.append(A.spmv_timed(algos[name], 1.0, x.data_ptr(), 0.5, y.data_ptr(),
+                                              stream.cuda_stream))
+                out["cold_span_us"] = round(float(np.median(spans[2:])) * 1e3, 1)
+                out["cold_span_min_us"] = round(float(np.min(spans[2:])) * 1e3, 1)
             A.close()
             print(json.dumps({"world": world, "algo": name, "local_rows": int(len(lrp) - 1),
                               "local_nnz": int(lrp[-1]), **out}), flush=True)
+        if args.floor:
+            # streaming floor for the slice's bytes: a cold torch sum over a
+            # buffer of the slice's algorithmic size (stream events)
+            nbytes = 12 * int(lrp[-1]) + 4 * len(lrp) + 8 * n + 16 * (len(lrp) - 1)
+            buf = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
+            ts = []
+            with torch.cuda.stream(stream):
+                for k in range(args.reps + 2):
+                    scrub.sum(dtype=torch.int64)
+                    torch.cuda.synchronize()
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    buf.sum()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+            us = float(np.median(ts[2:])) * 1e3
+            print(json.dumps({"world": world, "floor": "torch sum over the slice's bytes, cold",
+                              "bytes": nbytes, "us": round(us, 1),
+                              "gbps": round(nbytes / us / 1e3, 1)}), flush=True)
+            del buf
 
 
 if __name__ == "__main__":

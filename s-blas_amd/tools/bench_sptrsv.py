@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rhs", default="",
                     help="comma list of rhs counts for the SpTRSM executor (x, b n x rhs)")
+    ap.add_argument("--no-push-rhs", action="store_true",
+                    help="time only the pull executor for --rhs")
     ap.add_argument("--mgpu", default="",
                     help="comma list of block counts for the multi-device executor "
                          "(blocks wrap onto the visible GPUs; kernel wall time reported)")
@@ -85,21 +87,27 @@ def main():
         dX = torch.from_numpy(X).to(dev)
         dB = torch.from_numpy(B).to(dev)
         dXs = torch.zeros_like(dB)
-        with torch.cuda.stream(s):
-            T.solve_rhs(r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
-            torch.cuda.synchronize()
-            ms = []
-            for _ in range(args.steps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                T.solve_rhs(r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
-                e1.record(s)
+        # pull executor, then the reference's push dataflow with each lane
+        # mapping (opt 1 = OPT_WARP_NNZ, 2 = OPT_WARP_RHS, 3 = OPT_WARP_AUTO)
+        for name, algo, opt in ((f"trsm_pull_rhs{r}", 1, 0), (f"trsm_push_nnz_rhs{r}", 0, 1),
+                                (f"trsm_push_rhs_rhs{r}", 0, 2), (f"trsm_push_auto_rhs{r}", 0, 3)):
+            if algo == 0 and args.no_push_rhs:
+                continue
+            with torch.cuda.stream(s):
+                T.solve_rhs_opt(algo, opt, r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
                 torch.cuda.synchronize()
-                ms.append(e0.elapsed_time(e1))
-        t = float(np.median(ms))
-        res[f"trsm_pull_rhs{r}"] = {
-            "ms": round(t, 4), "gflops": round(2.0 * nnz * r / t / 1e6, 3),
-            "rel_l1_vs_xref": float((dXs - dX).abs().sum() / dX.abs().sum())}
+                ms = []
+                for _ in range(args.steps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    T.solve_rhs_opt(algo, opt, r, dB.data_ptr(), dXs.data_ptr(), s.cuda_stream)
+                    e1.record(s)
+                    torch.cuda.synchronize()
+                    ms.append(e0.elapsed_time(e1))
+            t = float(np.median(ms))
+            res[name] = {
+                "ms": round(t, 4), "gflops": round(2.0 * nnz * r / t / 1e6, 3),
+                "rel_l1_vs_xref": float((dXs - dX).abs().sum() / dX.abs().sum())}
         del dX, dB, dXs
     T.close()
     for g in [int(t) for t in args.mgpu.split(",") if t]:

@@ -472,6 +472,62 @@ def test_sptrsm_kat(torch_cuda, sb, name, sub, rhs):
         assert np.array_equal(x, X)
 
 
+@pytest.mark.parametrize("opt", [1, 2, 3], ids=["warp_nnz", "warp_rhs", "warp_auto"])
+@pytest.mark.parametrize("rhs", [1, 3, 17, 64, 100])
+def test_sptrsm_push_lane_mappings(torch_cuda, sb, opt, rhs):
+    """The reference's SpTRSM push dataflow with each `opt` lane mapping
+    (sptrsv_syncfree_cuda.h:229-281) on the KAT matrices (integer systems:
+    exact whatever the atomic order) and on a 300k banded system (against the
+    pull executor, fp64 bound)."""
+    torch = torch_cuda
+    for name, sub in (("qh768", "fwd"), ("ash85", "bwd"), ("qh768", "bwd")):
+        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
+        cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
+        n = len(cp) - 1
+        X = np.random.default_rng(rhs + opt).integers(1, 11, (n, rhs)).astype(np.float64)
+        B = csc_matmat(cp, ri, cv, X)
+        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, B)]
+        xd = torch.zeros((n, rhs), dtype=torch.float64, device="cuda")
+        T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                          0 if sub == "fwd" else 1)
+        for _ in range(2):  # scratch reuse
+            xd.fill_(-1.0)
+            T.solve_rhs_opt(0, opt, rhs, d[3].data_ptr(), xd.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(xd.cpu().numpy(), X), (name, sub)
+        T.close()
+    n, k = 300_000, 4 if rhs > 4 else rhs
+    cp, ri, v, b1, _ = _banded_system(sb, n)
+    Bk = np.repeat(b1[:, None], k, axis=1) * (1.0 + np.arange(k))[None, :]
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, v, Bk)]
+    T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 0)
+    xp = torch.zeros((n, k), dtype=torch.float64, device="cuda")
+    xq = torch.zeros((n, k), dtype=torch.float64, device="cuda")
+    T.solve_rhs_opt(0, opt, k, d[3].data_ptr(), xp.data_ptr())
+    T.solve_rhs_opt(1, opt, k, d[3].data_ptr(), xq.data_ptr())
+    torch.cuda.synchronize()
+    T.close()
+    p, q = xp.cpu().numpy(), xq.cpu().numpy()
+    assert np.abs(p - q).sum() / np.abs(q).sum() < 1e-12
+
+
+@pytest.mark.parametrize("opt", [1, 2])
+def test_sptrsm_reference_api_push(torch_cuda, sb, capfd, opt):
+    """sptrsv_syncfree_cuda with rhs > 1 and an explicit lane mapping runs the
+    reference's push executor; exact on the integer KAT system."""
+    g = np.load(os.path.join(GOLDEN, "trsv_ash85_fwd.npz"))
+    cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
+    n, rhs = len(cp) - 1, 6
+    X = np.random.default_rng(2).integers(1, 11, (n, rhs)).astype(np.float64)
+    B = csc_matmat(cp, ri, cv, X)
+    x = np.zeros((n, rhs))
+    gf = np.zeros(1)
+    rc = sb.lib.sblas_sptrsv_syncfree(sb.ptr(cp), sb.ptr(ri), sb.ptr(cv), n, n, len(ri), 0,
+                                      rhs, opt, sb.ptr(x), sb.ptr(B), sb.ptr(X), sb.ptr(gf), 1)
+    assert rc == 0 and np.array_equal(x, X)
+    assert "executor passed!" in capfd.readouterr().out
+
+
 def test_sptrsm_reference_api(torch_cuda, sb, capfd):
     g = np.load(os.path.join(GOLDEN, "trsv_qh768_fwd.npz"))
     cp, ri, cv = g["colptr"], g["rowidx"], g["val"]

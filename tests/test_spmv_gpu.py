@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 # with each other), and PAIR=0 runs one sub-item per workgroup.  Q = 2 / 3
 # column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
 # cover the wide sub-items' group ranges and the narrow wrap at q > 1.
-ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
+ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
@@ -35,7 +35,7 @@ ALGOS = [(1, {}), (2, {}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANE
          (5, {"SBLAS_XS_K24": "2"}), (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K24": "0"})]
-ALGO_IDS = ["rowsplit", "csr5", "panel", "panel3", "panel8", "xsort", "xsort_w50",
+ALGO_IDS = ["rowsplit", "csr5", "csr5_hostplan", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_k24", "xsort_k24_w50", "xsort_k24_q3_w50", "xsort_k24_u2_w50", "xsort_k32"]
@@ -147,6 +147,42 @@ def test_edge_shapes(torch_cuda, sb, orc, algo):
     y0 = rng.standard_normal(m)
     got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, 1.0, 1.0, y0)
     check(orc, rp, col, val, x, 1.0, 1.0, y0, got)
+
+
+@pytest.mark.parametrize("case", ["ragged", "empty_runs", "tile_rows", "synth"])
+def test_csr5_device_plan_matches_host_plan(torch_cuda, sb, orc, monkeypatch, case):
+    """CSR5 tile descriptors built on the device (row-start bits, tile rows,
+    empty-row segment lists; format_cuda.h:21-300's job) give the same y, bit
+    for bit, as the host-built descriptors (SBLAS_CSR5_HOSTPLAN=1)."""
+    rng = np.random.default_rng(11)
+    if case == "ragged":
+        m, n = 3000, 40000
+        rp, col, val = random_csr(rng, m, n, 60, long_rows=[(5, 2049), (17, 8192), (900, 30000)])
+    elif case == "empty_runs":  # long runs of empty rows inside and across tiles
+        m, n = 20000, 5000
+        lens = np.zeros(m, np.int64)
+        live = rng.choice(m, 900, replace=False)
+        lens[live] = rng.integers(1, 40, 900)
+        lens[-1] = 3000
+        rp = np.concatenate([[0], np.cumsum(lens)])
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    elif case == "tile_rows":  # rows of exactly one tile, and of 1 / 16 entries
+        m, n = 600, 3000
+        lens = rng.choice([1, 16, 1024, 0], m)
+        rp = np.concatenate([[0], np.cumsum(lens)])
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    else:
+        m = n = 20000
+        rp, col, val = orc.gen_synth(n)
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    got = run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 1.5, 0.5, y0)
+    monkeypatch.setenv("SBLAS_CSR5_HOSTPLAN", "1")
+    want = run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 1.5, 0.5, y0)
+    assert np.array_equal(got, want)
+    check(orc, rp, col, val, x, 1.5, 0.5, y0, got)
 
 
 def test_repeat_deterministic(torch_cuda, sb, orc):
