@@ -369,6 +369,26 @@ def main() -> int:
                            "roofline_frac": round(local_bytes / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "cache": "cold"}
     del scrub
+    copy_peak = None
+    if world == 1:
+        # a STREAM-copy peak measured on this box, reported
+        # beside the 8 TB/s spec (torch copy of 512 MiB -> 512 MiB: 1 GiB
+        # moved, past the 256 MB Infinity Cache; best of 5, stream events)
+        src = torch.ones(1 << 26, dtype=torch.float64, device=dev)
+        dst = torch.empty_like(src)
+        best = None
+        with torch.cuda.stream(stream):
+            dst.copy_(src)
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                dst.copy_(src)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                t = e0.elapsed_time(e1)
+                best = t if best is None else min(best, t)
+        copy_peak = 2.0 * src.numel() * 8 / (best * 1e-3) / 1e9
+        del src, dst
 
     check = None
     if args.check:
@@ -444,6 +464,11 @@ def main() -> int:
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
             },
+            **({"measured_copy_peak": {
+                "GBps": round(copy_peak, 1),
+                "frac": round(achieved / copy_peak, 4),
+                "how": "torch copy 512 MiB -> 512 MiB on this GPU, best of 5 (SURVEY M1-roof)"}}
+               if copy_peak else {}),
             "kernel_ms": round(kern_ms, 5),
             "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
             "kernel_only_gflops": round(total_flops / (kern_ms_max * 1e-3) / 1e9, 3),

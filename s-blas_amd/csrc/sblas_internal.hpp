@@ -230,6 +230,7 @@ struct XsPlan {
     bool pair = true;            // items pair two sub-items (two teams of waves)
     int split = 8;               // waves of a pair's first team (of 16)
     bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
+    int u = 1;                   // chunks per dynamic claim (planner; SBLAS_XS_U)
     bool ready = false;
 };
 

@@ -1088,6 +1088,14 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         P.nitems += P.qlen[k];
     }
     P.grid = std::min(P.nitems, resident);
+    // chunks per dynamic claim: one (finer claims balance the waves and
+    // shorten the last stage; rank 0's cyclic slice of config 2, cold span,
+    // U = 1 vs 2: N = 1 130.4 vs 134.3 us, N = 2 77.2 vs 82.7, N = 4 51.3 vs
+    // 57.0, N = 8 35.6 vs 41.3; profiles/r02/slice/).  SBLAS_XS_U forces it.
+    {
+        const char *ue = getenv("SBLAS_XS_U");
+        P.u = ue ? std::max(1, std::min(4, atoi(ue))) : 1;
+    }
     int nstat = 0;
     for (int k = 0; k < 8; ++k) {
         const int blocks_k = P.grid > k ? (P.grid - k + 7) / 8 : 0;  // blocks b < grid with b % 8 == k
@@ -1227,10 +1235,9 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     } else {
         kern = b ? k_spmv_xsort<true, 0, W, false> : k_spmv_xsort<false, 0, W, false>;
     }
-    static const int xu = [] {  // experiments: chunks per pipeline stage (dynamic claims)
-        const char *e = getenv("SBLAS_XS_U");
-        return e ? atoi(e) : kXsUnroll;
-    }();
+    const int xu = P.u;  // chunks per dynamic claim (planner; SBLAS_XS_U)
+    if (P.pair && P.dyn && !b && xu == 1 && mode == 0)
+        kern = k_spmv_xsort<false, 0, W, true, 8, false, true, 1>;
     if (P.pair && P.dyn && b && (xu != kXsUnroll || (mode & 4))) {
 #define XS_DYN(M, U) k_spmv_xsort<true, M, W, true, 8, false, true, U>
         const int mm = mode & 6;
