@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -221,12 +222,57 @@ __global__ __launch_bounds__(kRxThreads, 2) void k_rx_scatter(
 // group's size, so LDS work per element is O(waves), not O(digits).
 constexpr int kRx2MaxDigits = 2048;
 constexpr int kRx2CountSplit = 8;  // count workgroups per scatter workgroup segment
+// scatter workgroup size: 512 threads = 8 waves, 8 entries per thread of a
+// 4096-entry tile (256 threads left only 8 waves per CU at 71 KiB of LDS)
+#ifndef SBLAS_R2_THREADS
+#define SBLAS_R2_THREADS 512
+#endif
+constexpr int kR2Threads = SBLAS_R2_THREADS;
 
-// counts[d][wg] of each scatter workgroup's segment: kRx2CountSplit small
+// Segments.  kSegTiles: workgroup w's contiguous tiles [w*S, (w+1)*S), counts
+// indexed [digit][w].  kSegBuckets (the MSD passes): workgroup w = b*J + j
+// takes part j of J of bucket b, the bucket's range read off the previous
+// pass's scanned counts (bucket b = entries [Jp*b, Jp*b + Jp) of prev), and
+// counts are indexed [(b*D + digit)*J + j], so one inclusive scan of them,
+// bucket-major, yields the stable partition of every bucket by the digit.
+constexpr int kSegTiles = 0, kSegBuckets = 1;
+
+struct SegArgs {
+    int S, nwg;               // kSegTiles
+    const int *prev;          // kSegBuckets: previous pass's inclusive scan
+    int Jp, J;
+    int nb;                   // kSegFinal: number of buckets (grid-stride)
+};
+
+__device__ __forceinline__ void seg_range(int mode, const SegArgs &g, int wg, long long nnz, long long &s0,
+                                          long long &s1)
+{
+    if (mode == kSegTiles) {
+        s0 = (long long)wg * g.S * kRxTile;
+        s1 = min(nnz, s0 + (long long)g.S * kRxTile);
+        if (s0 > s1) s0 = s1;
+        return;
+    }
+    const int b = wg / g.J, j = wg % g.J;
+    const long long i0 = (long long)b * g.Jp;
+    const long long bs = i0 ? g.prev[i0 - 1] : 0, be = g.prev[i0 + g.Jp - 1];
+    const long long len = be - bs;
+    s0 = bs + len * j / g.J;
+    s1 = bs + len * (j + 1) / g.J;
+}
+
+__device__ __forceinline__ size_t seg_count_idx(int mode, const SegArgs &g, int wg, int D, int d)
+{
+    if (mode == kSegTiles) return (size_t)d * g.nwg + wg;
+    return ((size_t)(wg / g.J) * D + d) * g.J + (wg % g.J);
+}
+
+// counts of each scatter workgroup's segment: kRx2CountSplit small
 // workgroups per segment (8 KiB LDS each, many per CU), 16 keys in flight per
 // thread, histograms merged with global atomics (counts zeroed first).
+template <int kSeg>
 __global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict__ keys, long long nnz,
-                                                          int shift, int rb, int S, int nwg,
+                                                          int shift, int rb, SegArgs g,
                                                           int *__restrict__ counts)
 {
     __shared__ int h[kRx2MaxDigits];
@@ -234,8 +280,8 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict_
     for (int d = threadIdx.x; d < D; d += kRxThreads) h[d] = 0;
     __syncthreads();
     const int wg = (int)blockIdx.x / kRx2CountSplit, part = (int)blockIdx.x % kRx2CountSplit;
-    const long long seg0 = (long long)wg * S * kRxTile;
-    const long long seg1 = min(nnz, seg0 + (long long)S * kRxTile);
+    long long seg0, seg1;
+    seg_range(kSeg, g, wg, nnz, seg0, seg1);
     const long long len = max(0LL, seg1 - seg0);
     const long long p0 = seg0 + len * part / kRx2CountSplit, p1 = seg0 + len * (part + 1) / kRx2CountSplit;
     constexpr int kU = 16;
@@ -252,7 +298,7 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict_
     }
     __syncthreads();
     for (int dd = threadIdx.x; dd < D; dd += kRxThreads)
-        if (h[dd]) atomicAdd(&counts[(size_t)dd * nwg + wg], h[dd]);
+        if (h[dd]) atomicAdd(&counts[seg_count_idx(kSeg, g, wg, D, dd)], h[dd]);
 }
 
 // Scatter: workgroup b sorts tiles [b*S, (b+1)*S) in order.  Wave w ranks
@@ -262,29 +308,32 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict_
 // from RB ballots.  Two barriers per tile then turn the per-wave counts into
 // the tile's digit offsets.  The next tile's (key, row, value) are loaded
 // into registers while the current one is ranked and written.
-template <int kMaxD>
-__global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
+// kSegFinal (the MSD transpose's last pass): workgroup b owns bucket b of the
+// previous pass whole (its entries share every column bit above `rb`), counts
+// its digits itself, so its output is the contiguous run [s0, s1) in column
+// order; it writes colptr for its 2^rb columns, and keys only if kout.
+constexpr int kSegFinal = 2;
+
+template <int kMaxD, int kSeg, int kT>
+__global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
-    int shift, int rb, int S, int nwg, const int *__restrict__ incl, int *__restrict__ kout,
-    int *__restrict__ rout, double *__restrict__ vout)
+    int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
+    int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n)
 {
-    __shared__ int wcnt[kRxWaves][kMaxD];  // per-wave counts, then per-wave starts
+    constexpr int kW = kT / 64;  // waves
+    __shared__ int wcnt[kW][kMaxD];  // per-wave counts, then per-wave starts
     __shared__ int lstart[kMaxD], gbase[kMaxD];
-    __shared__ int wtot[kRxWaves];
+    __shared__ int wtot[kW];
     __shared__ int skey[kRxTile], srow[kRxTile];
     __shared__ double sval[kRxTile];
-    constexpr int kQ = kRxTile / kRxWaves;  // elements per wave per tile (1024)
+    constexpr int kQ = kRxTile / kW;  // elements per wave per tile
     constexpr int kB = kQ / 64;             // batches per wave (16)
-    static_assert(kB == kRxItems, "one register slot per batch");
+    static_assert(kB * kT == kRxTile, "one register slot per batch");
     const int D = 1 << rb, dm = D - 1;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int d = t; d < D; d += kRxThreads) {
-        const size_t idx = (size_t)d * nwg + blockIdx.x;
-        gbase[d] = idx ? incl[idx - 1] : 0;  // exclusive start of this workgroup's run of d
-#pragma unroll
-        for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] = 0;
-    }
+    long long s0, s1;
+    seg_range(kSeg == kSegFinal ? kSegBuckets : kSeg, sg, (int)blockIdx.x, nnz, s0, s1);
     int kk[kB], rr[kB];
     double vv[kB];
     auto load_tile = [&](long long base, int valid) {
@@ -298,11 +347,10 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
             vv[j] = ok ? vin[gi] : 0.0;
         }
     };
-    long long base = (long long)blockIdx.x * S * kRxTile;
-    int valid = base < nnz ? (int)min((long long)kRxTile, nnz - base) : 0;
-    if (valid > 0) load_tile(base, valid);
-    __syncthreads();
-    for (int st = 0; st < S && valid > 0; ++st) {  // valid: workgroup-uniform
+    // Steps 1-5 on the tile in registers (valid entries); the tile at
+    // (nbase, nvalid) is loaded into the registers between staging and
+    // write-out; gbase[] then points past this tile's runs.
+    auto process_tile = [&](int valid, long long nbase, int nvalid) {
         int lp[kB];
         // 1. wave-private ranking
 #pragma unroll
@@ -318,10 +366,10 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
             if (rank == 0) wcnt[w][d] += __popcll(mm);
         }
         // padding (top digit, after every real element) is not part of the output
-        if (t == kRxThreads - 1 && valid < kRxTile) wcnt[kRxWaves - 1][dm] -= kRxTile - valid;
+        if (t == kT - 1 && valid < kRxTile) wcnt[kW - 1][dm] -= kRxTile - valid;
         __syncthreads();
         // 2. digit totals, per-wave starts inside each digit, exclusive scan
-        constexpr int kPer = (kMaxD + kRxThreads - 1) / kRxThreads;
+        constexpr int kPer = (kMaxD + kT - 1) / kT;
         int tot[kPer];
         int sum = 0;
 #pragma unroll
@@ -330,7 +378,7 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
             int c = 0;
             if (d < D) {
 #pragma unroll
-                for (int q = 0; q < kRxWaves; ++q) {
+                for (int q = 0; q < kW; ++q) {
                     const int v = wcnt[q][d];
                     wcnt[q][d] = c;  // this wave's start within digit d
                     c += v;
@@ -350,7 +398,7 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
             if (d < D) {
                 lstart[d] = ex;
 #pragma unroll
-                for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] += ex;  // absolute tile position
+                for (int q = 0; q < kW; ++q) wcnt[q][d] += ex;  // absolute tile position
             }
             ex += tot[k];
         }
@@ -367,28 +415,116 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_scatter(
         }
         __syncthreads();
         // 4. prefetch the next tile, write this one out as per-digit runs
-        const long long nbase = base + kRxTile;
-        const int nvalid = (st + 1 < S && nbase < nnz) ? (int)min((long long)kRxTile, nnz - nbase) : 0;
         if (nvalid > 0) load_tile(nbase, nvalid);
-        for (int li = t; li < valid; li += kRxThreads) {
+        for (int li = t; li < valid; li += kT) {
             const int k = skey[li];
             const int d = (k >> shift) & dm;
             const long long g = (long long)gbase[d] + (li - lstart[d]);
-            kout[g] = k;
+            if (kout) kout[g] = k;
             rout[g] = srow[li];
             vout[g] = sval[li];
         }
         __syncthreads();
         // 5. the next tile appends after this one; counters restart
-        for (int d = t; d < D; d += kRxThreads) {
+        for (int d = t; d < D; d += kT) {
             const int nxt = d < dm ? lstart[d + 1] : valid;
             gbase[d] += nxt - lstart[d];
 #pragma unroll
-            for (int q = 0; q < kRxWaves; ++q) wcnt[q][d] = 0;
+            for (int q = 0; q < kW; ++q) wcnt[q][d] = 0;
         }
         __syncthreads();
-        base = nbase;
-        valid = nvalid;
+    };
+    long long base = s0;
+    int valid = base < s1 ? (int)min((long long)kRxTile, s1 - base) : 0;
+    if (valid > 0) load_tile(base, valid);
+    if constexpr (kSeg == kSegFinal) {
+        // buckets bk = blockIdx.x, + gridDim.x, ...; each: its own digit
+        // histogram -> exclusive starts -> colptr for its 2^rb columns, then
+        // its tiles; the next bucket's first tile is loaded while the last
+        // tile of this one is written.  A one-tile bucket counts from the
+        // registers of its tile, a longer one reads its keys first.
+        static_assert(kMaxD <= kT, "one digit per thread");
+        if (blockIdx.x == 0 && t == 0) colptr[n] = (int)nnz;
+        int bk = (int)blockIdx.x;
+        while (bk < sg.nb) {
+            if (t < D) gbase[t] = 0;
+            __syncthreads();
+            if (s1 - s0 <= kRxTile) {
+#pragma unroll
+                for (int j = 0; j < kB; ++j)
+                    if (w * kQ + j * 64 + lane < valid) atomicAdd(&gbase[(kk[j] >> shift) & dm], 1);
+            } else {
+                constexpr int kU = 8;
+                for (long long i0 = s0; i0 < s1; i0 += (long long)kU * kT) {
+                    int d[kU];
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        const long long i = i0 + (long long)u * kT + t;
+                        d[u] = i < s1 ? ((kin[i] >> shift) & dm) : -1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kU; ++u)
+                        if (d[u] >= 0) atomicAdd(&gbase[d[u]], 1);
+                }
+            }
+            __syncthreads();
+            {
+                const int c = t < D ? gbase[t] : 0;
+                const int inc = wave_incl_scan(c);
+                if (lane == 63) wtot[w] = inc;
+                __syncthreads();
+                int ex = inc - c;
+                for (int q = 0; q < w; ++q) ex += wtot[q];
+                if (t < D) {
+                    gbase[t] = (int)s0 + ex;
+                    const long long col = ((long long)bk << rb) + t;
+                    if (col < n) colptr[col] = (int)s0 + ex;
+#pragma unroll
+                    for (int q = 0; q < kW; ++q) wcnt[q][t] = 0;
+                }
+                __syncthreads();
+            }
+            for (;;) {  // the bucket's tiles (all values workgroup-uniform)
+                long long nbase = 0, ns0 = s0, ns1 = s1;
+                int nvalid = 0, nbk = bk;
+                if (base + kRxTile < s1) {
+                    nbase = base + kRxTile;
+                    nvalid = (int)min((long long)kRxTile, s1 - nbase);
+                } else {
+                    nbk = bk + (int)gridDim.x;
+                    if (nbk < sg.nb) {
+                        seg_range(kSegBuckets, sg, nbk, nnz, ns0, ns1);
+                        nbase = ns0;
+                        nvalid = (int)min((long long)kRxTile, ns1 - ns0);
+                    }
+                }
+                if (valid > 0) process_tile(valid, nbase, nvalid);
+                else if (nvalid > 0) load_tile(nbase, nvalid);
+                base = nbase;
+                valid = nvalid;
+                if (nbk != bk) {
+                    bk = nbk;
+                    s0 = ns0;
+                    s1 = ns1;
+                    break;
+                }
+            }
+        }
+    } else {
+        for (int d = t; d < D; d += kT) {
+            const size_t idx = seg_count_idx(kSeg, sg, (int)blockIdx.x, D, d);
+            gbase[d] = idx ? incl[idx - 1] : 0;  // exclusive start of this workgroup's run of d
+#pragma unroll
+            for (int q = 0; q < kW; ++q) wcnt[q][d] = 0;
+        }
+        __syncthreads();
+        while (valid > 0) {  // valid: workgroup-uniform
+            const long long nbase = base + kRxTile;
+            const int nvalid = nbase < s1 ? (int)min((long long)kRxTile, s1 - nbase) : 0;
+            process_tile(valid, nbase, nvalid);
+            base = nbase;
+            valid = nvalid;
+        }
     }
 }
 
@@ -410,6 +546,34 @@ struct TransposeScratch {
 };
 static thread_local TransposeScratch g_tscratch[64];
 
+// MSD transpose (default when n > 2^9): two stable partition passes on the
+// high column bits (pass A over the whole array in fixed tile segments,
+// pass B inside each pass-A bucket), then one pass per final bucket of 2^c
+// columns that counts, ranks and writes the bucket's run in column order
+// together with its colptr entries.  Every pass is a stable partition, so
+// the composition is the stable sort by column (rows ascend in a column).
+// Writes: passes A and B append per-digit runs (2^7 and 2^6 digits: few
+// partially written lines per workgroup); the last pass writes one
+// contiguous run per workgroup and no keys (unless colidx is asked for).
+struct MsdShape {
+    int c = 0, bA = 0, bB = 0;
+};
+
+static MsdShape msd_shape(int nbits, int n, long long nnz)
+{
+    MsdShape m;
+    // final buckets of 2^c columns: the widest whose average fits one
+    // 4096-entry tile with room for the spread (<= 3072 entries), so most
+    // final workgroups count from the registers of their only tile
+    m.c = std::min(8, nbits);
+    while (m.c > 1 && nnz / std::max<long long>(1, ((long long)n + (1LL << m.c) - 1) >> m.c) > 3072) --m.c;
+    if (const char *e = getenv("SBLAS_TRANSPOSE_MSD_C")) m.c = std::max(1, std::min(8, atoi(e)));
+    const int high = nbits - m.c;
+    m.bA = (high + 1) / 2;
+    m.bB = high - m.bA;
+    return m;
+}
+
 int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cval, hipStream_t s,
                      int *colidx)
 {
@@ -421,14 +585,19 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     }
     int nbits = 0;
     while (nbits < 31 && (n - 1) >> nbits) ++nbits;
-    // wide digits (default; SBLAS_TRANSPOSE_RB=8 selects the 8-bit path)
-    // SBLAS_TRANSPOSE_RB=8 selects the one-tile-per-workgroup 8-bit path;
-    // otherwise digits of at most SBLAS_TRANSPOSE_RBMAX bits (default 8: a
+    // algorithm: MSD (default where both high passes exist, i.e. n > 2^9),
+    // SBLAS_TRANSPOSE_ALGO=lsd the LSD passes below, SBLAS_TRANSPOSE_RB=8
+    // the one-tile-per-workgroup 8-bit LSD path
+    const char *alg_e = getenv("SBLAS_TRANSPOSE_ALGO");
+    const char *rb_e = getenv("SBLAS_TRANSPOSE_RB");
+    const int rb_env = rb_e ? atoi(rb_e) : 0;
+    const MsdShape ms = msd_shape(nbits, n, nnz);
+    const bool msd = rb_env != 8 && !(alg_e && !strcmp(alg_e, "lsd")) && ms.bA >= 1 && ms.bB >= 1 &&
+                     ms.bA <= 8 && ms.bB <= 8;
+    // LSD: digits of at most SBLAS_TRANSPOSE_RBMAX bits (default 8: a
     // workgroup's partially written digit runs -- 2^rb per array -- must fit
     // its share of the XCD's L2 until they merge; 11-bit digits measured
     // 0.85 ms per pass against ~0.3 ms), spread evenly over the passes
-    const char *rb_e = getenv("SBLAS_TRANSPOSE_RB");
-    const int rb_env = rb_e ? atoi(rb_e) : 0;
     const char *rbm_e = getenv("SBLAS_TRANSPOSE_RBMAX");
     const int rbmax = std::max(1, std::min(11, rbm_e ? atoi(rbm_e) : 8));
     const bool wide = rb_env != 8;
@@ -447,7 +616,11 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     const int wgcu = wgcu_e ? std::max(1, atoi(wgcu_e)) : 2;
     const int S_t = wide ? std::max(1, (ntiles + ncu * wgcu - 1) / (ncu * wgcu)) : 1;
     const int nwg = (ntiles + S_t - 1) / S_t;
-    const long long ncnt = wide ? (long long)(1 << rb) * nwg : 256LL * ntiles;
+    // MSD pass B: J parts per pass-A bucket, about two workgroups per CU
+    const int JB = msd ? std::max(1, (ncu * wgcu) >> ms.bA) : 1;
+    const long long ncntA = msd ? (long long)(1 << ms.bA) * nwg : 0;
+    const long long ncntB = msd ? (long long)(1 << (ms.bA + ms.bB)) * JB : 0;
+    const long long ncnt = msd ? ncntA + ncntB : (wide ? (long long)(1 << rb) * nwg : 256LL * ntiles);
     const size_t scan_ints = (size_t)(ncnt / kScanTile + 64) * 2;
     // scratch: keysA rowsA valsA | keysB rowsB valsB | counts | scan (+ outputs when null)
     const size_t z = (size_t)nnz;
@@ -474,6 +647,34 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     int *rout_final = rowidx ? rowidx : scan + scan_ints;
     double *vout_final = cval ? cval : (double *)(((uintptr_t)(rout_final + (rowidx ? 0 : z)) + 7) & ~(uintptr_t)7);
     hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
+    if (msd) {
+        int *cntA = counts, *cntB = counts + ncntA;
+        SBLAS_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)ncnt, s));
+        // pass A: the top bA bits, fixed tile segments, (col, expanded row, val) -> set A
+        const int shA = ms.c + ms.bB;
+        const SegArgs gA{S_t, nwg, nullptr, 1, 1};
+        hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s,
+                           A.col, nnz, shA, ms.bA, gA, cntA);
+        SBLAS_TRY(scan_inclusive(cntA, ncntA, scan, s));
+        hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, A.col, rowsB, A.val,
+                           nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n);
+        // pass B: the next bB bits inside each pass-A bucket, set A -> set B
+        const int nwgB = (1 << ms.bA) * JB;
+        const SegArgs gB{0, 0, cntA, nwg, JB};
+        hipLaunchKernelGGL(k_rx2_count<kSegBuckets>, dim3((unsigned)nwgB * kRx2CountSplit), dim3(kRxThreads), 0,
+                           s, keysA, nnz, ms.c, ms.bB, gB, cntB);
+        SBLAS_TRY(scan_inclusive(cntB, ncntB, scan, s));
+        hipLaunchKernelGGL((k_rx2_scatter<256, kSegBuckets, kR2Threads>), dim3(nwgB), dim3(kR2Threads), 0, s, keysA, rowsA,
+                           valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n);
+        // last pass: one workgroup per pass-B bucket (2^c columns), set B -> CSC + colptr
+        const int nbC = 1 << (ms.bA + ms.bB);
+        const SegArgs gC{0, 0, cntB, JB, 1, nbC};
+        hipLaunchKernelGGL((k_rx2_scatter<256, kSegFinal, kR2Threads>), dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
+                           keysB, rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final, vout_final,
+                           colptr, n);
+        SBLAS_HIP(hipGetLastError());
+        return SBLAS_OK;
+    }
     const int *kin = A.col, *rin = rowsB;
     const double *vin = A.val;
     for (int ps = 0; ps < passes; ++ps) {
@@ -485,16 +686,17 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         double *vo = last ? vout_final : ((ps & 1) ? valsB : valsA);
         if (wide) {
             const int sh = rb * ps;
+            const SegArgs gt{S_t, nwg, nullptr, 1, 1};
             SBLAS_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)ncnt, s));
-            hipLaunchKernelGGL(k_rx2_count, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s, kin, nnz,
-                               sh, rb, S_t, nwg, counts);
+            hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s,
+                               kin, nnz, sh, rb, gt, counts);
             SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
             if (rb <= 8)  // 71 KiB of LDS: two workgroups per CU
-                hipLaunchKernelGGL(k_rx2_scatter<256>, dim3(nwg), dim3(kRxThreads), 0, s, kin, rin, vin, nnz, sh, rb,
-                                   S_t, nwg, counts, ko, ro, vo);
+                hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, kin, rin, vin,
+                                   nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n);
             else
-                hipLaunchKernelGGL(k_rx2_scatter<kRx2MaxDigits>, dim3(nwg), dim3(kRxThreads), 0, s, kin, rin, vin, nnz,
-                                   sh, rb, S_t, nwg, counts, ko, ro, vo);
+                hipLaunchKernelGGL((k_rx2_scatter<kRx2MaxDigits, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, kin,
+                                   rin, vin, nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n);
         } else {
             hipLaunchKernelGGL(k_rx_count, dim3(ntiles), dim3(kRxThreads), 0, s, kin, nnz, shift, ntiles, counts);
             SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));

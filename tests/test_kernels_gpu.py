@@ -110,17 +110,23 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "rb11", "rb8"])
-@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "big"])
+@pytest.mark.parametrize("digits", ["default", "msd_c3", "msd_c5", "lsd", "rb11", "rb8"])
+@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
-    """Stable radix transpose: tiles-per-workgroup path with <= 8-bit digits
-    (default; "big" = 3 passes of 8 bits at n = 3M, 2 tiles per workgroup),
-    the same with 11-bit digits, and the one-tile 8-bit path."""
+    """Stable transpose, every path: the MSD partition passes + per-bucket
+    final pass (default where n > 512; SBLAS_TRANSPOSE_MSD_C moves the final
+    bucket width so small matrices take it too, with few, long buckets on
+    "longcols"), the LSD tiles-per-workgroup path with <= 8-bit digits ("big"
+    = 3 passes at n = 3M) and with 11-bit digits, and the one-tile 8-bit path."""
     torch = torch_cuda
     if digits == "rb8":
         monkeypatch.setenv("SBLAS_TRANSPOSE_RB", "8")
+    if digits in ("lsd", "rb11"):
+        monkeypatch.setenv("SBLAS_TRANSPOSE_ALGO", "lsd")
     if digits == "rb11":
         monkeypatch.setenv("SBLAS_TRANSPOSE_RBMAX", "11")
+    if digits.startswith("msd_c"):
+        monkeypatch.setenv("SBLAS_TRANSPOSE_MSD_C", digits[5:])
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
@@ -133,6 +139,9 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
         val = rng.standard_normal(int(rp[-1]))
+    elif case == "wide":  # more columns than rows, many empty columns
+        m, n = 50, 100000
+        rp, col, val = rand_csr(rng, m, n, 400, empty_frac=0.3)
     else:  # columns longer than 32 / 4096 (medium and big sort paths)
         m, n = 9000, 40
         rp, col, val = rand_csr(rng, m, n, 40, empty_frac=0.2)
