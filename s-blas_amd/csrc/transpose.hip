@@ -570,6 +570,7 @@ static MsdShape msd_shape(int nbits, int n, long long nnz)
     if (const char *e = getenv("SBLAS_TRANSPOSE_MSD_C")) m.c = std::max(1, std::min(8, atoi(e)));
     const int high = nbits - m.c;
     m.bA = (high + 1) / 2;
+    if (const char *e = getenv("SBLAS_TRANSPOSE_MSD_A")) m.bA = std::max(1, std::min(high - 1, atoi(e)));
     m.bB = high - m.bA;
     return m;
 }
