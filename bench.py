@@ -24,8 +24,8 @@ beside it under `warm`.
   python bench.py [--gpus N --steps K --warmup W] [--algo auto|xsort|panel|rowsplit|csr5]
                   [--cache cold|warm] [--partition cyclic|nnz]
 
-Default kernel (`auto`): `xsort` while a rank holds >= 8M nonzeros (N <= 4
-for config 2), else `panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
+Default kernel (`auto`): `xsort` while a rank holds >= 2M nonzeros (every N
+<= 8 on config 2, one-chunk claims), else `panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
 (row range x column group) blocks, column groups dealt to the XCDs so every
 x gather stays in the XCD's own L2, lane-consecutive gathers, LDS fp64 row
 accumulators.  Within the fp64 error bound of the sequential row sum but not
@@ -123,7 +123,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--algo", choices=["auto", "rowsplit", "csr5", "panel", "xsort"], default="auto",
-                    help="auto (default): xsort when a rank holds >= 8M nonzeros, else panel "
+                    help="auto (default): xsort when a rank holds >= 2M nonzeros, else panel "
                          "(s-blas_amd/tools/bench_slice.py: per-rank kernel times at N = 1..8)")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
@@ -192,11 +192,13 @@ def main() -> int:
     auto = args.algo == "auto"
     if auto:
         # the column-sorted kernel's per-item costs (padding to 256-entry
-        # chunks, item set-up) pay off on large slices; the XCD-panel row
-        # split wins below ~8M nonzeros per rank.  Its column
-        # groups cover at most 127 x 2^18 columns; past ~120 MiB of x the
-        # panel kernel is used as well.
-        args.algo = "xsort" if nnz / world >= 8e6 and n * 8 <= 120 * 2**20 else "panel"
+        # chunks, item set-up) need a few chunks per wave: with one-chunk
+        # claims it wins at every N <= 8 on config 2 (slice cold spans
+        # 35.6 vs 42.8 us at N = 8, 51.3 vs 70.3 at N = 4), so
+        # the XCD-panel row split is kept for slices under ~2M nonzeros.  Its
+        # column groups cover at most 127 x 2^18 columns; past ~120 MiB of x
+        # the panel kernel is used as well.
+        args.algo = "xsort" if nnz / world >= 2e6 and n * 8 <= 120 * 2**20 else "panel"
     algo = algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
