@@ -154,6 +154,8 @@ struct SpmmPlan {
     unsigned *ct_key = nullptr;
     double *ct_val = nullptr;
     long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets
+    bool ct_own = false;                 // rows owned by waves, plain LDS read-add-write
+    long long *ct_woff = nullptr;        // own: [8*ns*nrb][17] per-wave entry offsets
     double fill_thresh = 0.25;
     bool ready = false;
 };

@@ -495,6 +495,87 @@ __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     }
 }
 
+// Owned-row form (opt-in, SBLAS_SPMM_CTOWN=1; global-column keys).  The C tile's rows are dealt to the 16 waves (balanced by entry
+// count, plan time), each wave walks only the entries of its own rows --
+// column-sorted, in steps of 8 entries with 8 distinct rows -- so no other
+// lane can touch a row between a wave's read and write: the update is a
+// plain ds_read_b128 / add / ds_write_b128 of the lane's two columns instead
+// of two ds_add_f64 (whose atomic read-modify-write costs the LDS ~12 cycles
+// per wave instruction).  Row stride 18 doubles (16-B aligned pairs); rows
+// R .. R+15 are the waves' private sinks for padding entries (value 0).
+constexpr int kCoPad = 18;
+constexpr int kCoWaves = kCtThreads / 64;
+constexpr int kCoMaxRows = 163840 / (kCoPad * 8) - kCoWaves;  // 1121 real rows
+
+template <bool kFast>
+__global__ __launch_bounds__(kCtThreads) void k_spmm_ctown(
+    const unsigned *__restrict__ key, const double *__restrict__ val, const long long *__restrict__ woff,
+    int ns, int nrb, int R, int rbits, int ncg, const double *__restrict__ B, long long ldb, int n, int m,
+    double *__restrict__ part)
+{
+    extern __shared__ double tile[];  // [R + 16][kCoPad]
+    const int x = (int)(blockIdx.x & 7);
+    int rest = (int)(blockIdx.x >> 3);
+    const int cg = rest % ncg;
+    rest /= ncg;
+    const int rb = rest % nrb, ss = rest / nrb;
+    const int slot = x * ns + ss;
+    const int r0 = rb * R, nr = min(R, m - r0);
+    for (int i = threadIdx.x; i < (R + kCoWaves) * kCoPad; i += kCtThreads) tile[i] = 0.0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long bk = (long long)slot * nrb + rb;
+    const long long w0 = woff[bk * (kCoWaves + 1) + wv], w1 = woff[bk * (kCoWaves + 1) + wv + 1];
+    const int g = lane >> 4, h = (lane >> 3) & 1, q = lane & 7;
+    const int myoff = 8 * (lane & 7) + 2 * g + h;
+    const unsigned rmask = (1u << rbits) - 1;
+    const unsigned ldb8 = (unsigned)(ldb * 8);
+    const int c0 = cg * kCtCols + 2 * q;
+    const char *Bc = reinterpret_cast<const char *>(B) + (size_t)c0 * 8;
+    typedef double v2d_t __attribute__((ext_vector_type(2)));
+    for (long long it = w0; it < w1; it += 64) {
+        const long long e = it + myoff;
+        const unsigned kk = key[e];
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(val[e]);
+        const unsigned vlo = (unsigned)vb, vhi = (unsigned)(vb >> 32);
+        unsigned kt[8];
+        kt[0] = ct_bcast<0>(kk); kt[1] = ct_bcast<1>(kk); kt[2] = ct_bcast<2>(kk); kt[3] = ct_bcast<3>(kk);
+        kt[4] = ct_bcast<4>(kk); kt[5] = ct_bcast<5>(kk); kt[6] = ct_bcast<6>(kk); kt[7] = ct_bcast<7>(kk);
+        v2d_t bb[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if constexpr (kFast) {
+                bb[t] = *reinterpret_cast<const v2d_t *>(Bc + (unsigned)(kt[t] >> rbits) * ldb8);
+            } else {  // guarded columns, 64-bit offsets
+                const double *br = B + (long long)(kt[t] >> rbits) * ldb;
+                bb[t].x = c0 < n ? br[c0] : 0.0;
+                bb[t].y = c0 + 1 < n ? br[c0 + 1] : 0.0;
+            }
+        }
+        unsigned lo[8], hi[8];
+        lo[0] = ct_bcast<0>(vlo); lo[1] = ct_bcast<1>(vlo); lo[2] = ct_bcast<2>(vlo); lo[3] = ct_bcast<3>(vlo);
+        lo[4] = ct_bcast<4>(vlo); lo[5] = ct_bcast<5>(vlo); lo[6] = ct_bcast<6>(vlo); lo[7] = ct_bcast<7>(vlo);
+        hi[0] = ct_bcast<0>(vhi); hi[1] = ct_bcast<1>(vhi); hi[2] = ct_bcast<2>(vhi); hi[3] = ct_bcast<3>(vhi);
+        hi[4] = ct_bcast<4>(vhi); hi[5] = ct_bcast<5>(vhi); hi[6] = ct_bcast<6>(vhi); hi[7] = ct_bcast<7>(vhi);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const double vt = __longlong_as_double((long long)(((unsigned long long)hi[t] << 32) | lo[t]));
+            v2d_t *cp = reinterpret_cast<v2d_t *>(&tile[(kt[t] & rmask) * kCoPad + 2 * q]);
+            v2d_t c = *cp;
+            c.x += vt * bb[t].x;
+            c.y += vt * bb[t].y;
+            *cp = c;
+        }
+    }
+    __syncthreads();
+    const int ncol = min(kCtCols, n - cg * kCtCols);
+    double *out = part + ((long long)slot * n + cg * kCtCols) * m + r0;
+    for (int i = threadIdx.x; i < nr * ncol; i += kCtThreads) {
+        const int c = i / nr, r = i - c * nr;
+        out[(long long)c * m + r] = tile[r * kCoPad + c];
+    }
+}
+
 // C = alpha * sum_slot part[slot] (+ beta * C), slots in order
 template <bool kBeta>
 __global__ __launch_bounds__(256) void k_spmm_ctreduce(const double *__restrict__ part, int nslot, int m, int n,
@@ -519,12 +600,19 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     const int m = A.m, k = A.n;
     int wlog = 11;  // 2048 B rows = 1 MiB of B per slab at n = 64
     if (const char *e = getenv("SBLAS_SPMM_CTW")) wlog = std::max(4, std::min(20, atoi(e)));
-    int rmax = kCtMaxRows;  // experiments: SBLAS_SPMM_CTR caps the tile rows
-    if (const char *e = getenv("SBLAS_SPMM_CTR")) rmax = std::max(16, std::min(kCtMaxRows, atoi(e)));
+    // owned-row form (k_spmm_ctown, opt-in SBLAS_SPMM_CTOWN=1: bitwise
+    // repeatable, but measured 0.468 vs 0.370 ms on config 4 -- on gfx950 a
+    // ds_write_b128 costs ~13 LDS cycles of transfer, so read + write of two
+    // columns outweighs two ds_add_f64, and the b128 read groups conflict)
+    bool own = getenv("SBLAS_SPMM_CTOWN") && atoi(getenv("SBLAS_SPMM_CTOWN")) == 1 &&
+               !(getenv("SBLAS_SPMM_CTSLOT") && atoi(getenv("SBLAS_SPMM_CTSLOT")) != 0);
+    const int rcap = own ? kCoMaxRows : kCtMaxRows;
+    int rmax = rcap;  // experiments: SBLAS_SPMM_CTR caps the tile rows
+    if (const char *e = getenv("SBLAS_SPMM_CTR")) rmax = std::max(16, std::min(rcap, atoi(e)));
     const int nrb = (m + rmax - 1) / rmax;
     const int R = (m + nrb - 1) / nrb;
     int rbits = 1;
-    while ((1 << rbits) < R) ++rbits;
+    while ((1 << rbits) < R + (own ? kCoWaves : 0)) ++rbits;  // own: the waves' sink rows too
     const long long nslab = ((long long)k + (1LL << wlog) - 1) >> wlog;
     const long long jc_max = ((nslab + 7) / 8) << wlog;  // XCD-local columns
     if (rbits + 1 > 32 || jc_max > (1LL << (32 - rbits))) return SBLAS_ERR_UNSUPPORTED;
@@ -557,6 +645,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // kernel then needs no slab arithmetic; sorting is the same order
     const bool direct = (long long)k <= (1LL << (32 - rbits)) && !(getenv("SBLAS_SPMM_CTDIRECT") &&
                                                                      atoi(getenv("SBLAS_SPMM_CTDIRECT")) == 0);
+    own = own && direct;
     std::vector<unsigned long long> kv((size_t)std::max<long long>(A.nnz, 1));  // key << 32 | entry index
     {
         std::vector<long long> next(off.begin(), off.end() - 1);
@@ -575,7 +664,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // in parity.  So inside each aligned 8-entry step, odd rows go to the even
     // slots and even rows to the odd slots as far as the step allows (the
     // order inside a step does not change which products are summed).
-    const bool pair_rows = !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
+    const bool pair_rows = !own && !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int b = 0; b < nbk; ++b) {
         std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
@@ -616,6 +705,106 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     }
     bool slots = false;
     if (const char *e = getenv("SBLAS_SPMM_CTSLOT")) slots = atoi(e) != 0 && A.nnz > 0;
+    if (own) {
+        // per bucket: rows dealt to the 16 waves by entry count (longest
+        // first to the least loaded), each wave's entries kept in column
+        // order and cut into steps of 8 entries with 8 distinct rows (an
+        // entry whose row is already in the step waits for the next one;
+        // look-ahead 32), short steps and the list's end padded to whole
+        // 64-entry iterations with value-0 entries on the wave's sink row
+        constexpr int W = kCoWaves;
+        constexpr unsigned kPadIdx = 0xffffffffu;
+        std::vector<std::vector<unsigned long long>> bl((size_t)nbk);
+        std::vector<long long> blen((size_t)nbk * W, 0);  // padded entries per (bucket, wave)
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int b = 0; b < nbk; ++b) {
+            const long long e0 = off[(size_t)b], e1 = off[(size_t)b + 1];
+            const unsigned rm = (1u << rbits) - 1;
+            std::vector<long long> cnt((size_t)R, 0);
+            for (long long e = e0; e < e1; ++e) cnt[(size_t)((unsigned)(kv[(size_t)e] >> 32) & rm)]++;
+            std::vector<int> order((size_t)R);
+            for (int r = 0; r < R; ++r) order[(size_t)r] = r;
+            std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return cnt[(size_t)a] > cnt[(size_t)c]; });
+            std::vector<int> owner((size_t)R, 0);
+            long long load[W] = {0};
+            for (int r : order) {
+                int best = 0;
+                for (int w = 1; w < W; ++w)
+                    if (load[w] < load[best]) best = w;
+                owner[(size_t)r] = best;
+                load[best] += cnt[(size_t)r];
+            }
+            std::vector<std::vector<unsigned long long>> lists(W);
+            for (long long e = e0; e < e1; ++e)
+                lists[(size_t)owner[(size_t)((unsigned)(kv[(size_t)e] >> 32) & rm)]].push_back(kv[(size_t)e]);
+            std::vector<unsigned long long> &out = bl[(size_t)b];
+            for (int w = 0; w < W; ++w) {
+                std::vector<unsigned long long> &L = lists[(size_t)w];
+                const unsigned sink = (unsigned)(R + w);
+                std::vector<char> used(L.size(), 0);
+                size_t head = 0;
+                std::vector<unsigned long long> wl;
+                wl.reserve(L.size() + 64);
+                unsigned lastcol = 0;
+                auto pad = [&]() { wl.push_back(((unsigned long long)((lastcol << rbits) | sink) << 32) | kPadIdx); };
+                while (head < L.size()) {
+                    unsigned rows[8];
+                    int nr8 = 0;
+                    for (size_t i = head; i < L.size() && i < head + 32 && nr8 < 8; ++i) {
+                        if (used[i]) continue;
+                        const unsigned r = (unsigned)(L[i] >> 32) & rm;
+                        bool clash = false;
+                        for (int j = 0; j < nr8; ++j) clash |= rows[j] == r;
+                        if (clash) continue;
+                        rows[nr8++] = r;
+                        used[i] = 1;
+                        wl.push_back(L[i]);
+                        lastcol = (unsigned)(L[i] >> 32) >> rbits;
+                    }
+                    for (int j = nr8; j < 8; ++j) pad();
+                    while (head < L.size() && used[head]) ++head;
+                }
+                while (wl.size() % 64) pad();
+                out.insert(out.end(), wl.begin(), wl.end());
+                blen[(size_t)b * W + w] = (long long)wl.size();
+            }
+        }
+        std::vector<long long> woff((size_t)nbk * (W + 1));
+        long long tot = 0;
+        for (int b = 0; b < nbk; ++b)
+            for (int w = 0; w <= W; ++w) {
+                woff[(size_t)b * (W + 1) + w] = tot;
+                if (w < W) tot += blen[(size_t)b * W + w];
+            }
+        std::vector<unsigned> okey((size_t)std::max<long long>(tot, 1));
+        std::vector<double> oval((size_t)std::max<long long>(tot, 1));
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int b = 0; b < nbk; ++b) {
+            const std::vector<unsigned long long> &v = bl[(size_t)b];
+            long long o = woff[(size_t)b * (W + 1)];
+            for (unsigned long long e : v) {
+                okey[(size_t)o] = (unsigned)(e >> 32);
+                const unsigned idx = (unsigned)(e & 0xffffffffu);
+                oval[(size_t)o] = idx == kPadIdx ? 0.0 : hval[(size_t)idx];
+                ++o;
+            }
+        }
+        SBLAS_HIP(hipMalloc(&P.ct_key, sizeof(unsigned) * okey.size()));
+        SBLAS_HIP(hipMalloc(&P.ct_val, sizeof(double) * oval.size()));
+        SBLAS_HIP(hipMalloc(&P.ct_woff, sizeof(long long) * woff.size()));
+        SBLAS_HIP(hipMemcpy(P.ct_key, okey.data(), sizeof(unsigned) * okey.size(), hipMemcpyHostToDevice));
+        SBLAS_HIP(hipMemcpy(P.ct_val, oval.data(), sizeof(double) * oval.size(), hipMemcpyHostToDevice));
+        SBLAS_HIP(hipMemcpy(P.ct_woff, woff.data(), sizeof(long long) * woff.size(), hipMemcpyHostToDevice));
+        P.ct_own = true;
+        P.ct_slots = false;
+        P.ct_ns = ns;
+        P.ct_nrb = nrb;
+        P.ct_R = R;
+        P.ct_rbits = rbits;
+        P.ct_wlog = wlog;
+        P.ct_direct = direct;
+        return SBLAS_OK;
+    }
     const long long nunits = slots ? soff.back() : A.nnz;
     std::vector<unsigned> hkey((size_t)std::max<long long>(nunits, 1)), hkey2;
     std::vector<double> hv((size_t)std::max<long long>(nunits, 1)), hv2;
@@ -796,6 +985,7 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.ct_off);
     (void)hipFree(P.ct_key2);
     (void)hipFree(P.ct_val2);
+    (void)hipFree(P.ct_woff);
     A.mm = SpmmPlan{};
 }
 
@@ -877,6 +1067,19 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         }
         const bool fast = (ldr % 2 == 0) && (n % kCtCols == 0) && (((uintptr_t)Brow & 15) == 0) &&
                           (unsigned long long)A.n * (unsigned long long)ldr * 8ULL < (1ULL << 32);
+        if (P.ct_own) {
+            static thread_local bool own_attr[64] = {};
+            if (!own_attr[A.device & 63]) {
+                for (const void *kf : {(const void *)k_spmm_ctown<true>, (const void *)k_spmm_ctown<false>})
+                    SBLAS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)(sizeof(double) * (kCoMaxRows + kCoWaves) * kCoPad)));
+                own_attr[A.device & 63] = true;
+            }
+            const size_t lds_o = sizeof(double) * (size_t)(P.ct_R + kCoWaves) * kCoPad;
+            hipLaunchKernelGGL(fast ? k_spmm_ctown<true> : k_spmm_ctown<false>, dim3((unsigned)nwg),
+                               dim3(kCtThreads), lds_o, s, P.ct_key, P.ct_val, P.ct_woff, P.ct_ns, P.ct_nrb,
+                               P.ct_R, P.ct_rbits, ncg, Brow, ldr, n, A.m, S.bt);
+        } else {
         using K = void (*)(const unsigned *, const double *, const unsigned *, const double *, const long long *,
                            int, int, int, int, int, int, const double *, long long, int, int, double *);
         K kern;
@@ -889,6 +1092,7 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_key2,
                            P.ct_val2, P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr,
                            n, A.m, S.bt);
+        }
         const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
         if (beta != 0.0)
             hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,

@@ -120,8 +120,8 @@ def cfg4(orc):
                 want=want, bound=bound)
 
 
-@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ctslot"),
-                                         ("row", "l2slice")])
+@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ctown"),
+                                         ("row", "ctslot"), ("row", "l2slice")])
 def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form):
     """BASELINE configs[3]: C = -0.7 A B + 0.8 C on the rail4284-shaped matrix,
     all 4284 x 64 entries of C checked (B row-major as resident in HBM, and
@@ -132,6 +132,8 @@ def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form)
         monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     if form == "ctslot":
         monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
+    if form == "ctown":  # owned rows (opt-in, bitwise repeatable)
+        monkeypatch.setenv("SBLAS_SPMM_CTOWN", "1")
     c = cfg4
     m, k, n = c["m"], c["k"], c["n"]
     A = sb.DeviceCSR.upload(0, k, c["rp"], c["col"], c["val"])

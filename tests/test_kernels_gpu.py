@@ -33,7 +33,8 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows", "ctslab", "ctslot"])
+@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows", "ctslab", "ctslot",
+                                    "ctown", "ctownrows", "ctownw"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
@@ -42,7 +43,8 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     (forced: "l2" = 3 slices of 2048 columns, "l2w" = 79 slices of 64) and
     the column-sorted C-tile form (forced: "ct" = 3 slabs of 2048 columns,
     one slab set; "ctw" = 313 slabs of 16 columns in 3 sets per XCD;
-    "ctrows" = 2,500 rows, i.e. 3 row blocks of 834)."""
+    "ctrows" = 2,500 rows, i.e. 3 row blocks of 834), in its LDS-atomic form
+    (default) and its owned-row form ("ctown*", opt-in)."""
     torch = torch_cuda
     if splitk in ("0", "1"):
         monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
@@ -57,11 +59,16 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
             monkeypatch.setenv("SBLAS_SPMM_CTDIRECT", "0")
         if splitk == "ctslot":  # column-run slots of two entries (opt-in form)
             monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
+        if splitk.startswith("ctown"):  # owned rows, plain LDS read-add-write
+            monkeypatch.setenv("SBLAS_SPMM_CTOWN", "1")
+        if splitk == "ctownw":
+            monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
+            monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
         if splitk == "ctw":
             monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
             monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
     rng = np.random.default_rng(ncols + 10 * layout)
-    m, k = (2500 if splitk == "ctrows" else 700), 5000
+    m, k = (2500 if splitk in ("ctrows", "ctownrows") else 700), 5000
     rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
     B = rng.standard_normal((k, ncols))
     C0 = rng.standard_normal((m, ncols))
