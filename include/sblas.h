@@ -161,7 +161,9 @@ int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb,
 
 /* Device CSR -> CSC transpose of a handle; outputs DEVICE arrays sized
  * colptr[n+1], rowidx[nnz], cval[nnz]; row indices ascend within columns
- * (bit-exact with tranpose.h:6-43). */
+ * (bit-exact with tranpose.h:6-43).  A stable sort of the entries by column:
+ * MSD partition passes + one pass per final bucket of columns (n > 512), or
+ * LSD radix passes (n <= 512, or SBLAS_TRANSPOSE_ALGO=lsd). */
 int sblas_csr_transpose(sblas_csr A, int *d_colptr, int *d_rowidx,
                         double *d_cval, void *stream);
 

@@ -313,6 +313,7 @@ __global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict_
 // its digits itself, so its output is the contiguous run [s0, s1) in column
 // order; it writes colptr for its 2^rb columns, and keys only if kout.
 constexpr int kSegFinal = 2;
+constexpr int kSegFinalDirect = 3;  // the same, each entry written from registers
 
 template <int kMaxD, int kSeg, int kT>
 __global__ __launch_bounds__(kT) void k_rx2_scatter(
@@ -320,6 +321,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
     int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n)
 {
+    constexpr bool kFinal = kSeg >= kSegFinal;
     constexpr int kW = kT / 64;  // waves
     __shared__ int wcnt[kW][kMaxD];  // per-wave counts, then per-wave starts
     __shared__ int lstart[kMaxD], gbase[kMaxD];
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const unsigned long long lt = (1ull << lane) - 1ull;
     long long s0, s1;
-    seg_range(kSeg == kSegFinal ? kSegBuckets : kSeg, sg, (int)blockIdx.x, nnz, s0, s1);
+    seg_range(kFinal ? kSegBuckets : kSeg, sg, (int)blockIdx.x, nnz, s0, s1);
     int kk[kB], rr[kB];
     double vv[kB];
     auto load_tile = [&](long long base, int valid) {
@@ -403,26 +405,43 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             ex += tot[k];
         }
         __syncthreads();
-        // 3. stage in digit order
+        if constexpr (kSeg == kSegFinalDirect) {
+            // 3'. the last pass writes a bucket's compact run: every entry
+            // straight from its registers to its final place (the run's lines
+            // fill within the tile, so the L2 merges them), no LDS staging
 #pragma unroll
-        for (int j = 0; j < kB; ++j) {
-            if (w * kQ + j * 64 + lane < valid) {
-                const int pos = wcnt[w][(kk[j] >> shift) & dm] + lp[j];
-                skey[pos] = kk[j];
-                srow[pos] = rr[j];
-                sval[pos] = vv[j];
+            for (int j = 0; j < kB; ++j) {
+                if (w * kQ + j * 64 + lane < valid) {
+                    const int d = (kk[j] >> shift) & dm;
+                    const long long g = (long long)gbase[d] + (wcnt[w][d] + lp[j] - lstart[d]);
+                    if (kout) kout[g] = kk[j];
+                    rout[g] = rr[j];
+                    vout[g] = vv[j];
+                }
             }
-        }
-        __syncthreads();
-        // 4. prefetch the next tile, write this one out as per-digit runs
-        if (nvalid > 0) load_tile(nbase, nvalid);
-        for (int li = t; li < valid; li += kT) {
-            const int k = skey[li];
-            const int d = (k >> shift) & dm;
-            const long long g = (long long)gbase[d] + (li - lstart[d]);
-            if (kout) kout[g] = k;
-            rout[g] = srow[li];
-            vout[g] = sval[li];
+            if (nvalid > 0) load_tile(nbase, nvalid);
+        } else {
+            // 3. stage in digit order
+#pragma unroll
+            for (int j = 0; j < kB; ++j) {
+                if (w * kQ + j * 64 + lane < valid) {
+                    const int pos = wcnt[w][(kk[j] >> shift) & dm] + lp[j];
+                    skey[pos] = kk[j];
+                    srow[pos] = rr[j];
+                    sval[pos] = vv[j];
+                }
+            }
+            __syncthreads();
+            // 4. prefetch the next tile, write this one out as per-digit runs
+            if (nvalid > 0) load_tile(nbase, nvalid);
+            for (int li = t; li < valid; li += kT) {
+                const int k = skey[li];
+                const int d = (k >> shift) & dm;
+                const long long g = (long long)gbase[d] + (li - lstart[d]);
+                if (kout) kout[g] = k;
+                rout[g] = srow[li];
+                vout[g] = sval[li];
+            }
         }
         __syncthreads();
         // 5. the next tile appends after this one; counters restart
@@ -437,7 +456,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     long long base = s0;
     int valid = base < s1 ? (int)min((long long)kRxTile, s1 - base) : 0;
     if (valid > 0) load_tile(base, valid);
-    if constexpr (kSeg == kSegFinal) {
+    if constexpr (kFinal) {
         // buckets bk = blockIdx.x, + gridDim.x, ...; each: its own digit
         // histogram -> exclusive starts -> colptr for its 2^rb columns, then
         // its tiles; the next bucket's first tile is loaded while the last
@@ -669,8 +688,12 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
                            valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n);
         // last pass: one workgroup per pass-B bucket (2^c columns), set B -> CSC + colptr
         const int nbC = 1 << (ms.bA + ms.bB);
+        // SBLAS_TRANSPOSE_DIRECT=1: entries written from registers (experiment)
+        const char *de = getenv("SBLAS_TRANSPOSE_DIRECT");
         const SegArgs gC{0, 0, cntB, JB, 1, nbC};
-        hipLaunchKernelGGL((k_rx2_scatter<256, kSegFinal, kR2Threads>), dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
+        auto kfin = (de && atoi(de) == 1) ? k_rx2_scatter<256, kSegFinalDirect, kR2Threads>
+                                          : k_rx2_scatter<256, kSegFinal, kR2Threads>;
+        hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
                            keysB, rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final, vout_final,
                            colptr, n);
         SBLAS_HIP(hipGetLastError());

@@ -1265,6 +1265,8 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else if (P.pair && P.dyn && P.k24)
             kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1, true>
                      : k_spmv_xsort<false, 0, W, true, 8, true, true, 1, true>;
+        else if (P.pair && P.dyn && xu == 1)
+            kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1> : k_spmv_xsort<false, 0, W, true, 8, true, true, 1>;
         else if (P.pair && P.dyn) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true> : k_spmv_xsort<false, 0, W, true, 8, true, true>;
         else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;

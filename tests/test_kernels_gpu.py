@@ -117,7 +117,7 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "msd_c3", "msd_c5", "lsd", "rb11", "rb8"])
+@pytest.mark.parametrize("digits", ["default", "direct", "msd_c3", "msd_c5", "msd_c3_direct", "lsd", "rb11", "rb8"])
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     """Stable transpose, every path: the MSD partition passes + per-bucket
@@ -133,7 +133,9 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     if digits == "rb11":
         monkeypatch.setenv("SBLAS_TRANSPOSE_RBMAX", "11")
     if digits.startswith("msd_c"):
-        monkeypatch.setenv("SBLAS_TRANSPOSE_MSD_C", digits[5:])
+        monkeypatch.setenv("SBLAS_TRANSPOSE_MSD_C", digits[5])
+    if digits.endswith("direct"):  # last pass writes from registers
+        monkeypatch.setenv("SBLAS_TRANSPOSE_DIRECT", "1")
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
