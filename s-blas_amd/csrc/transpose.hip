@@ -97,11 +97,24 @@ constexpr int kRxItems = 16;
 constexpr int kRxTile = kRxThreads * kRxItems;
 constexpr int kRxWaves = kRxThreads / 64;
 
-__global__ void k_expand_rows(const int *__restrict__ rowptr, int m, int *__restrict__ rows)
+// row of every nonzero: a wave per 64 rows writes them one after another,
+// all 64 lanes on one row's entries (consecutive stores).  (A thread per
+// row left a long row's lane storing ~100 words alone -- 84 us on the
+// config-2 matrix; 16-B stores per thread 157 us; a binary search per four
+// entries 176 us, its 21 dependent loads per thread.)
+__global__ __launch_bounds__(256) void k_expand_rows(const int *__restrict__ rowptr, int m, int *__restrict__ rows)
 {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= m) return;
-    for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) rows[e] = r;
+    const int lane = threadIdx.x & 63;
+    const int r0 = ((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * 64;
+    if (r0 >= m) return;
+    const int nrow = min(64, m - r0);
+    const int b = rowptr[min(r0 + lane, m)];
+    const int last = rowptr[r0 + nrow];
+    for (int j = 0; j < nrow; ++j) {
+        const int s = __builtin_amdgcn_readlane(b, j);
+        const int e = j + 1 < nrow ? __builtin_amdgcn_readlane(b, j + 1) : last;
+        for (int k = s + lane; k < e; k += 64) rows[k] = r0 + j;
+    }
 }
 
 __global__ __launch_bounds__(kRxThreads) void k_rx_count(const int *__restrict__ keys, long long nnz,
@@ -221,7 +234,6 @@ __global__ __launch_bounds__(kRxThreads, 2) void k_rx_scatter(
 // the in-wave rank; the first lane of each (wave, digit) group posts the
 // group's size, so LDS work per element is O(waves), not O(digits).
 constexpr int kRx2MaxDigits = 2048;
-constexpr int kRx2CountSplit = 8;  // count workgroups per scatter workgroup segment
 // scatter workgroup size: 512 threads = 8 waves, 8 entries per thread of a
 // 4096-entry tile (256 threads left only 8 waves per CU at 71 KiB of LDS)
 #ifndef SBLAS_R2_THREADS
@@ -267,38 +279,50 @@ __device__ __forceinline__ size_t seg_count_idx(int mode, const SegArgs &g, int 
     return ((size_t)(wg / g.J) * D + d) * g.J + (wg % g.J);
 }
 
-// counts of each scatter workgroup's segment: kRx2CountSplit small
-// workgroups per segment (8 KiB LDS each, many per CU), 16 keys in flight per
-// thread, histograms merged with global atomics (counts zeroed first).
+// counts of each scatter workgroup's segment: one 1024-thread workgroup per
+// segment, 16 keys in flight per thread, LDS histogram, then every digit's
+// count stored plainly (no zeroing, no global atomics: with eight workgroups
+// per segment merging by atomics the two count passes took 75 us each on the
+// config-2 matrix, memory-side atomics being one 64-B request per lane).
+constexpr int kCntThreads = 1024;
 template <int kSeg>
-__global__ __launch_bounds__(kRxThreads) void k_rx2_count(const int *__restrict__ keys, long long nnz,
-                                                          int shift, int rb, SegArgs g,
-                                                          int *__restrict__ counts)
+__global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict__ keys, long long nnz,
+                                                           int shift, int rb, SegArgs g,
+                                                           int *__restrict__ counts)
 {
     __shared__ int h[kRx2MaxDigits];
     const int D = 1 << rb;
-    for (int d = threadIdx.x; d < D; d += kRxThreads) h[d] = 0;
+    for (int d = threadIdx.x; d < D; d += kCntThreads) h[d] = 0;
     __syncthreads();
-    const int wg = (int)blockIdx.x / kRx2CountSplit, part = (int)blockIdx.x % kRx2CountSplit;
-    long long seg0, seg1;
-    seg_range(kSeg, g, wg, nnz, seg0, seg1);
-    const long long len = max(0LL, seg1 - seg0);
-    const long long p0 = seg0 + len * part / kRx2CountSplit, p1 = seg0 + len * (part + 1) / kRx2CountSplit;
-    constexpr int kU = 16;
-    for (long long i0 = p0; i0 < p1; i0 += (long long)kU * kRxThreads) {
-        int d[kU];
+    const int wg = (int)blockIdx.x;
+    long long p0, p1;
+    seg_range(kSeg, g, wg, nnz, p0, p1);
+    // 16-B loads over the aligned body (keys arrays are 16-B aligned), single
+    // keys for the head and tail
+    const long long q0 = min(p1, (p0 + 3) & ~3LL), q1 = max(q0, p1 & ~3LL);
+    for (long long i = p0 + threadIdx.x; i < q0; i += kCntThreads) atomicAdd(&h[(keys[i] >> shift) & (D - 1)], 1);
+    for (long long i = q1 + threadIdx.x; i < p1; i += kCntThreads) atomicAdd(&h[(keys[i] >> shift) & (D - 1)], 1);
+    const int4 *k4 = reinterpret_cast<const int4 *>(keys + q0);
+    const long long n4 = (q1 - q0) >> 2;
+    constexpr int kU = 8;
+    for (long long i0 = 0; i0 < n4; i0 += (long long)kU * kCntThreads) {
+        int4 v[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const long long i = i0 + (long long)u * kRxThreads + threadIdx.x;
-            d[u] = i < p1 ? ((keys[i] >> shift) & (D - 1)) : -1;
+            const long long i = i0 + (long long)u * kCntThreads + threadIdx.x;
+            v[u] = i < n4 ? k4[i] : make_int4(-1, -1, -1, -1);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-            if (d[u] >= 0) atomicAdd(&h[d[u]], 1);
+            if (v[u].x != -1) {
+                atomicAdd(&h[(v[u].x >> shift) & (D - 1)], 1);
+                atomicAdd(&h[(v[u].y >> shift) & (D - 1)], 1);
+                atomicAdd(&h[(v[u].z >> shift) & (D - 1)], 1);
+                atomicAdd(&h[(v[u].w >> shift) & (D - 1)], 1);
+            }
     }
     __syncthreads();
-    for (int dd = threadIdx.x; dd < D; dd += kRxThreads)
-        if (h[dd]) atomicAdd(&counts[seg_count_idx(kSeg, g, wg, D, dd)], h[dd]);
+    for (int dd = threadIdx.x; dd < D; dd += kCntThreads) counts[seg_count_idx(kSeg, g, wg, D, dd)] = h[dd];
 }
 
 // Scatter: workgroup b sorts tiles [b*S, (b+1)*S) in order.  Wave w ranks
@@ -319,7 +343,7 @@ template <int kMaxD, int kSeg, int kT>
 __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
-    int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n)
+    int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n, int pack)
 {
     constexpr bool kFinal = kSeg >= kSegFinal;
     constexpr int kW = kT / 64;  // waves
@@ -336,8 +360,12 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const unsigned long long lt = (1ull << lane) - 1ull;
     long long s0, s1;
     seg_range(kFinal ? kSegBuckets : kSeg, sg, (int)blockIdx.x, nnz, s0, s1);
+    int bk = (int)blockIdx.x;  // the last pass: current bucket (grid-stride)
+    // column written to kout: a packed last-pass key keeps only the bits below rb
+    auto colkey = [&](int k) { return (kFinal && pack >= 0) ? ((bk << rb) | (k & dm)) : k; };
     int kk[kB], rr[kB];
     double vv[kB];
+    auto rowof = [&](int j) { return (kFinal && pack >= 0) ? (int)((unsigned)kk[j] >> pack) : rr[j]; };
     auto load_tile = [&](long long base, int valid) {
 #pragma unroll
         for (int j = 0; j < kB; ++j) {
@@ -345,7 +373,9 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             const bool ok = li < valid;
             const long long gi = ok ? base + li : 0;
             kk[j] = ok ? kin[gi] : -1;  // top digit, ranked after every real element
-            rr[j] = ok ? rin[gi] : 0;
+            // a packed last-pass key carries the row; it is unpacked where it is
+            // used (here it would make the prefetch wait for its load)
+            if (!(kFinal && pack >= 0)) rr[j] = ok ? rin[gi] : 0;
             vv[j] = ok ? vin[gi] : 0.0;
         }
     };
@@ -414,8 +444,8 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                 if (w * kQ + j * 64 + lane < valid) {
                     const int d = (kk[j] >> shift) & dm;
                     const long long g = (long long)gbase[d] + (wcnt[w][d] + lp[j] - lstart[d]);
-                    if (kout) kout[g] = kk[j];
-                    rout[g] = rr[j];
+                    if (kout) kout[g] = colkey(kk[j]);
+                    rout[g] = rowof(j);
                     vout[g] = vv[j];
                 }
             }
@@ -427,7 +457,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                 if (w * kQ + j * 64 + lane < valid) {
                     const int pos = wcnt[w][(kk[j] >> shift) & dm] + lp[j];
                     skey[pos] = kk[j];
-                    srow[pos] = rr[j];
+                    srow[pos] = rowof(j);
                     sval[pos] = vv[j];
                 }
             }
@@ -438,8 +468,12 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                 const int k = skey[li];
                 const int d = (k >> shift) & dm;
                 const long long g = (long long)gbase[d] + (li - lstart[d]);
-                if (kout) kout[g] = k;
-                rout[g] = srow[li];
+                if (!kFinal && pack >= 0) {  // pass B -> last pass: row and the low `pack` bits in one word
+                    kout[g] = (srow[li] << pack) | (k & ((1 << pack) - 1));
+                } else {
+                    if (kout) kout[g] = colkey(k);
+                    rout[g] = srow[li];
+                }
                 vout[g] = sval[li];
             }
         }
@@ -464,7 +498,6 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
         // registers of its tile, a longer one reads its keys first.
         static_assert(kMaxD <= kT, "one digit per thread");
         if (blockIdx.x == 0 && t == 0) colptr[n] = (int)nnz;
-        int bk = (int)blockIdx.x;
         while (bk < sg.nb) {
             if (t < D) gbase[t] = 0;
             __syncthreads();
@@ -643,7 +676,7 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     const long long ncnt = msd ? ncntA + ncntB : (wide ? (long long)(1 << rb) * nwg : 256LL * ntiles);
     const size_t scan_ints = (size_t)(ncnt / kScanTile + 64) * 2;
     // scratch: keysA rowsA valsA | keysB rowsB valsB | counts | scan (+ outputs when null)
-    const size_t z = (size_t)nnz;
+    const size_t z = ((size_t)nnz + 3) & ~(size_t)3;  // array stride: every array 16-B aligned
     const size_t need = z * 32 + (size_t)ncnt * 4 + scan_ints * 4 + (rowidx ? 0 : z * 4) +
                         (cval ? 0 : z * 8) + 256;
     TransposeScratch &S = g_tscratch[A.device & 63];
@@ -669,23 +702,29 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
     if (msd) {
         int *cntA = counts, *cntB = counts + ncntA;
-        SBLAS_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)ncnt, s));
         // pass A: the top bA bits, fixed tile segments, (col, expanded row, val) -> set A
         const int shA = ms.c + ms.bB;
         const SegArgs gA{S_t, nwg, nullptr, 1, 1};
-        hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s,
+        hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg), dim3(kCntThreads), 0, s,
                            A.col, nnz, shA, ms.bA, gA, cntA);
         SBLAS_TRY(scan_inclusive(cntA, ncntA, scan, s));
         hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, A.col, rowsB, A.val,
-                           nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n);
-        // pass B: the next bB bits inside each pass-A bucket, set A -> set B
+                           nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1);
+        // pass B: the next bB bits inside each pass-A bucket, set A -> set B.
+        // Its output keeps (row << c | low c column bits) in one word when
+        // they fit (the last pass needs nothing else of the key): 12 B per
+        // entry written and read instead of 16.  SBLAS_TRANSPOSE_PACK=0 off.
+        int mbits = 0;
+        while (mbits < 31 && (m - 1) >> mbits) ++mbits;
+        const char *pk_e = getenv("SBLAS_TRANSPOSE_PACK");
+        const int pack = (mbits + ms.c <= 31 && !(pk_e && atoi(pk_e) == 0)) ? ms.c : -1;
         const int nwgB = (1 << ms.bA) * JB;
         const SegArgs gB{0, 0, cntA, nwg, JB};
-        hipLaunchKernelGGL(k_rx2_count<kSegBuckets>, dim3((unsigned)nwgB * kRx2CountSplit), dim3(kRxThreads), 0,
+        hipLaunchKernelGGL(k_rx2_count<kSegBuckets>, dim3((unsigned)nwgB), dim3(kCntThreads), 0,
                            s, keysA, nnz, ms.c, ms.bB, gB, cntB);
         SBLAS_TRY(scan_inclusive(cntB, ncntB, scan, s));
         hipLaunchKernelGGL((k_rx2_scatter<256, kSegBuckets, kR2Threads>), dim3(nwgB), dim3(kR2Threads), 0, s, keysA, rowsA,
-                           valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n);
+                           valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n, pack);
         // last pass: one workgroup per pass-B bucket (2^c columns), set B -> CSC + colptr
         const int nbC = 1 << (ms.bA + ms.bB);
         // SBLAS_TRANSPOSE_DIRECT=1: entries written from registers (experiment)
@@ -694,8 +733,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         auto kfin = (de && atoi(de) == 1) ? k_rx2_scatter<256, kSegFinalDirect, kR2Threads>
                                           : k_rx2_scatter<256, kSegFinal, kR2Threads>;
         hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
-                           keysB, rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final, vout_final,
-                           colptr, n);
+                           keysB, pack >= 0 ? nullptr : rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final,
+                           vout_final, colptr, n, pack);
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;
     }
@@ -711,16 +750,15 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         if (wide) {
             const int sh = rb * ps;
             const SegArgs gt{S_t, nwg, nullptr, 1, 1};
-            SBLAS_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)ncnt, s));
-            hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg * kRx2CountSplit), dim3(kRxThreads), 0, s,
+            hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg), dim3(kCntThreads), 0, s,
                                kin, nnz, sh, rb, gt, counts);
             SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));
             if (rb <= 8)  // 71 KiB of LDS: two workgroups per CU
                 hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, kin, rin, vin,
-                                   nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n);
+                                   nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n, -1);
             else
                 hipLaunchKernelGGL((k_rx2_scatter<kRx2MaxDigits, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, kin,
-                                   rin, vin, nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n);
+                                   rin, vin, nnz, sh, rb, gt, counts, ko, ro, vo, nullptr, n, -1);
         } else {
             hipLaunchKernelGGL(k_rx_count, dim3(ntiles), dim3(kRxThreads), 0, s, kin, nnz, shift, ntiles, counts);
             SBLAS_TRY(scan_inclusive(counts, ncnt, scan, s));

@@ -105,6 +105,33 @@ def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     A.close()
 
 
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["packed", "unpacked"])
+def test_config2_transpose_full_size(torch_cuda, sb, orc, cfg2, monkeypatch, pack):
+    """CSR -> CSC of the config-2 matrix (the size tools/bench_transpose.py
+    times): colptr, row indices and values bit-exact against orc_transpose
+    (tranpose.h:6-43's stable scatter).  Both last-pass input forms."""
+    torch = torch_cuda
+    if cfg2["prefix"]:
+        pytest.skip("random columns only")
+    monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", pack)
+    rp, col, val = cfg2["rp"], cfg2["col"], cfg2["val"]
+    nnz = int(rp[-1])
+    cp, ri, cv = orc.transpose(N2, N2, rp, col, val)
+    A = sb.DeviceCSR.upload(0, N2, rp, col, val)
+    try:
+        dcp = torch.zeros(N2 + 1, dtype=torch.int32, device="cuda")
+        dri = torch.zeros(nnz, dtype=torch.int32, device="cuda")
+        dcv = torch.zeros(nnz, dtype=torch.float64, device="cuda")
+        for _ in range(2):  # the second call reuses the grown scratch
+            A.transpose(dcp.data_ptr(), dri.data_ptr(), dcv.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(dcp.cpu().numpy(), cp)
+            assert np.array_equal(dri.cpu().numpy(), ri)
+            assert np.array_equal(dcv.cpu().numpy(), cv)
+    finally:
+        A.close()
+
+
 # ------------------------------------------------------------- config 4 ----
 @pytest.fixture(scope="module")
 def cfg4(orc):

@@ -117,11 +117,13 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "direct", "msd_c3", "msd_c5", "msd_c3_direct", "lsd", "rb11", "rb8"])
+@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "msd_c3", "msd_c5", "msd_c3_direct",
+                                    "msd_c5_nopack", "lsd", "rb11", "rb8"])
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     """Stable transpose, every path: the MSD partition passes + per-bucket
-    final pass (default where n > 512; SBLAS_TRANSPOSE_MSD_C moves the final
+    final pass (default where n > 512; pass B hands the last pass one word of
+    row and low column bits, SBLAS_TRANSPOSE_PACK=0 two; SBLAS_TRANSPOSE_MSD_C moves the final
     bucket width so small matrices take it too, with few, long buckets on
     "longcols"), the LSD tiles-per-workgroup path with <= 8-bit digits ("big"
     = 3 passes at n = 3M) and with 11-bit digits, and the one-tile 8-bit path."""
@@ -136,6 +138,8 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         monkeypatch.setenv("SBLAS_TRANSPOSE_MSD_C", digits[5])
     if digits.endswith("direct"):  # last pass writes from registers
         monkeypatch.setenv("SBLAS_TRANSPOSE_DIRECT", "1")
+    if digits.endswith("nopack"):  # pass B keeps separate key and row arrays
+        monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
