@@ -285,10 +285,14 @@ __device__ __forceinline__ size_t seg_count_idx(int mode, const SegArgs &g, int 
 // per segment merging by atomics the two count passes took 75 us each on the
 // config-2 matrix, memory-side atomics being one 64-B request per lane).
 constexpr int kCntThreads = 1024;
+// wgrow (MSD pass A): also the row holding each segment's first entry,
+// the start of the scatter's row derivation.
 template <int kSeg>
 __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict__ keys, long long nnz,
                                                            int shift, int rb, SegArgs g,
-                                                           int *__restrict__ counts)
+                                                           int *__restrict__ counts,
+                                                           const int *__restrict__ rowptr = nullptr, int m = 0,
+                                                           int *__restrict__ wgrow = nullptr)
 {
     __shared__ int h[kRx2MaxDigits];
     const int D = 1 << rb;
@@ -297,6 +301,15 @@ __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict
     const int wg = (int)blockIdx.x;
     long long p0, p1;
     seg_range(kSeg, g, wg, nnz, p0, p1);
+    if (wgrow && threadIdx.x == 0) {  // largest r with rowptr[r] <= p0
+        int lo = 0, hi = m - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rowptr[mid] <= p0) lo = mid;
+            else hi = mid - 1;
+        }
+        wgrow[wg] = lo;
+    }
     // 16-B loads over the aligned body (keys arrays are 16-B aligned), single
     // keys for the head and tail
     const long long q0 = min(p1, (p0 + 3) & ~3LL), q1 = max(q0, p1 & ~3LL);
@@ -339,17 +352,29 @@ __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict
 constexpr int kSegFinal = 2;
 constexpr int kSegFinalDirect = 3;  // the same, each entry written from registers
 
-template <int kMaxD, int kSeg, int kT>
+// kDerive (the MSD transpose's pass A): the entries' rows are not read from
+// an expanded array but derived per tile from rowptr.  The workgroup walks
+// its tiles in order with the row rc that contains the tile's first entry
+// (the first from wgrow[], written by the count pass).  Thread t holds the
+// start of row rc+1+t (a window of kT rows, loaded one tile ahead); each row
+// starting inside the tile marks its position in srow with atomicMax (empty
+// rows share a position, the largest wins), and a prefix max over the
+// positions -- per wave over its contiguous quarter, then across waves --
+// is every entry's row.  Rows starting exactly at the tile's end give the
+// next tile's rc.  A tile holding more than kT row starts takes more windows.
+template <int kMaxD, int kSeg, int kT, bool kDerive = false>
 __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
-    int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n, int pack)
+    int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n, int pack,
+    const int *__restrict__ rowptr = nullptr, int m = 0, const int *__restrict__ wgrow = nullptr)
 {
     constexpr bool kFinal = kSeg >= kSegFinal;
     constexpr int kW = kT / 64;  // waves
     __shared__ int wcnt[kW][kMaxD];  // per-wave counts, then per-wave starts
     __shared__ int lstart[kMaxD], gbase[kMaxD];
     __shared__ int wtot[kW];
+    __shared__ int wmaxs[kW], s_next, s_more[2];  // kDerive
     __shared__ int skey[kRxTile], srow[kRxTile];
     __shared__ double sval[kRxTile];
     constexpr int kQ = kRxTile / kW;  // elements per wave per tile
@@ -375,14 +400,67 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             kk[j] = ok ? kin[gi] : -1;  // top digit, ranked after every real element
             // a packed last-pass key carries the row; it is unpacked where it is
             // used (here it would make the prefetch wait for its load)
-            if (!(kFinal && pack >= 0)) rr[j] = ok ? rin[gi] : 0;
+            if (!(kFinal && pack >= 0) && !kDerive) rr[j] = ok ? rin[gi] : 0;
             vv[j] = ok ? vin[gi] : 0.0;
         }
     };
     // Steps 1-5 on the tile in registers (valid entries); the tile at
     // (nbase, nvalid) is loaded into the registers between staging and
     // write-out; gbase[] then points past this tile's runs.
-    auto process_tile = [&](int valid, long long nbase, int nvalid) {
+    int rc = 0, wv = 0;  // kDerive: row containing the tile's first entry; window
+    auto derive_rows = [&](long long cbase, int valid) {
+        int rw = rc, wvv = wv;
+        for (int round = 0;; ++round) {
+            const int r = rw + 1 + t;
+            if (r < m) {
+                const long long p = (long long)wvv - cbase;  // >= 1: rows after rc start past cbase
+                if (p < valid) atomicMax(&srow[p], r);
+                else if (p == valid) atomicMax(&s_next, r);
+            }
+            if (t == kT - 1) s_more[round & 1] = (r < m && (long long)wvv <= cbase + valid) ? 1 : 0;
+            __syncthreads();
+            if (!s_more[round & 1]) break;
+            rw += kT;
+            wvv = rowptr[min(rw + 1 + t, m)];
+        }
+        int run = -1;
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            int v = srow[w * kQ + j * 64 + lane];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int u = __shfl_up(v, off, 64);
+                if (lane >= off) v = max(v, u);
+            }
+            v = max(v, run);
+            rr[j] = v;
+            run = __builtin_amdgcn_readlane(v, 63);
+        }
+        if (lane == 0) wmaxs[w] = run;
+        __syncthreads();
+        int pre = -1, all = s_next;
+#pragma unroll
+        for (int q = 0; q < kW; ++q) {
+            const int mq = wmaxs[q];
+            if (q < w) pre = max(pre, mq);
+            all = max(all, mq);
+        }
+#pragma unroll
+        for (int j = 0; j < kB; ++j) rr[j] = max(rr[j], pre);
+        rc = all;  // the next tile's first entry lies in row rc
+        wv = rowptr[min(rc + 1 + t, m)];
+    };
+    // srow = -1 everywhere but srow[0] = rc (the row of the tile's first entry)
+    auto derive_init = [&]() {
+#pragma unroll
+        for (int j = 0; j < kB; ++j) srow[w * kQ + j * 64 + lane] = -1;
+        if (t == 0) {
+            srow[0] = rc;
+            s_next = rc;
+        }
+    };
+    auto process_tile = [&](int valid, long long nbase, int nvalid, long long cbase) {
+        if constexpr (kDerive) derive_rows(cbase, valid);
         int lp[kB];
         // 1. wave-private ranking
 #pragma unroll
@@ -485,6 +563,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
 #pragma unroll
             for (int q = 0; q < kW; ++q) wcnt[q][d] = 0;
         }
+        if constexpr (kDerive) derive_init();
         __syncthreads();
     };
     long long base = s0;
@@ -550,7 +629,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                         nvalid = (int)min((long long)kRxTile, ns1 - ns0);
                     }
                 }
-                if (valid > 0) process_tile(valid, nbase, nvalid);
+                if (valid > 0) process_tile(valid, nbase, nvalid, base);
                 else if (nvalid > 0) load_tile(nbase, nvalid);
                 base = nbase;
                 valid = nvalid;
@@ -569,11 +648,18 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
 #pragma unroll
             for (int q = 0; q < kW; ++q) wcnt[q][d] = 0;
         }
+        if constexpr (kDerive) {
+            if (valid > 0) {
+                rc = wgrow[blockIdx.x];
+                wv = rowptr[min(rc + 1 + t, m)];
+                derive_init();
+            }
+        }
         __syncthreads();
         while (valid > 0) {  // valid: workgroup-uniform
             const long long nbase = base + kRxTile;
             const int nvalid = nbase < s1 ? (int)min((long long)kRxTile, s1 - nbase) : 0;
-            process_tile(valid, nbase, nvalid);
+            process_tile(valid, nbase, nvalid, base);
             base = nbase;
             valid = nvalid;
         }
@@ -699,17 +785,28 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     int *scan = counts + ncnt;
     int *rout_final = rowidx ? rowidx : scan + scan_ints;
     double *vout_final = cval ? cval : (double *)(((uintptr_t)(rout_final + (rowidx ? 0 : z)) + 7) & ~(uintptr_t)7);
-    hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
+    // MSD pass A derives the rows from rowptr (SBLAS_TRANSPOSE_DERIVE=0: from
+    // an expanded row array, as the LSD passes do)
+    const char *dv_e = getenv("SBLAS_TRANSPOSE_DERIVE");
+    const bool derive = msd && !(dv_e && atoi(dv_e) == 0);
+    if (!derive)
+        hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
     if (msd) {
         int *cntA = counts, *cntB = counts + ncntA;
-        // pass A: the top bA bits, fixed tile segments, (col, expanded row, val) -> set A
+        int *wgrow = rowsB;  // nwg <= nnz ints; rowsB is not written before pass B
+        // pass A: the top bA bits, fixed tile segments, (col, row, val) -> set A
         const int shA = ms.c + ms.bB;
         const SegArgs gA{S_t, nwg, nullptr, 1, 1};
         hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg), dim3(kCntThreads), 0, s,
-                           A.col, nnz, shA, ms.bA, gA, cntA);
+                           A.col, nnz, shA, ms.bA, gA, cntA, A.rowptr, m, derive ? wgrow : nullptr);
         SBLAS_TRY(scan_inclusive(cntA, ncntA, scan, s));
-        hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s, A.col, rowsB, A.val,
-                           nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1);
+        if (derive)
+            hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads, true>), dim3(nwg), dim3(kR2Threads), 0, s,
+                               A.col, nullptr, A.val, nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1,
+                               A.rowptr, m, wgrow);
+        else
+            hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s,
+                               A.col, rowsB, A.val, nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1);
         // pass B: the next bB bits inside each pass-A bucket, set A -> set B.
         // Its output keeps (row << c | low c column bits) in one word when
         // they fit (the last pass needs nothing else of the key): 12 B per
@@ -734,7 +831,7 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
                                           : k_rx2_scatter<256, kSegFinal, kR2Threads>;
         hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
                            keysB, pack >= 0 ? nullptr : rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final,
-                           vout_final, colptr, n, pack);
+                           vout_final, colptr, n, pack, nullptr, 0, nullptr);
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;
     }

@@ -117,12 +117,13 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "msd_c3", "msd_c5", "msd_c3_direct",
-                                    "msd_c5_nopack", "lsd", "rb11", "rb8"])
-@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big"])
+@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "noderive", "msd_c3", "msd_c5",
+                                    "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
+@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     """Stable transpose, every path: the MSD partition passes + per-bucket
-    final pass (default where n > 512; pass B hands the last pass one word of
+    final pass (default where n > 512; pass A derives each entry's row from rowptr,
+    SBLAS_TRANSPOSE_DERIVE=0 reads an expanded row array; pass B hands the last pass one word of
     row and low column bits, SBLAS_TRANSPOSE_PACK=0 two; SBLAS_TRANSPOSE_MSD_C moves the final
     bucket width so small matrices take it too, with few, long buckets on
     "longcols"), the LSD tiles-per-workgroup path with <= 8-bit digits ("big"
@@ -140,6 +141,8 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         monkeypatch.setenv("SBLAS_TRANSPOSE_DIRECT", "1")
     if digits.endswith("nopack"):  # pass B keeps separate key and row arrays
         monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
+    if digits == "noderive":  # pass A reads an expanded row array instead of deriving rows
+        monkeypatch.setenv("SBLAS_TRANSPOSE_DERIVE", "0")
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
@@ -149,6 +152,13 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     elif case == "big":  # 2.2M nonzeros over 3M columns: 2 passes x 11 bits, 2 tiles per workgroup
         m, n = 110000, 3_000_000
         lens = rng.integers(0, 40, m)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    elif case == "shortrows":  # 0-3 entries per row, half the rows empty: a 4096-entry tile
+        # holds thousands of row starts (pass A's row derivation takes several windows)
+        m, n = 200000, 5000
+        lens = rng.integers(0, 4, m) * (rng.random(m) < 0.5)
         rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
         val = rng.standard_normal(int(rp[-1]))
