@@ -157,6 +157,9 @@ def main() -> int:
                     help="N>1 cyclic allgather: split each rank's chunks in two halves and "
                          "all-gather the first while the kernel runs on the second")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="join a process group even at WORLD_SIZE 1 (torchrun --nproc-per-node 1): "
+                         "runs the N > 1 exchange and timing path, RCCL included, on one GPU")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -175,7 +178,7 @@ def main() -> int:
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist_always:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -306,7 +309,7 @@ def main() -> int:
         for k in range(args.steps):
             evict()  # 1 GiB sweep: evicts MALL (256 MB) and L2
             sync_barrier()
-            if world == 1 and op.dm > 0:
+            if dist is None and op.dm > 0:
                 span_ms.append(op.A.spmv_timed(op.algo, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp))
             else:
                 torch.cuda._sleep(500_000)
