@@ -362,7 +362,7 @@ constexpr int kSegFinalDirect = 3;  // the same, each entry written from registe
 // positions -- per wave over its contiguous quarter, then across waves --
 // is every entry's row.  Rows starting exactly at the tile's end give the
 // next tile's rc.  A tile holding more than kT row starts takes more windows.
-template <int kMaxD, int kSeg, int kT, bool kDerive = false>
+template <int kMaxD, int kSeg, int kT, bool kDerive = false, int kTile = kRxTile>
 __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
@@ -375,11 +375,12 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     __shared__ int lstart[kMaxD], gbase[kMaxD];
     __shared__ int wtot[kW];
     __shared__ int wmaxs[kW], s_next, s_more[2];  // kDerive
-    __shared__ int skey[kRxTile], srow[kRxTile];
-    __shared__ double sval[kRxTile];
-    constexpr int kQ = kRxTile / kW;  // elements per wave per tile
+    __shared__ int skey[kTile], srow[kTile];
+    __shared__ double sval[kTile];
+    constexpr int kQ = kTile / kW;  // elements per wave per tile
     constexpr int kB = kQ / 64;             // batches per wave (16)
-    static_assert(kB * kT == kRxTile, "one register slot per batch");
+    static_assert(kB * kT == kTile, "one register slot per batch");
+    static_assert(kTile == kRxTile || kSeg >= kSegFinal, "tile segments (seg_range) assume kRxTile");
     const int D = 1 << rb, dm = D - 1;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -476,7 +477,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             if (rank == 0) wcnt[w][d] += __popcll(mm);
         }
         // padding (top digit, after every real element) is not part of the output
-        if (t == kT - 1 && valid < kRxTile) wcnt[kW - 1][dm] -= kRxTile - valid;
+        if (t == kT - 1 && valid < kTile) wcnt[kW - 1][dm] -= kTile - valid;
         __syncthreads();
         // 2. digit totals, per-wave starts inside each digit, exclusive scan
         constexpr int kPer = (kMaxD + kT - 1) / kT;
@@ -567,7 +568,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
         __syncthreads();
     };
     long long base = s0;
-    int valid = base < s1 ? (int)min((long long)kRxTile, s1 - base) : 0;
+    int valid = base < s1 ? (int)min((long long)kTile, s1 - base) : 0;
     if (valid > 0) load_tile(base, valid);
     if constexpr (kFinal) {
         // buckets bk = blockIdx.x, + gridDim.x, ...; each: its own digit
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
         while (bk < sg.nb) {
             if (t < D) gbase[t] = 0;
             __syncthreads();
-            if (s1 - s0 <= kRxTile) {
+            if (s1 - s0 <= kTile) {
 #pragma unroll
                 for (int j = 0; j < kB; ++j)
                     if (w * kQ + j * 64 + lane < valid) atomicAdd(&gbase[(kk[j] >> shift) & dm], 1);
@@ -618,15 +619,15 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             for (;;) {  // the bucket's tiles (all values workgroup-uniform)
                 long long nbase = 0, ns0 = s0, ns1 = s1;
                 int nvalid = 0, nbk = bk;
-                if (base + kRxTile < s1) {
-                    nbase = base + kRxTile;
-                    nvalid = (int)min((long long)kRxTile, s1 - nbase);
+                if (base + kTile < s1) {
+                    nbase = base + kTile;
+                    nvalid = (int)min((long long)kTile, s1 - nbase);
                 } else {
                     nbk = bk + (int)gridDim.x;
                     if (nbk < sg.nb) {
                         seg_range(kSegBuckets, sg, nbk, nnz, ns0, ns1);
                         nbase = ns0;
-                        nvalid = (int)min((long long)kRxTile, ns1 - ns0);
+                        nvalid = (int)min((long long)kTile, ns1 - ns0);
                     }
                 }
                 if (valid > 0) process_tile(valid, nbase, nvalid, base);
@@ -657,8 +658,8 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
         }
         __syncthreads();
         while (valid > 0) {  // valid: workgroup-uniform
-            const long long nbase = base + kRxTile;
-            const int nvalid = nbase < s1 ? (int)min((long long)kRxTile, s1 - nbase) : 0;
+            const long long nbase = base + kTile;
+            const int nvalid = nbase < s1 ? (int)min((long long)kTile, s1 - nbase) : 0;
             process_tile(valid, nbase, nvalid, base);
             base = nbase;
             valid = nvalid;
@@ -827,8 +828,18 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         // SBLAS_TRANSPOSE_DIRECT=1: entries written from registers (experiment)
         const char *de = getenv("SBLAS_TRANSPOSE_DIRECT");
         const SegArgs gC{0, 0, cntB, JB, 1, nbC};
-        auto kfin = (de && atoi(de) == 1) ? k_rx2_scatter<256, kSegFinalDirect, kR2Threads>
-                                          : k_rx2_scatter<256, kSegFinal, kR2Threads>;
+        // final tile: 3072 entries (6 per thread) when the buckets average <=
+        // 2600 -- uniform columns then fit one tile (spread ~ sqrt(avg)) with
+        // 83% of its lanes busy instead of 62% in a 4096 tile; fuller buckets
+        // keep the 4096 tile (SBLAS_TRANSPOSE_FTILE=4096 forces it)
+        const long long favg = nnz / std::max(1, nbC);
+        const char *ft_e = getenv("SBLAS_TRANSPOSE_FTILE");
+        const bool small_tile = ft_e ? atoi(ft_e) == 3072 : favg <= 2600;
+        auto kfin = (de && atoi(de) == 1)
+                        ? (small_tile ? k_rx2_scatter<256, kSegFinalDirect, kR2Threads, false, 3072>
+                                      : k_rx2_scatter<256, kSegFinalDirect, kR2Threads>)
+                        : (small_tile ? k_rx2_scatter<256, kSegFinal, kR2Threads, false, 3072>
+                                      : k_rx2_scatter<256, kSegFinal, kR2Threads>);
         hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
                            keysB, pack >= 0 ? nullptr : rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final,
                            vout_final, colptr, n, pack, nullptr, 0, nullptr);

@@ -117,8 +117,8 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "noderive", "msd_c3", "msd_c5",
-                                    "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
+@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "noderive", "ftile4096", "ftile3072",
+                                    "msd_c3", "msd_c5", "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     """Stable transpose, every path: the MSD partition passes + per-bucket
@@ -143,6 +143,8 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
     if digits == "noderive":  # pass A reads an expanded row array instead of deriving rows
         monkeypatch.setenv("SBLAS_TRANSPOSE_DERIVE", "0")
+    if digits.startswith("ftile"):  # last-pass tile forced to 4096 / 3072 entries (3072: buckets
+        monkeypatch.setenv("SBLAS_TRANSPOSE_FTILE", digits[5:])  # past it take the multi-tile path)
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
