@@ -24,12 +24,27 @@ import os
 import statistics
 
 
+def split_kernels(kernel):
+    """Split a comma-separated kernel list at top-level commas only: template
+    names such as k_rx2_scatter<256, 0, 512> keep theirs."""
+    out, depth, cur = [], 0, ""
+    for ch in kernel:
+        if ch == "," and depth == 0:
+            out.append(cur)
+            cur = ""
+            continue
+        depth += (ch == "<") - (ch == ">")
+        cur += ch
+    out.append(cur)
+    return [k for k in out if k]
+
+
 def counter_values(d, kernel, name):
     """Per-launch values; `kernel` may list several comma-separated kernels
     that make up one operation (e.g. panel SpMV + its reduce): their medians
     are summed into a single per-operation value."""
     total = []
-    for k in kernel.split(","):
+    for k in split_kernels(kernel):
         vals = []
         for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(path) as fh:
