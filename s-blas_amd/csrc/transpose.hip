@@ -301,14 +301,20 @@ __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict
     const int wg = (int)blockIdx.x;
     long long p0, p1;
     seg_range(kSeg, g, wg, nnz, p0, p1);
-    if (wgrow && threadIdx.x == 0) {  // largest r with rowptr[r] <= p0
+    if (wgrow && threadIdx.x < 2) {
+        // thread 0: the row holding the segment's first entry (largest r with
+        // rowptr[r] <= p0); thread 1: the row of its last; wgrow[nseg + wg] =
+        // the rows the segment spans beyond its first (0 when empty)
+        const long long p = threadIdx.x == 0 ? p0 : max(p0, p1 - 1);
         int lo = 0, hi = m - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (rowptr[mid] <= p0) lo = mid;
+            if (rowptr[mid] <= p) lo = mid;
             else hi = mid - 1;
         }
-        wgrow[wg] = lo;
+        const int first = __shfl(lo, 0, 64);
+        if (threadIdx.x == 0) wgrow[wg] = lo;
+        if (threadIdx.x == 1) wgrow[(int)gridDim.x + wg] = p1 > p0 ? lo - first : 0;
     }
     // 16-B loads over the aligned body (keys arrays are 16-B aligned), single
     // keys for the head and tail
@@ -367,9 +373,21 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
     int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n, int pack,
-    const int *__restrict__ rowptr = nullptr, int m = 0, const int *__restrict__ wgrow = nullptr)
+    const int *__restrict__ rowptr = nullptr, int m = 0, const int *__restrict__ wgrow = nullptr,
+    int packA = -1)
 {
     constexpr bool kFinal = kSeg >= kSegFinal;
+    // packA (MSD passes A and B): pass A writes ONE word per entry, the key's
+    // low packA bits (all pass B and the last pass read) with the row's offset
+    // from its segment's first row above them, and no row array; pass B finds
+    // each entry's segment (the segments' runs inside its bucket, in LDS) and
+    // adds that segment's first row.  Taken when every segment spans fewer
+    // than 2^(32 - packA) rows (wgrow[nseg + s] = segment s's span, from the
+    // count pass); all workgroups read the same spans, so all agree.
+    constexpr bool kPA = (kSeg == kSegTiles && kDerive) || kSeg == kSegBuckets;
+    constexpr int kSegMax = 512;
+    __shared__ int s_segstart[kSeg == kSegBuckets ? kSegMax + 1 : 1];
+    __shared__ int s_segrow[kSeg == kSegBuckets ? kSegMax : 1];
     constexpr int kW = kT / 64;  // waves
     __shared__ int wcnt[kW][kMaxD];  // per-wave counts, then per-wave starts
     __shared__ int lstart[kMaxD], gbase[kMaxD];
@@ -387,8 +405,29 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     long long s0, s1;
     seg_range(kFinal ? kSegBuckets : kSeg, sg, (int)blockIdx.x, nnz, s0, s1);
     int bk = (int)blockIdx.x;  // the last pass: current bucket (grid-stride)
-    // column written to kout: a packed last-pass key keeps only the bits below rb
-    auto colkey = [&](int k) { return (kFinal && pack >= 0) ? ((bk << rb) | (k & dm)) : k; };
+    // column written to kout by the last pass: its bucket's bits and the key's
+    // low rb bits (the key above them may be a packed word)
+    auto colkey = [&](int k) { return kFinal ? ((bk << rb) | (k & dm)) : k; };
+    bool pA = false;  // workgroup-uniform
+    const int nseg = kSeg == kSegBuckets ? sg.Jp : (int)gridDim.x;
+    if constexpr (kPA) {
+        if (packA >= 0 && nseg <= kSegMax) {
+            int v = 0;
+            for (int i = t; i < nseg; i += kT) v = max(v, wgrow[nseg + i]);
+#pragma unroll
+            for (int off = 32; off; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+            if (lane == 0) wmaxs[w] = v;
+            __syncthreads();
+            int mx = 0;
+#pragma unroll
+            for (int q = 0; q < kW; ++q) mx = max(mx, wmaxs[q]);
+            pA = packA >= 31 || mx < (1 << (32 - packA));
+            __syncthreads();
+        }
+    }
+    const unsigned kbmask = packA >= 0 && packA < 32 ? (1u << packA) - 1u : ~0u;
+    int segrow0 = 0;  // pass A: the segment's first row
+    int scur = 0;     // pass B: this wave's current segment
     int kk[kB], rr[kB];
     double vv[kB];
     auto rowof = [&](int j) { return (kFinal && pack >= 0) ? (int)((unsigned)kk[j] >> pack) : rr[j]; };
@@ -401,7 +440,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             kk[j] = ok ? kin[gi] : -1;  // top digit, ranked after every real element
             // a packed last-pass key carries the row; it is unpacked where it is
             // used (here it would make the prefetch wait for its load)
-            if (!(kFinal && pack >= 0) && !kDerive) rr[j] = ok ? rin[gi] : 0;
+            if (!(kFinal && pack >= 0) && !kDerive && !(kSeg == kSegBuckets && pA)) rr[j] = ok ? rin[gi] : 0;
             vv[j] = ok ? vin[gi] : 0.0;
         }
     };
@@ -530,6 +569,18 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
             }
             if (nvalid > 0) load_tile(nbase, nvalid);
         } else {
+            if constexpr (kSeg == kSegBuckets) {
+                if (pA) {  // rows from the packed pass-A words: segment (cursor walk) + offset
+#pragma unroll
+                    for (int j = 0; j < kB; ++j) {
+                        const long long gi = cbase + min(w * kQ + j * 64 + lane, valid - 1);
+                        int sgi = scur;
+                        while (gi >= s_segstart[sgi + 1]) ++sgi;
+                        rr[j] = s_segrow[sgi] + (int)((unsigned)kk[j] >> packA);
+                        scur = __builtin_amdgcn_readlane(sgi, 63);
+                    }
+                }
+            }
             // 3. stage in digit order
 #pragma unroll
             for (int j = 0; j < kB; ++j) {
@@ -547,7 +598,9 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                 const int k = skey[li];
                 const int d = (k >> shift) & dm;
                 const long long g = (long long)gbase[d] + (li - lstart[d]);
-                if (!kFinal && pack >= 0) {  // pass B -> last pass: row and the low `pack` bits in one word
+                if (kSeg == kSegTiles && kDerive && pA) {  // pass A -> pass B: low key bits + row offset
+                    kout[g] = (int)(((unsigned)k & kbmask) | ((unsigned)(srow[li] - segrow0) << packA));
+                } else if (!kFinal && pack >= 0) {  // pass B -> last pass: row and the low `pack` bits in one word
                     kout[g] = (srow[li] << pack) | (k & ((1 << pack) - 1));
                 } else {
                     if (kout) kout[g] = colkey(k);
@@ -652,11 +705,34 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
         if constexpr (kDerive) {
             if (valid > 0) {
                 rc = wgrow[blockIdx.x];
+                segrow0 = rc;
                 wv = rowptr[min(rc + 1 + t, m)];
                 derive_init();
             }
         }
+        if constexpr (kSeg == kSegBuckets) {
+            if (pA) {  // the segments' runs inside this bucket, and their first rows
+                const long long i0 = (long long)(blockIdx.x / sg.J) * nseg;
+                for (int i = t; i < nseg; i += kT) {
+                    s_segstart[i] = (i0 + i) ? sg.prev[i0 + i - 1] : 0;
+                    s_segrow[i] = wgrow[i];
+                }
+                if (t == 0) s_segstart[nseg] = INT_MAX;
+            }
+        }
         __syncthreads();
+        if constexpr (kSeg == kSegBuckets) {
+            if (pA && valid > 0) {  // this wave's first entry: largest i with s_segstart[i] <= p
+                const long long p = min(s0 + (long long)w * kQ, s1 - 1);
+                int lo = 0, hi = nseg - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_segstart[mid] <= p) lo = mid;
+                    else hi = mid - 1;
+                }
+                scur = lo;
+            }
+        }
         while (valid > 0) {  // valid: workgroup-uniform
             const long long nbase = base + kTile;
             const int nvalid = nbase < s1 ? (int)min((long long)kTile, s1 - nbase) : 0;
@@ -764,7 +840,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     const size_t scan_ints = (size_t)(ncnt / kScanTile + 64) * 2;
     // scratch: keysA rowsA valsA | keysB rowsB valsB | counts | scan (+ outputs when null)
     const size_t z = ((size_t)nnz + 3) & ~(size_t)3;  // array stride: every array 16-B aligned
-    const size_t need = z * 32 + (size_t)ncnt * 4 + scan_ints * 4 + (rowidx ? 0 : z * 4) +
+    const size_t wg_ints = ((size_t)2 * nwg + 67) & ~(size_t)3;  // MSD: segment first rows + spans
+    const size_t need = z * 32 + (size_t)ncnt * 4 + scan_ints * 4 + wg_ints * 4 + (rowidx ? 0 : z * 4) +
                         (cval ? 0 : z * 8) + 256;
     TransposeScratch &S = g_tscratch[A.device & 63];
     if (S.bytes < need) {
@@ -784,7 +861,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     int *rowsB = keysB + z;
     int *counts = rowsB + z;
     int *scan = counts + ncnt;
-    int *rout_final = rowidx ? rowidx : scan + scan_ints;
+    int *wgrow = scan + scan_ints;
+    int *rout_final = rowidx ? rowidx : wgrow + wg_ints;
     double *vout_final = cval ? cval : (double *)(((uintptr_t)(rout_final + (rowidx ? 0 : z)) + 7) & ~(uintptr_t)7);
     // MSD pass A derives the rows from rowptr (SBLAS_TRANSPOSE_DERIVE=0: from
     // an expanded row array, as the LSD passes do)
@@ -794,17 +872,22 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
     if (msd) {
         int *cntA = counts, *cntB = counts + ncntA;
-        int *wgrow = rowsB;  // nwg <= nnz ints; rowsB is not written before pass B
         // pass A: the top bA bits, fixed tile segments, (col, row, val) -> set A
         const int shA = ms.c + ms.bB;
         const SegArgs gA{S_t, nwg, nullptr, 1, 1};
         hipLaunchKernelGGL(k_rx2_count<kSegTiles>, dim3((unsigned)nwg), dim3(kCntThreads), 0, s,
                            A.col, nnz, shA, ms.bA, gA, cntA, A.rowptr, m, derive ? wgrow : nullptr);
         SBLAS_TRY(scan_inclusive(cntA, ncntA, scan, s));
+        // pass A -> pass B in one word per key (low bB + c bits + row offset in
+        // the segment) when the segments' row spans allow; decided on the
+        // device from the spans the count pass wrote.  SBLAS_TRANSPOSE_PACKA=0 off.
+        const char *pa_e = getenv("SBLAS_TRANSPOSE_PACKA");
+        const int packA = (derive && nwg <= 512 && ms.bB + ms.c <= 24 && !(pa_e && atoi(pa_e) == 0))
+                              ? ms.bB + ms.c : -1;
         if (derive)
             hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads, true>), dim3(nwg), dim3(kR2Threads), 0, s,
                                A.col, nullptr, A.val, nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1,
-                               A.rowptr, m, wgrow);
+                               A.rowptr, m, wgrow, packA);
         else
             hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads>), dim3(nwg), dim3(kR2Threads), 0, s,
                                A.col, rowsB, A.val, nnz, shA, ms.bA, gA, cntA, keysA, rowsA, valsA, nullptr, n, -1);
@@ -821,8 +904,14 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         hipLaunchKernelGGL(k_rx2_count<kSegBuckets>, dim3((unsigned)nwgB), dim3(kCntThreads), 0,
                            s, keysA, nnz, ms.c, ms.bB, gB, cntB);
         SBLAS_TRY(scan_inclusive(cntB, ncntB, scan, s));
-        hipLaunchKernelGGL((k_rx2_scatter<256, kSegBuckets, kR2Threads>), dim3(nwgB), dim3(kR2Threads), 0, s, keysA, rowsA,
-                           valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n, pack);
+        if (ms.bB <= 7)  // 128 digits: smaller count tables leave LDS for the segment tables
+            hipLaunchKernelGGL((k_rx2_scatter<128, kSegBuckets, kR2Threads>), dim3(nwgB), dim3(kR2Threads), 0, s, keysA,
+                               rowsA, valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n, pack, nullptr,
+                               0, wgrow, packA);
+        else
+            hipLaunchKernelGGL((k_rx2_scatter<256, kSegBuckets, kR2Threads>), dim3(nwgB), dim3(kR2Threads), 0, s, keysA,
+                               rowsA, valsA, nnz, ms.c, ms.bB, gB, cntB, keysB, rowsB, valsB, nullptr, n, pack, nullptr,
+                               0, wgrow, packA);
         // last pass: one workgroup per pass-B bucket (2^c columns), set B -> CSC + colptr
         const int nbC = 1 << (ms.bA + ms.bB);
         // SBLAS_TRANSPOSE_DIRECT=1: entries written from registers (experiment)
@@ -842,7 +931,7 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
                                       : k_rx2_scatter<256, kSegFinal, kR2Threads>);
         hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
                            keysB, pack >= 0 ? nullptr : rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final,
-                           vout_final, colptr, n, pack, nullptr, 0, nullptr);
+                           vout_final, colptr, n, pack, nullptr, 0, nullptr, -1);
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;
     }

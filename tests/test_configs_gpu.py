@@ -105,15 +105,17 @@ def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     A.close()
 
 
-@pytest.mark.parametrize("pack", ["1", "0"], ids=["packed", "unpacked"])
-def test_config2_transpose_full_size(torch_cuda, sb, orc, cfg2, monkeypatch, pack):
+@pytest.mark.parametrize("pack,packa", [("1", "1"), ("1", "0"), ("0", "1")],
+                         ids=["packed", "packed_b_only", "packed_a_only"])
+def test_config2_transpose_full_size(torch_cuda, sb, orc, cfg2, monkeypatch, pack, packa):
     """CSR -> CSC of the config-2 matrix (the size tools/bench_transpose.py
     times): colptr, row indices and values bit-exact against orc_transpose
-    (tranpose.h:6-43's stable scatter).  Both last-pass input forms."""
+    (tranpose.h:6-43's stable scatter).  Packed and unpacked pass-A and last-pass inputs."""
     torch = torch_cuda
     if cfg2["prefix"]:
         pytest.skip("random columns only")
     monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", pack)
+    monkeypatch.setenv("SBLAS_TRANSPOSE_PACKA", packa)
     rp, col, val = cfg2["rp"], cfg2["col"], cfg2["val"]
     nnz = int(rp[-1])
     cp, ri, cv = orc.transpose(N2, N2, rp, col, val)

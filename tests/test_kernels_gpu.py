@@ -117,13 +117,15 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "noderive", "ftile4096", "ftile3072",
+@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "nopacka", "noderive", "ftile4096", "ftile3072",
                                     "msd_c3", "msd_c5", "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
-@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows"])
+@pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows", "sparserows"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     """Stable transpose, every path: the MSD partition passes + per-bucket
     final pass (default where n > 512; pass A derives each entry's row from rowptr,
-    SBLAS_TRANSPOSE_DERIVE=0 reads an expanded row array; pass B hands the last pass one word of
+    SBLAS_TRANSPOSE_DERIVE=0 reads an expanded row array, and hands pass B one word of key bits
+    and row offset when the segments' row spans allow (SBLAS_TRANSPOSE_PACKA=0 two words; "sparserows"
+    spans too many rows, the device falls back); pass B hands the last pass one word of
     row and low column bits, SBLAS_TRANSPOSE_PACK=0 two; SBLAS_TRANSPOSE_MSD_C moves the final
     bucket width so small matrices take it too, with few, long buckets on
     "longcols"), the LSD tiles-per-workgroup path with <= 8-bit digits ("big"
@@ -143,6 +145,8 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
     if digits == "noderive":  # pass A reads an expanded row array instead of deriving rows
         monkeypatch.setenv("SBLAS_TRANSPOSE_DERIVE", "0")
+    if digits == "nopacka":  # pass A writes key and row arrays instead of one packed word
+        monkeypatch.setenv("SBLAS_TRANSPOSE_PACKA", "0")
     if digits.startswith("ftile"):  # last-pass tile forced to 4096 / 3072 entries (3072: buckets
         monkeypatch.setenv("SBLAS_TRANSPOSE_FTILE", digits[5:])  # past it take the multi-tile path)
     rng = np.random.default_rng(5)
@@ -161,6 +165,13 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         # holds thousands of row starts (pass A's row derivation takes several windows)
         m, n = 200000, 5000
         lens = rng.integers(0, 4, m) * (rng.random(m) < 0.5)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    elif case == "sparserows":  # 2^24 columns (16 key bits past pass A) and one row in 100
+        # non-empty: a segment spans > 2^16 rows, so pass A cannot pack the row offset
+        m, n = 300000, 1 << 24
+        lens = np.where(rng.random(m) < 0.01, 5, 0)
         rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
         val = rng.standard_normal(int(rp[-1]))
