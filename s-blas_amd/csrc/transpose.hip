@@ -368,8 +368,12 @@ constexpr int kSegFinalDirect = 3;  // the same, each entry written from registe
 // positions -- per wave over its contiguous quarter, then across waves --
 // is every entry's row.  Rows starting exactly at the tile's end give the
 // next tile's rc.  A tile holding more than kT row starts takes more windows.
-template <int kMaxD, int kSeg, int kT, bool kDerive = false, int kTile = kRxTile>
-__global__ __launch_bounds__(kT) void k_rx2_scatter(
+// kPkF (last pass, packed input): rows are unpacked from the staged keys, so
+// no row array is staged (less LDS: more workgroups per CU); kWpe: waves per
+// SIMD asked of the register allocator.
+template <int kMaxD, int kSeg, int kT, bool kDerive = false, int kTile = kRxTile, bool kPkF = false,
+          int kWpe = 1>
+__global__ __launch_bounds__(kT, kWpe) void k_rx2_scatter(
     const int *__restrict__ kin, const int *__restrict__ rin, const double *__restrict__ vin, long long nnz,
     int shift, int rb, SegArgs sg, const int *__restrict__ incl, int *__restrict__ kout,
     int *__restrict__ rout, double *__restrict__ vout, int *__restrict__ colptr, int n, int pack,
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
     __shared__ int lstart[kMaxD], gbase[kMaxD];
     __shared__ int wtot[kW];
     __shared__ int wmaxs[kW], s_next, s_more[2];  // kDerive
-    __shared__ int skey[kTile], srow[kTile];
+    __shared__ int skey[kTile], srow[kPkF ? 1 : kTile];
     __shared__ double sval[kTile];
     constexpr int kQ = kTile / kW;  // elements per wave per tile
     constexpr int kB = kQ / 64;             // batches per wave (16)
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                 if (w * kQ + j * 64 + lane < valid) {
                     const int pos = wcnt[w][(kk[j] >> shift) & dm] + lp[j];
                     skey[pos] = kk[j];
-                    srow[pos] = rowof(j);
+                    if constexpr (!kPkF) srow[pos] = rowof(j);
                     sval[pos] = vv[j];
                 }
             }
@@ -604,7 +608,8 @@ __global__ __launch_bounds__(kT) void k_rx2_scatter(
                     kout[g] = (srow[li] << pack) | (k & ((1 << pack) - 1));
                 } else {
                     if (kout) kout[g] = colkey(k);
-                    rout[g] = srow[li];
+                    if constexpr (kPkF) rout[g] = (int)((unsigned)k >> pack);
+                    else rout[g] = srow[li];
                 }
                 vout[g] = sval[li];
             }
@@ -929,7 +934,19 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
                                       : k_rx2_scatter<256, kSegFinalDirect, kR2Threads>)
                         : (small_tile ? k_rx2_scatter<256, kSegFinal, kR2Threads, false, 3072>
                                       : k_rx2_scatter<256, kSegFinal, kR2Threads>);
-        hipLaunchKernelGGL(kfin, dim3((unsigned)std::min(nbC, ncu * wgcu)), dim3(kR2Threads), 0, s,
+        // lean last pass (packed input, <= 7 final bits, 3072 tile; default):
+        // no row staging and 128-digit tables leave 42 KB of LDS, and 80
+        // VGPRs, so three workgroups share a CU (config 2: 332 -> 290 us).
+        // SBLAS_TRANSPOSE_FLEAN=1: lean at two per CU, =0: the staged form.
+        const char *fl_e = getenv("SBLAS_TRANSPOSE_FLEAN");
+        const int flean = (pack >= 0 && ms.c <= 7 && small_tile && !(de && atoi(de) == 1)) ? (fl_e ? atoi(fl_e) : 2) : 0;
+        int fgrid = std::min(nbC, ncu * wgcu);
+        if (flean == 1) kfin = k_rx2_scatter<128, kSegFinal, kR2Threads, false, 3072, true, 1>;
+        if (flean == 2) {
+            kfin = k_rx2_scatter<128, kSegFinal, kR2Threads, false, 3072, true, 6>;
+            fgrid = std::min(nbC, ncu * 3);
+        }
+        hipLaunchKernelGGL(kfin, dim3((unsigned)fgrid), dim3(kR2Threads), 0, s,
                            keysB, pack >= 0 ? nullptr : rowsB, valsB, nnz, 0, ms.c, gC, nullptr, colidx, rout_final,
                            vout_final, colptr, n, pack, nullptr, 0, nullptr, -1);
         SBLAS_HIP(hipGetLastError());

@@ -118,6 +118,7 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 # ----------------------------------------------------------- transpose ----
 @pytest.mark.parametrize("digits", ["default", "direct", "nopack", "nopacka", "noderive", "ftile4096", "ftile3072",
+                                    "flean1", "flean2",
                                     "msd_c3", "msd_c5", "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows", "sparserows"])
 def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
@@ -145,6 +146,8 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
         monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
     if digits == "noderive":  # pass A reads an expanded row array instead of deriving rows
         monkeypatch.setenv("SBLAS_TRANSPOSE_DERIVE", "0")
+    if digits.startswith("flean"):  # last pass unpacks rows from the staged keys (1), 3 WGs per CU (2)
+        monkeypatch.setenv("SBLAS_TRANSPOSE_FLEAN", digits[5:])
     if digits == "nopacka":  # pass A writes key and row arrays instead of one packed word
         monkeypatch.setenv("SBLAS_TRANSPOSE_PACKA", "0")
     if digits.startswith("ftile"):  # last-pass tile forced to 4096 / 3072 entries (3072: buckets
