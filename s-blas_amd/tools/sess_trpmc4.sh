@@ -1,0 +1,10 @@
+#!/bin/bash
+# FETCH_SIZE / WRITE_SIZE of the default transpose kernels (separate passes), per kernel
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out/pmc_tr4
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 150 rocprofv3 --pmc $c -d $O/$c -o run --output-format csv -- python3 s-blas_amd/tools/bench_transpose.py --mgpu= --steps 3 > $O.$c.log 2>&1 || { tail -5 $O.$c.log; exit 1; }
+done
+echo done
