@@ -198,6 +198,60 @@ def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
     A.close()
 
 
+@pytest.mark.parametrize("shape", ["one_entry", "one_row", "one_col_tall", "last_col", "tile_edge",
+                                   "dup_free_dense_row", "empty_tail_rows"])
+def test_transpose_edges(torch_cuda, sb, orc, shape):
+    """Edge shapes on the default MSD path (n > 512): a single nonzero, every
+    entry in one row, one populated column over many rows, entries only in the
+    last column, nnz exactly one tile / one past it, rows empty at the end."""
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    n = 5000
+    if shape == "one_entry":
+        m = 3
+        rp = np.array([0, 0, 1, 1], np.int64)
+        col = np.array([4321], np.int32)
+    elif shape == "one_row":
+        m = 1
+        col = np.sort(rng.choice(n, 3000, replace=False)).astype(np.int32)
+        rp = np.array([0, len(col)], np.int64)
+    elif shape == "one_col_tall":
+        m = 20000
+        rp = np.arange(m + 1, dtype=np.int64)
+        col = np.full(m, 777, np.int32)
+    elif shape == "last_col":
+        m = 4096
+        rp = np.arange(m + 1, dtype=np.int64)
+        col = np.full(m, n - 1, np.int32)
+    elif shape == "tile_edge":  # 4097 nonzeros: one full tile and one entry
+        m = 4097
+        rp = np.arange(m + 1, dtype=np.int64)
+        col = rng.integers(0, n, m).astype(np.int32)
+    elif shape == "dup_free_dense_row":  # every column of one row, then sparse rows
+        m = 700
+        lens = np.concatenate([[n], rng.integers(0, 5, m - 1)])
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.arange(n)] + [np.sort(rng.choice(n, L, replace=False)) for L in lens[1:]]).astype(np.int32)
+    else:  # empty_tail_rows
+        m = 50000
+        lens = np.concatenate([rng.integers(1, 6, 1000), np.zeros(m - 1000, np.int64)])
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens[:1000]]).astype(np.int32)
+    val = rng.standard_normal(len(col))
+    nnz = int(rp[-1])
+    cp, ri, cv = orc.transpose(m, n, rp, col, val)
+    A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    dcp = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    dri = torch.zeros(max(nnz, 1), dtype=torch.int32, device="cuda")
+    dcv = torch.zeros(max(nnz, 1), dtype=torch.float64, device="cuda")
+    A.transpose(dcp.data_ptr(), dri.data_ptr(), dcv.data_ptr())
+    torch.cuda.synchronize()
+    A.close()
+    assert np.array_equal(dcp.cpu().numpy(), cp)
+    assert np.array_equal(dri.cpu().numpy()[:nnz], ri)
+    assert np.array_equal(dcv.cpu().numpy()[:nnz], cv)
+
+
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide"])
 @pytest.mark.parametrize("ngpu", [1, 2, 3, 5])
 def test_transpose_mgpu_bit_exact(torch_cuda, sb, orc, case, ngpu):
