@@ -16,6 +16,7 @@ libsblas's.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 
@@ -245,7 +246,10 @@ class DistSpMVCyclic:
         # of every rank, then the rest), each its own handle; the all-gather
         # of half A runs while half B's kernel runs
         # (needs two chunks per rank to split)
-        self.overlap = bool(overlap) and plan.world > 1 and plan.nchunks > plan.world
+        # SBLAS_DIST_XCHG_W1=1 (with a process group at world size 1): run the
+        # exchange and placement path anyway, so one GPU exercises it over RCCL
+        self.xw1 = os.environ.get("SBLAS_DIST_XCHG_W1") == "1" and dist is not None
+        self.overlap = bool(overlap) and (plan.world > 1 or self.xw1) and plan.nchunks > plan.world
         self._work = []
         if self.overlap:
             self.hA, self.strideA, self.strideB, self.rows_a = overlap_halves(plan)
@@ -288,7 +292,7 @@ class DistSpMVCyclic:
         out.copy_(self.torch.cat(chunks).to(out.device))
 
     def exchange(self, stream=None) -> None:
-        if self.plan.world == 1:
+        if self.plan.world == 1 and not self.xw1:
             return
         if self.overlap:
             yB = self.y_local[self.strideA: self.strideA + self.strideB]
@@ -320,7 +324,7 @@ class DistSpMVCyclic:
             self.plan.m, self.y_full.data_ptr(), stream), "assemble_cyclic")
 
     def result(self):
-        if self.plan.world == 1:
+        if self.plan.world == 1 and not self.xw1:
             return self.y_local[: self.plan.m]
         return self.y_full
 
