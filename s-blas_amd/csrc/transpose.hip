@@ -294,33 +294,47 @@ __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict
                                                            const int *__restrict__ rowptr = nullptr, int m = 0,
                                                            int *__restrict__ wgrow = nullptr)
 {
-    __shared__ int h[kRx2MaxDigits];
+    // digits <= 128: one private histogram per wave (waves do not contend
+    // for the same LDS words), summed at the end
+    constexpr int kCW = kCntThreads / 64;
+    __shared__ int h[kRx2MaxDigits > 128 * kCW ? kRx2MaxDigits : 128 * kCW];
+    __shared__ int s_first;
     const int D = 1 << rb;
-    for (int d = threadIdx.x; d < D; d += kCntThreads) h[d] = 0;
-    __syncthreads();
+    const bool priv = D <= 128;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int *hw = priv ? h + wv * 128 : h;
+    for (int d = threadIdx.x; d < (priv ? 128 * kCW : D); d += kCntThreads) h[d] = 0;
     const int wg = (int)blockIdx.x;
     long long p0, p1;
     seg_range(kSeg, g, wg, nnz, p0, p1);
-    if (wgrow && threadIdx.x < 2) {
-        // thread 0: the row holding the segment's first entry (largest r with
-        // rowptr[r] <= p0); thread 1: the row of its last; wgrow[nseg + wg] =
-        // the rows the segment spans beyond its first (0 when empty)
-        const long long p = threadIdx.x == 0 ? p0 : max(p0, p1 - 1);
-        int lo = 0, hi = m - 1;
+    int lo = 0;
+    if (wgrow && wv < 2) {
+        // wave 0: the row holding the segment's first entry (largest r with
+        // rowptr[r] <= p0); wave 1: the row of its last; wgrow[nseg + wg] =
+        // the rows the segment spans beyond its first (0 when empty).  A
+        // 64-ary search: each round the 64 lanes probe evenly spaced rows.
+        const long long p = wv == 0 ? p0 : max(p0, p1 - 1);
+        int hi = m - 1;  // rowptr[lo] <= p
         while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (rowptr[mid] <= p) lo = mid;
-            else hi = mid - 1;
+            const int step = (hi - lo + 63) / 64;
+            const long long r = (long long)lo + (long long)(lane + 1) * step;
+            const bool ok = r <= hi && rowptr[r] <= p;
+            const int k = __popcll(__ballot(ok));  // ok holds for a prefix of the lanes
+            lo += k * step;
+            hi = min(hi, lo + step - 1);
         }
-        const int first = __shfl(lo, 0, 64);
-        if (threadIdx.x == 0) wgrow[wg] = lo;
-        if (threadIdx.x == 1) wgrow[(int)gridDim.x + wg] = p1 > p0 ? lo - first : 0;
+        if (wv == 0 && lane == 0) {
+            wgrow[wg] = lo;
+            s_first = lo;
+        }
     }
+    __syncthreads();  // histograms zeroed, s_first set
+    if (wgrow && wv == 1 && lane == 0) wgrow[(int)gridDim.x + wg] = p1 > p0 ? lo - s_first : 0;
     // 16-B loads over the aligned body (keys arrays are 16-B aligned), single
     // keys for the head and tail
     const long long q0 = min(p1, (p0 + 3) & ~3LL), q1 = max(q0, p1 & ~3LL);
-    for (long long i = p0 + threadIdx.x; i < q0; i += kCntThreads) atomicAdd(&h[(keys[i] >> shift) & (D - 1)], 1);
-    for (long long i = q1 + threadIdx.x; i < p1; i += kCntThreads) atomicAdd(&h[(keys[i] >> shift) & (D - 1)], 1);
+    for (long long i = p0 + threadIdx.x; i < q0; i += kCntThreads) atomicAdd(&hw[(keys[i] >> shift) & (D - 1)], 1);
+    for (long long i = q1 + threadIdx.x; i < p1; i += kCntThreads) atomicAdd(&hw[(keys[i] >> shift) & (D - 1)], 1);
     const int4 *k4 = reinterpret_cast<const int4 *>(keys + q0);
     const long long n4 = (q1 - q0) >> 2;
     constexpr int kU = 8;
@@ -334,14 +348,19 @@ __global__ __launch_bounds__(kCntThreads) void k_rx2_count(const int *__restrict
 #pragma unroll
         for (int u = 0; u < kU; ++u)
             if (v[u].x != -1) {
-                atomicAdd(&h[(v[u].x >> shift) & (D - 1)], 1);
-                atomicAdd(&h[(v[u].y >> shift) & (D - 1)], 1);
-                atomicAdd(&h[(v[u].z >> shift) & (D - 1)], 1);
-                atomicAdd(&h[(v[u].w >> shift) & (D - 1)], 1);
+                atomicAdd(&hw[(v[u].x >> shift) & (D - 1)], 1);
+                atomicAdd(&hw[(v[u].y >> shift) & (D - 1)], 1);
+                atomicAdd(&hw[(v[u].z >> shift) & (D - 1)], 1);
+                atomicAdd(&hw[(v[u].w >> shift) & (D - 1)], 1);
             }
     }
     __syncthreads();
-    for (int dd = threadIdx.x; dd < D; dd += kCntThreads) counts[seg_count_idx(kSeg, g, wg, D, dd)] = h[dd];
+    for (int dd = threadIdx.x; dd < D; dd += kCntThreads) {
+        int c = h[dd];
+        if (priv)
+            for (int q = 1; q < kCW; ++q) c += h[q * 128 + dd];
+        counts[seg_count_idx(kSeg, g, wg, D, dd)] = c;
+    }
 }
 
 // Scatter: workgroup b sorts tiles [b*S, (b+1)*S) in order.  Wave w ranks
