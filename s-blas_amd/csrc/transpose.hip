@@ -3,11 +3,18 @@
 // Semantics of sptrsv/sptrsv_v1/src/tranpose.h:6-43 (matrix_transposition):
 // column histogram, exclusive scan, then a STABLE scatter in row order, so
 // row indices ascend inside every column and equal-(row,col) duplicates keep
-// their CSR order.  GPU form: a stable LSD radix sort of the nonzeros (in
-// CSR order) keyed by column, carrying (row, value), 8 bits per pass
-// (ceil(log2 n / 8) passes); stability makes rows ascend inside each column
-// exactly as the reference's ordered scatter does.  colptr is read off the
-// sorted keys.
+// their CSR order.  GPU forms, both stable sorts of the nonzeros (in CSR
+// order) by column, so rows ascend inside each column exactly as the
+// reference's ordered scatter leaves them:
+//  * default (n > 512): MSD -- two stable partition passes on the high column
+//    bits (pass A over fixed segments of the CSR order, deriving each entry's
+//    row from rowptr; pass B inside each pass-A bucket), then one pass per
+//    final bucket of 2^c columns that counts, ranks and writes its run in
+//    column order with its colptr entries.  Between the passes an entry
+//    travels as one packed word (the key bits still needed + the row or its
+//    offset in the segment) and its value;
+//  * LSD radix passes of <= 8-bit digits carrying (key, row, value), colptr
+//    read off the sorted keys (n <= 512, or SBLAS_TRANSPOSE_ALGO=lsd).
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
