@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--algos", default="xsort,panel,rowsplit")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warm-x", action="store_true",
+                    help="experiment: read x after each scrub (x in the Infinity Cache and L2s "
+                         "when the timed span starts; the matrix stays cold)")
     ap.add_argument("--floor", action="store_true",
                     help="also time a cold streaming read of the slice's byte count")
     args = ap.parse_args()
@@ -72,6 +75,8 @@ def main():
                 spans = []
                 for k in range(args.reps + 2):
                     scrub.sum(dtype=torch.int64)
+                    if args.warm_x:
+                        x.sum()
                     torch.cuda.synchronize()
                     spans.append(A.spmv_timed(algos[name], 1.0, x.data_ptr(), 0.5, y.data_ptr(),
                                               stream.cuda_stream))
