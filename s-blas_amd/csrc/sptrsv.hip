@@ -181,6 +181,20 @@ __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long lon
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Poll back-off of a wave whose lanes all still wait (SBLAS_TRSV_SLEEP):
+// slp >= 0 sleeps slp x 64 clocks after every poll; slp < 0 doubles the
+// sleep after each poll on which no lane of the wave advanced, up to 2^-slp,
+// and drops it back to one on progress.  Every polling lane is an L2 request
+// the producers also need, so fewer polls can shorten the chain.
+__device__ __forceinline__ void trsv_backoff(int units)
+{
+    // s_sleep takes an immediate: whole 8-unit steps, then the remainder
+    for (; units >= 8; units -= 8) __builtin_amdgcn_s_sleep(8);
+    if (units & 4) __builtin_amdgcn_s_sleep(4);
+    if (units & 2) __builtin_amdgcn_s_sleep(2);
+    if (units & 1) __builtin_amdgcn_s_sleep(1);
+}
+
 // kLevel (algo 3): tickets walk the level-ordered CSR of the level-set
 // analysis (position t holds row lrow[t]; rows of one level are contiguous),
 // so the 64 rows of a wave belong to one level and become ready together
@@ -189,10 +203,11 @@ template <bool kLevel>
 __global__ __launch_bounds__(256) void k_trsv_pull(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, int n, int backward, const double *__restrict__ b,
-    unsigned long long *xbits, unsigned *ctl, const int *__restrict__ lrow)
+    unsigned long long *xbits, unsigned *ctl, const int *__restrict__ lrow, int slp)
 {
     constexpr int kBatch = 8;
     const int lane = threadIdx.x & 63;
+    const int slp_cap = slp < 0 ? 1 << min(-slp, 10) : slp;
     for (;;) {
         int t0 = 0;
         if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? n : (int)atomicAdd(&ctl[0], 64u);
@@ -218,13 +233,16 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
         }
         bool pending = live;
         unsigned spins = 0;
+        int cur = 1;  // adaptive back-off (slp < 0), wave-uniform
         // current dependency cached in registers: a spin costs ONE sc1 load
         int cj = (live && j < jend) ? col[j] : 0;
         double vj = (live && j < jend) ? val[j] : 0.0;
         while (__any(pending)) {
+            bool adv = false;
             if (pending && j < jend) {
                 const unsigned long long x0 = ld_sc1_u64(xbits + cj);
                 if (x0 != kXPending) {
+                    adv = true;
                     sum += vj * __longlong_as_double((long long)x0);
                     ++j;
                     if (j < jend) {  // ready: batch the next dependencies
@@ -263,12 +281,19 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
                 __hip_atomic_store(xbits + i, (unsigned long long)__double_as_longlong(xi),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 pending = false;
+                adv = true;
             }
             if (__any(pending)) {
                 // a timeout voids the whole solve (every wave exits)
-                __builtin_amdgcn_s_sleep(1);
+                if (slp < 0) {
+                    cur = __any(adv) ? 1 : min(2 * cur, slp_cap);
+                    trsv_backoff(cur);
+                } else {
+                    trsv_backoff(slp_cap);
+                }
                 if ((++spins & 1023u) == 0) {
-                    if (spins > kSpinLimit) {
+                    // the limit keeps ~1 s of polling at any back-off
+                    if (spins > kSpinLimit / (unsigned)max(slp_cap, 1)) {
                         if (lane == 0) atomicOr(&ctl[kAbort], 1u);
                         return;
                     }
@@ -900,10 +925,14 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     if (algo == 3) SBLAS_TRY(build_levelset(T, s));
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     const int grid = grid_for(T->device);
+    // poll back-off of the pull executors (k_trsv_pull header); 1 = one
+    // s_sleep(1) per poll, the measured default
+    int slp = 1;
+    if (const char *e = getenv("SBLAS_TRSV_SLEEP")) slp = std::max(-10, std::min(64, atoi(e)));
     if (algo == 3) {  // sync-free pull, tickets in level order
         fill_pending((unsigned long long *)d_x, T->n, s);
         hipLaunchKernelGGL(k_trsv_pull<true>, dim3(grid), dim3(256), 0, s, T->lrp, T->lcol, T->lval, T->n,
-                           T->substitution, d_b, (unsigned long long *)d_x, T->ctl, T->lrow);
+                           T->substitution, d_b, (unsigned long long *)d_x, T->ctl, T->lrow, slp);
     } else if (algo == 0) {
         SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
         SBLAS_HIP(hipMemsetAsync(T->left, 0, sizeof(double) * T->n, s));
@@ -912,7 +941,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     } else {
         fill_pending((unsigned long long *)d_x, T->n, s);
         hipLaunchKernelGGL(k_trsv_pull<false>, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
-                           T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl, nullptr);
+                           T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl, nullptr, slp);
     }
     SBLAS_HIP(hipGetLastError());
     unsigned h[kCtlBytes / 4] = {0};
