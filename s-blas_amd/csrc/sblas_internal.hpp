@@ -209,6 +209,7 @@ struct XsPlan {
     int nranges = 0, nwide = 0, nitems = 0, grid = 0, nt = 0;
     XsRange *ranges = nullptr;
     int *wide = nullptr;         // [nwide] range ids
+    XsRange *wranges = nullptr;  // [nwide] the wide ranges' records (k_xsort_reduce)
     long long *blk = nullptr;
     uint32_t *key = nullptr;     // owns the chunk storage (keys and values)
     double *val = nullptr;       // values inside it (interleaved per chunk by default)

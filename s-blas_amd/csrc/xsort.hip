@@ -680,14 +680,15 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
 
 // Wide ranges: y = alpha * sum_k partial[k] (+ beta*y), XCD slots in order.
 // All 8 partial loads (and y) of a row are issued before the first add.
+// wr[] holds the wide ranges' records in wide order: one scalar load ahead of
+// the partials instead of an index and then the record.
 template <bool kBeta>
-__global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict__ ranges,
-                                                      const int *__restrict__ wide,
+__global__ __launch_bounds__(256) void k_xsort_reduce(const XsRange *__restrict__ wr,
                                                       const double *__restrict__ partial,
                                                       double alpha, double beta,
                                                       double *__restrict__ y)
 {
-    const XsRange R = ranges[wide[blockIdx.y]];
+    const XsRange R = wr[blockIdx.y];
     for (int r = blockIdx.x * 256 + threadIdx.x; r < R.nrows; r += gridDim.x * 256) {
         const double *p = partial + R.pbase + r;
         double v[8];
@@ -707,6 +708,7 @@ void free_xsort_plan(sblas_csr_s &A)
     XsPlan &P = A.xs;
     (void)hipFree(P.ranges);
     (void)hipFree(P.wide);
+    (void)hipFree(P.wranges);
     (void)hipFree(P.blk);
     (void)hipFree(P.key);  // P.val points into the same allocation
     (void)hipFree(P.qitems);
@@ -1113,6 +1115,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
 
     SBLAS_HIP(hipMalloc(&P.ranges, sizeof(XsRange) * std::max(I, 1)));
     SBLAS_HIP(hipMalloc(&P.wide, sizeof(int) * std::max<size_t>(wide.size(), 1)));
+    SBLAS_HIP(hipMalloc(&P.wranges, sizeof(XsRange) * std::max<size_t>(wide.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.blk, sizeof(long long) * blk.size()));
     SBLAS_HIP(hipMalloc(&P.key, hbuf.size()));
     P.val = (double *)((unsigned char *)P.key + ((unsigned char *)chunk_vals(0) - hbuf.data()));
@@ -1138,8 +1141,12 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMemcpy(P.rtasks, rtasks.data(), sizeof(int2) * rtasks.size(), hipMemcpyHostToDevice));
     P.epoch = 0;
     if (I) SBLAS_HIP(hipMemcpy(P.ranges, ranges.data(), sizeof(XsRange) * I, hipMemcpyHostToDevice));
-    if (!wide.empty())
+    if (!wide.empty()) {
         SBLAS_HIP(hipMemcpy(P.wide, wide.data(), sizeof(int) * wide.size(), hipMemcpyHostToDevice));
+        std::vector<XsRange> wr;
+        for (int i : wide) wr.push_back(ranges[(size_t)i]);
+        SBLAS_HIP(hipMemcpy(P.wranges, wr.data(), sizeof(XsRange) * wr.size(), hipMemcpyHostToDevice));
+    }
     SBLAS_HIP(hipMemcpy(P.blk, blk.data(), sizeof(long long) * blk.size(), hipMemcpyHostToDevice));
     if (nchunks) {
         SBLAS_HIP(hipMemcpy(P.key, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
@@ -1296,10 +1303,10 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     if (P.nwide && !P.fused) {
         const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
         if (b)
-            SBLAS_LAUNCH(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.ranges, P.wide, P.partial, alpha, beta,
+            SBLAS_LAUNCH(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.wranges, P.partial, alpha, beta,
                          y);
         else
-            SBLAS_LAUNCH(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.ranges, P.wide, P.partial, alpha, beta,
+            SBLAS_LAUNCH(k_xsort_reduce<false>, grid, dim3(256), 0, s, P.wranges, P.partial, alpha, beta,
                          y);
     }
     SBLAS_HIP(hipGetLastError());
