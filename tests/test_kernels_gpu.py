@@ -316,6 +316,25 @@ def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     T.close()
 
 
+@pytest.mark.parametrize("sleep", ["0", "16", "-5"])
+@pytest.mark.parametrize("algo", [1, 3])
+def test_sptrsv_pull_backoff(torch_cuda, sb, monkeypatch, algo, sleep):
+    """The pull executors' poll back-off (SBLAS_TRSV_SLEEP: none, fixed,
+    adaptive) changes only when waves poll, never the result: exact KAT."""
+    monkeypatch.setenv("SBLAS_TRSV_SLEEP", sleep)
+    torch = torch_cuda
+    for name, sub in (("qh768", 0), ("ash85", 1)):
+        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{'fwd' if sub == 0 else 'bwd'}.npz"))
+        cp, ri, cv, b = g["colptr"], g["rowidx"], g["val"], g["b"]
+        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
+        xd = torch.zeros(len(cp) - 1, dtype=torch.float64, device="cuda")
+        T = sb.DeviceTRSV(0, len(cp) - 1, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sub)
+        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xd.cpu().numpy(), g["x_ref"])  # exact KAT
+        T.close()
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     """Random lower-triangular with long chains and a long column/row."""
