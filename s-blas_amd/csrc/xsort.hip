@@ -802,17 +802,26 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     std::vector<XsRange> ranges;
     auto build_ranges = [&](double cap) {
         ranges.clear();
+        // cut(r): the first row always, then rows while the range's cost stays
+        // <= cap, at most rows_cap rows.  The cost grows strictly with the
+        // entry count rp[e] - rp[r], so the end is a binary search over e
+        // (O(log m) cost evaluations per range instead of one per row: the
+        // cap search below runs build_ranges many times over all m rows).
         auto cut = [&](int r, bool wide, long long &cnt) {
             const int start = r;
-            cnt = 0;
-            while (r < m && r - start < rows_cap) {
-                const long long len = rp[r + 1] - rp[r];
-                const double c = (double)(cnt + len);
-                if (r > start && (wide ? wide_cost(c) : narrow_cost(c)) > cap) break;
-                cnt += len;
-                ++r;
+            const int emax = (int)std::min<long long>(m, (long long)start + rows_cap);
+            auto fits = [&](int e) {
+                const double c = (double)(rp[e] - rp[start]);
+                return (wide ? wide_cost(c) : narrow_cost(c)) <= cap;
+            };
+            int lo = start + 1, hi = emax;  // answer in [lo, hi]; lo always taken
+            while (lo < hi) {
+                const int mid = lo + (hi - lo + 1) / 2;
+                if (fits(mid)) lo = mid;
+                else hi = mid - 1;
             }
-            return r;
+            cnt = rp[lo] - rp[start];
+            return lo;
         };
         int r = 0;
         long long wide_entries = 0;
