@@ -41,9 +41,12 @@
 // chunks from LDS counters (xs_stream_dyn), so a team that drains its own
 // sub-item continues on its partner's and both halves end together.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <utility>
 #include <vector>
 
@@ -728,6 +731,15 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     const int m = A.m, n = A.n;
     const long long nnz = A.nnz;
     const std::vector<int> &rp = A.h_rowptr;
+    // SBLAS_XS_TIMING: plan-build phase times on stderr (seconds since the last mark)
+    const bool timing = getenv("SBLAS_XS_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char *phase) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "xsort plan: %-10s %.3f s\n", phase, std::chrono::duration<double>(t - t_last).count());
+        t_last = t;
+    };
 
     // column groups: G = 8q groups of Wg < 2^18 columns (the all-ones column
     // field is the padding key) and ~1 MiB of x (an XCD's current group plus
@@ -871,22 +883,33 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         return SBLAS_ERR_UNSUPPORTED;
     }
 
-    // host copies of the CSR entries
-    std::vector<int> hcol((size_t)nnz);
-    std::vector<double> hval((size_t)nnz);
+    mark("planner");
+    // host copies of the CSR entries (uninitialised: the copies fill them)
+    std::unique_ptr<int[]> hcol(new int[(size_t)std::max<long long>(nnz, 1)]);
+    std::unique_ptr<double[]> hval(new double[(size_t)std::max<long long>(nnz, 1)]);
     if (nnz) {
-        SBLAS_HIP(hipMemcpy(hcol.data(), A.col, sizeof(int) * nnz, hipMemcpyDeviceToHost));
-        SBLAS_HIP(hipMemcpy(hval.data(), A.val, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+        SBLAS_HIP(hipMemcpy(hcol.get(), A.col, sizeof(int) * nnz, hipMemcpyDeviceToHost));
+        SBLAS_HIP(hipMemcpy(hval.get(), A.val, sizeof(double) * nnz, hipMemcpyDeviceToHost));
     }
 
+    mark("d2h");
     // pass 1: every block (range, group) bucketed and sorted by (column, row)
-    // once, kept for the fill (both key formats are sized from it)
+    // once, kept for the fill (both key formats are sized from it).  One
+    // range per task for the bucketing (a wide range holds ~13x a narrow
+    // one's entries, and they sit together at the heavy rows), then the
+    // blocks are sorted as tasks of their own.
     const size_t nblk = (size_t)I * G;
     std::vector<std::vector<std::pair<uint32_t, double>>> bk(nblk);
     bool bad = false;
-#pragma omp parallel for schedule(dynamic, 16) reduction(|| : bad)
+#pragma omp parallel for schedule(dynamic, 1) reduction(|| : bad)
     for (int i = 0; i < I; ++i) {
         const XsRange &R = ranges[i];
+        std::vector<int> cnt(G, 0);
+        for (int e = rp[R.row0]; e < rp[R.row0 + R.nrows]; ++e) {
+            const int c = hcol[e];
+            if (c >= 0 && c < n) ++cnt[c / Wg];
+        }
+        for (int g = 0; g < G; ++g) bk[(size_t)i * G + g].reserve(cnt[g]);
         for (int r = R.row0; r < R.row0 + R.nrows; ++r) {
             for (int e = rp[r]; e < rp[r + 1]; ++e) {
                 const int c = hcol[e];
@@ -900,12 +923,14 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
                 bk[(size_t)i * G + g].push_back({(cp << kXsRowBits) | lr, hval[e]});
             }
         }
-        for (int g = 0; g < G; ++g) {
-            auto &bb = bk[(size_t)i * G + g];
-            if (!nosort)
-                std::stable_sort(bb.begin(), bb.end(),
-                                 [](const std::pair<uint32_t, double> &u,
-                                    const std::pair<uint32_t, double> &v) { return u.first < v.first; });
+    }
+    if (!nosort) {
+#pragma omp parallel for schedule(dynamic, 4)
+        for (long long k = 0; k < (long long)nblk; ++k) {
+            auto &bb = bk[(size_t)k];
+            std::stable_sort(bb.begin(), bb.end(),
+                             [](const std::pair<uint32_t, double> &u,
+                                const std::pair<uint32_t, double> &v) { return u.first < v.first; });
         }
     }
     if (bad) {
@@ -949,13 +974,22 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     for (size_t k = 0; k < nblk; ++k) blk[k + 1] = blk[k] + (k24 ? n24[k] : n32[k]);
     const long long nchunks = blk.back();
 
+    mark("pass1");
     // pass 2: fill every chunk (lane-transposed, header comment / K24 notes)
     // 32-bit keys, interleaved (default): per chunk 1 KiB of keys then 2 KiB
     // of values, ONE 3-KiB run in HBM; split (SBLAS_XS_KV=0): all keys, then
     // all values.  K24: 3616-B chunks, keys | values | header.
     const bool kv = !(getenv("SBLAS_XS_KV") && atoi(getenv("SBLAS_XS_KV")) == 0);
     const size_t cbytes = k24 ? (size_t)kK24Bytes : (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
-    std::vector<unsigned char> hbuf((size_t)std::max<long long>(nchunks, 1) * cbytes);
+    // every byte of every chunk is written by the fill below: no zeroing pass
+    struct HostBuf {
+        std::unique_ptr<unsigned char[]> p;
+        size_t n;
+        unsigned char *data() const { return p.get(); }
+        size_t size() const { return n; }
+    };
+    const size_t hb_n = (size_t)std::max<long long>(nchunks, 1) * cbytes;
+    const HostBuf hbuf{std::unique_ptr<unsigned char[]>(new unsigned char[hb_n]), hb_n};
     auto chunk_keys = [&](long long c) {
         return (uint32_t *)(hbuf.data() + ((kv || k24) ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
     };
@@ -1028,6 +1062,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     }
     { std::vector<std::vector<std::pair<uint32_t, double>>>().swap(bk); }
 
+    mark("pass2");
     // sub-items, wide partial slots, then items (pairs) in XCD queues
     std::vector<int> wide, nsub;
     std::vector<std::vector<int>> wsub(8);
@@ -1160,6 +1195,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     if (nchunks) {
         SBLAS_HIP(hipMemcpy(P.key, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
     }
+    mark("h2d");
     SBLAS_HIP(hipMemcpy(P.qitems, qflat.data(), sizeof(int) * qflat.size(), hipMemcpyHostToDevice));
     {
         const size_t rl = (size_t)G + 5;
@@ -1178,6 +1214,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMalloc(&P.xrec, sizeof(long long) * xrec.size()));
         SBLAS_HIP(hipMemcpy(P.xrec, xrec.data(), sizeof(long long) * xrec.size(), hipMemcpyHostToDevice));
     }
+    mark("tail");
     P.ready = true;
     return SBLAS_OK;
 }
