@@ -904,21 +904,32 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     std::vector<double> atile;
     P.sparse_nnz = 0;
 
-    std::vector<int> U;
+    // 16-row blocks: the distinct columns of each (sorted) decide whether the
+    // block is dense enough for the MFMA tile; blocks are analysed in parallel
+    // (a sort per block), then assembled in block order
     const int nblk = (m + 15) / 16;
+    std::vector<std::vector<int>> Us((size_t)nblk);
+    std::vector<char> dense((size_t)nblk, 0);
+#pragma omp parallel for schedule(dynamic, 4)
     for (int b = 0; b < nblk; ++b) {
         const int r0 = b * 16, r1 = std::min(m, r0 + 16);
-        U.assign(hcol.begin() + rp[r0], hcol.begin() + rp[r1]);
+        std::vector<int> U(hcol.begin() + rp[r0], hcol.begin() + rp[r1]);
         std::sort(U.begin(), U.end());
         U.erase(std::unique(U.begin(), U.end()), U.end());
         const long long nz = rp[r1] - rp[r0];
-        const bool dense = P.fill_thresh <= 1.0 && !U.empty() &&
+        dense[(size_t)b] = P.fill_thresh <= 1.0 && !U.empty() &&
                            (double)nz >= P.fill_thresh * 16.0 * (double)U.size();
-        if (!dense) {
+        if (dense[(size_t)b]) Us[(size_t)b] = std::move(U);
+    }
+    for (int b = 0; b < nblk; ++b) {
+        const int r0 = b * 16, r1 = std::min(m, r0 + 16);
+        const long long nz = rp[r1] - rp[r0];
+        if (!dense[(size_t)b]) {
             for (int r = r0; r < r1; ++r) srows.push_back(r);
             P.sparse_nnz += nz;
             continue;
         }
+        const std::vector<int> &U = Us[(size_t)b];
         const int nch = ((int)U.size() + 3) / 4;
         const size_t t0 = atile.size();
         atile.resize(t0 + (size_t)nch * 64, 0.0);
