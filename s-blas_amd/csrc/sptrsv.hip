@@ -208,6 +208,10 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
     constexpr int kBatch = 8;
     const int lane = threadIdx.x & 63;
     const int slp_cap = slp < 0 ? 1 << min(-slp, 10) : slp;
+    // spin limit of ~1 s of polling at a fixed back-off; the adaptive one
+    // mixes short and long sleeps (a wave whose other lanes advance keeps
+    // sleeping short), so it keeps 1/8 of the count: >= ~2 s, <= ~2 min
+    const unsigned spin_lim = kSpinLimit / (unsigned)(slp < 0 ? 8 : max(slp_cap, 1));
     for (;;) {
         int t0 = 0;
         if (lane == 0) t0 = ld_sc1_i32((const int *)&ctl[kAbort]) ? n : (int)atomicAdd(&ctl[0], 64u);
@@ -292,8 +296,7 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
                     trsv_backoff(slp_cap);
                 }
                 if ((++spins & 1023u) == 0) {
-                    // the limit keeps ~1 s of polling at any back-off
-                    if (spins > kSpinLimit / (unsigned)max(slp_cap, 1)) {
+                    if (spins > spin_lim) {
                         if (lane == 0) atomicOr(&ctl[kAbort], 1u);
                         return;
                     }
