@@ -33,6 +33,15 @@ bitwise repeatable (LDS atomics); `--algo panel` (XCD-affine column panels of
 the row-split kernel) is the fastest bitwise-deterministic kernel.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Drivers (choose_driver): under a launcher (WORLD_SIZE set) one process per
+GPU over torch.distributed + RCCL.  Without one, `--gpus N` (N > 1) runs ONE
+process that drives N GPUs through the C-ABI context (sblas_ctx_*:
+ncclCommInitAll over devices 0..N-1, resident slices, per-device kernels,
+ncclAllGather or ncclAllReduce of y), the reference's own shape
+(dspmv_test.cu:355-383 -> dspmv_mgpu_v1.cu:16-280: one host call drives all
+GPUs); `--driver ctx` forces it at N = 1.  N above the visible devices exits
+non-zero instead of measuring fewer GPUs.
+
 Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes per
 launch (DESIGN.md: 12*nnz + 4*(m+1) + 8*n + 8*m + 8*m[beta!=0]) / average
 duration of the SpMV kernel measured with HIP events on the launch stream.
@@ -104,6 +113,30 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
     }
 
 
+def choose_driver(gpus: int, env, ndev: int, requested: str = "auto") -> str:
+    """How `bench.py --gpus N` runs: "torch" (one process per GPU, started by
+    a launcher that set WORLD_SIZE), "ctx" (one process driving N GPUs through
+    sblas_ctx), or "single" (one process, one GPU, the persistent device
+    API).  Raises ValueError (-> non-zero exit) when N cannot be measured as
+    asked -- never silently fewer GPUs."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least one GPU")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if requested == "ctx" and world > 1:
+            raise ValueError("--driver ctx drives every GPU from one process: run it without a launcher")
+        if world != gpus:
+            raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE {world} ranks")
+        return "ctx" if requested == "ctx" else "torch"
+    if gpus > ndev:
+        raise ValueError(f"--gpus {gpus} but {ndev} GPU(s) visible: refusing to measure fewer GPUs")
+    if requested == "torch" and gpus > 1:
+        raise ValueError("--driver torch needs a launcher (torch.distributed.run) for --gpus > 1")
+    if gpus == 1 and requested != "ctx":
+        return "single"
+    return "ctx"
+
+
 def pmc_traffic(algo_name: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary
     (profiles/pmc_<algo>.json, written by tools/pmc_traffic.py), or None."""
@@ -115,6 +148,192 @@ def pmc_traffic(algo_name: str):
             return float(json.load(fh)["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+def run_ctx(args) -> int:
+    """One process drives args.gpus GPUs through the C-ABI context
+    (csrc/ctx.hip): ncclCommInitAll over devices 0..N-1, each device's slice
+    resident, per-device SpMV kernels, then the exchange (ncclAllGather +
+    device placement, or the literal ncclAllReduce of the zero-padded y).
+    A cold step: a 1 GiB sweep on every device, then sblas_ctx_spmv_ex with
+    its timing protocol (each stream waits on the device while the host
+    enqueues the step, a one-word all-reduce lines the devices up), so a
+    device's span runs from its start event to the end of its exchange; the
+    step is the max over devices.  Replaces dspmv_test.cu:355-383 ->
+    dspmv_mgpu_v1.cu:16-280 (one host call driving every GPU)."""
+    import torch
+    import sblas
+
+    N = args.gpus
+    algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
+                "xsort": sblas.XSORT}
+    n = args.nrows
+    rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
+    nnz = int(rowptr[-1])
+    t_gen = time.perf_counter()
+    col, val = sblas.gen_synth_rows(n, rowptr, 0, n, args.heavy, args.light,
+                                    prefix=args.cols == "prefix", seed=42)
+    x_h = sblas.gen_vector(n, 43)
+    t_gen = time.perf_counter() - t_gen
+    exchange = sblas.CTX_ALLREDUCE if args.exchange == "allreduce" else sblas.CTX_ALLGATHER
+    partition = 1 if (args.partition == "nnz" or exchange == sblas.CTX_ALLREDUCE) else 0
+    auto = args.algo == "auto"
+    if auto:
+        args.algo = "xsort" if nnz / N >= 2e6 and n * 8 <= 120 * 2**20 else "panel"
+    # RCCL prints its version banner on stdout at communicator creation; the
+    # contract's stdout is ONE JSON line, so fd 1 points at stderr meanwhile
+    sys.stdout.flush()
+    saved_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        ctx = sblas.DeviceCtx(N)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved_fd, 1)
+        os.close(saved_fd)
+    t0 = time.perf_counter()
+    try:
+        ctx.upload(n, n, rowptr, col, val, algo_ids[args.algo], partition, exchange)
+    except sblas.SblasError:
+        if not (auto and args.algo == "xsort"):
+            raise
+        args.algo = "panel"
+        ctx.upload(n, n, rowptr, col, val, algo_ids[args.algo], partition, exchange)
+    plan_s = time.perf_counter() - t0
+    ctx.set_x(x_h)
+    ctx.set_y(np.zeros(n))
+    info = [ctx.slice_info(d) for d in range(N)]
+    beta_nz = BETA != 0.0
+    # per-device algorithmic bytes (sblas_spmv_algorithmic_bytes; beta != 0)
+    dev_bytes = [b if beta_nz else b - 8 * r for r, _, b in info]
+    delay_us = 300.0 + 150.0 * N
+    for _ in range(args.warmup):
+        ctx.spmv_ex(ALPHA, BETA)
+    scrubs = [torch.zeros(1 << 30, dtype=torch.uint8, device=torch.device("cuda", d)) for d in range(N)]
+
+    def sync_all():
+        for d in range(N):
+            torch.cuda.synchronize(d)
+
+    def evict():
+        for sc in scrubs:
+            if args.scrub == "write":
+                sc.add_(1)
+            else:
+                sc.sum(dtype=torch.int64)
+        sync_all()
+
+    def cold():
+        rows = []
+        for _ in range(args.steps):
+            evict()
+            rows.append(ctx.spmv_ex(ALPHA, BETA, delay_us=delay_us, wait=True))
+        return np.array(rows)
+
+    def warm():
+        sync_all()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.spmv_ex(ALPHA, BETA, wait=False)
+        last = ctx.sync()
+        sync_all()
+        return time.perf_counter() - t, last
+
+    if args.cache == "cold":
+        st = cold()
+        warm_el, warm_last = warm()
+    else:
+        warm_el, warm_last = warm()
+        st = cold()
+    del scrubs
+    # st[:, 0..2] = max over devices of kernel / exchange / step (ms); then
+    # per device d: st[:, 3+3d .. 5+3d]
+    step_ms = float(np.mean(st[:, 2]))
+    kern_max = float(np.mean(st[:, 0]))
+    xch_max = float(np.mean(st[:, 1]))
+    dev_kern = [float(np.mean(st[:, 3 + 3 * d])) for d in range(N)]
+    check = None
+    if args.check:
+        y0 = np.zeros(n)
+        ctx.set_y(y0)
+        ctx.spmv_ex(ALPHA, BETA)
+        ys = [ctx.get_y(d) for d in range(N)]
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import orc  # oracle: checker only
+        want = orc.csr_spmv(rowptr, col, val, x_h, ALPHA, BETA, y0)
+        bound = orc.spmv_bound(rowptr, col, val, x_h, ALPHA, BETA, y0)
+        check = bool(np.all(np.abs(ys[0] - want) <= bound)) and \
+            all(np.array_equal(ys[0], y) for y in ys[1:])
+    total_flops = 2.0 * nnz
+    achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
+    agg = sum(dev_bytes) / (kern_max * 1e-3) / 1e9
+    profiled = N == 1 and args.cols == "random" and n == 2_000_000 and \
+        (args.heavy, args.light) == (96, 9)
+    out = {
+        "metric": METRIC,
+        "value": round(total_flops / (step_ms * 1e-3) / 1e9, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 5),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic generator, DESIGN.md)",
+        "config": {
+            "workload": (f"synthetic non-uniform n={n} CSR fp64 SpMV, rows<n/8: {args.heavy} "
+                         f"nnz else {args.light}, {args.cols} sorted cols (seed 42), "
+                         f"y=alpha*A*x+beta*y, {args.algo} kernel"),
+            "n": n, "nnz": nnz, "algo": args.algo,
+            "partition": ("cyclic row chunks" if partition == 0 else "nnz-balanced (spMV_mgpu_v1)"),
+            "exchange": args.exchange if exchange == sblas.CTX_ALLREDUCE else "allgather",
+            "driver": "ctx (one process, sblas_ctx over RCCL, ncclCommInitAll)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved0, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved0 / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic(args.algo) if profiled else None,
+            "aggregate_GBps": round(agg, 1),
+            "aggregate_frac": round(agg / (HBM_PEAK_GBS * N), 4),
+        },
+        "kernel_ms": round(dev_kern[0], 5),
+        "kernel_ms_max_over_ranks": round(kern_max, 5),
+        "kernel_ms_per_device": [round(k, 5) for k in dev_kern],
+        "kernel_only_gflops": round(total_flops / (kern_max * 1e-3) / 1e9, 3),
+        "algorithmic_bytes_per_launch": int(dev_bytes[0]),
+        "algorithmic_bytes_all_ranks": int(sum(dev_bytes)),
+        "nnz_per_device": [int(z) for _, z, _ in info],
+        "host_gen_s": round(t_gen, 2),
+        "plan": {"upload_and_build_s": round(plan_s, 3)},
+        "exchange_ms_max_over_ranks": round(xch_max, 5),
+        "timing": ("cold steps: per-device span (start event .. end of exchange) after a device-side "
+                   "hold and a one-word all-reduce that align the devices (sblas_ctx_spmv_ex), max "
+                   "over devices" if args.cache == "cold"
+                   else "warm: host wall clock over K back-to-back steps"),
+        "cache": args.cache,
+        "scrub": args.scrub,
+        ("warm" if args.cache == "cold" else "cold"): (
+            {"value": round(total_flops / (warm_el / args.steps) / 1e9, 3),
+             "ms_per_step": round(warm_el / args.steps * 1e3, 5),
+             "last_step_kernel_ms_max": round(float(warm_last[0]), 5)}
+            if args.cache == "cold" else
+            {"value": round(total_flops / (step_ms * 1e-3) / 1e9, 3), "ms_per_step": round(step_ms, 5)}),
+    }
+    if args.cache == "warm":
+        out["value"] = round(total_flops / (warm_el / args.steps) / 1e9, 3)
+        out["ms_per_step"] = round(warm_el / args.steps * 1e3, 5)
+    if check is not None:
+        out["check_vs_oracle"] = check
+    if N == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(rowptr, col, val, x_h, n, nnz, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    return 0
 
 
 def main() -> int:
@@ -161,19 +380,29 @@ def main() -> int:
                     help="join a process group even at WORLD_SIZE 1 (torchrun --nproc-per-node 1): "
                          "runs the N > 1 exchange and timing path, RCCL included, on one GPU")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--driver", choices=["auto", "ctx", "torch"], default="auto",
+                    help="auto: torch.distributed ranks under a launcher, else one process over "
+                         "sblas_ctx for --gpus > 1 (the persistent single-GPU path at N = 1); "
+                         "ctx: force the C-ABI context (also at N = 1)")
     args = ap.parse_args()
 
     import torch
+
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    try:
+        driver = choose_driver(args.gpus, os.environ, ndev, args.driver)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        return 2
+    if driver == "ctx":
+        return run_ctx(args)
+
     import sblas
     import sblas_dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
-              file=sys.stderr)
-    ndev = torch.cuda.device_count()
     dev_idx = local_rank % max(ndev, 1)
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)

@@ -263,10 +263,20 @@ int sblas_assemble_cyclic(const double *d_gathered, int g, long long stride,
 /* 3. Multi-GPU context (single process, RCCL over xGMI).  Replaces the
  *    reference's host-driven multi-GPU SpMV (spmv/src/dspmv_mgpu_v1.cu:16-280)
  *    for callers that keep the matrix: the slices stay resident per device,
- *    x is replicated with ncclBroadcast, the y slices are exchanged with ONE
- *    ncclAllGather and placed on the device, so every device holds the full
- *    y.  Devices must be distinct (no wrapping: one RCCL rank per GPU). */
+ *    x is replicated with ncclBroadcast, and the y slices are exchanged on the
+ *    devices (one ncclAllGather + placement, or the literal ncclAllReduce of
+ *    the zero-padded y of BASELINE configs[2]), so every device holds the full
+ *    y.  Devices must be distinct (no wrapping: one RCCL rank per GPU).
+ *    Hardware status: on the 1-GPU pool this runs with g = 1 only; g > 1
+ *    (ncclCommInitAll over distinct devices, split-row carries, cyclic
+ *    placement across devices) is covered by CPU tests of the partition and
+ *    placement logic and is unverified on multi-GPU hardware. */
 typedef struct sblas_ctx_s *sblas_ctx;
+typedef enum {
+    SBLAS_CTX_ALLGATHER = 0, /* equal padded slices all-gathered, placed on device */
+    SBLAS_CTX_ALLREDUCE = 1  /* zero-padded full y summed (nnz partition only;
+                                dspmv_mgpu_v1.cu:235-248's merge as a collective) */
+} sblas_ctx_exchange;
 /* ncclCommInitAll over devlist[0..ngpu) (NULL: 0..ngpu-1). */
 int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist);
 int sblas_ctx_destroy(sblas_ctx ctx);
@@ -274,20 +284,45 @@ int sblas_ctx_ngpu(sblas_ctx ctx, int *ngpu);
 /* HOST CSR (int64 rowptr) distributed over the devices and analysed for
  * `algo` (sblas_spmv_algo).  partition 0 = cyclic row chunks (chunk j of
  * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
- * nnz-balanced split with split rows merged on the device. */
+ * nnz-balanced split with split rows merged on the device.  Exchange
+ * SBLAS_CTX_ALLGATHER. */
 int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr,
                             const int *col, const double *val, int algo, int partition);
+/* Same with the exchange chosen (sblas_ctx_exchange); SBLAS_CTX_ALLREDUCE
+ * needs partition 1 (SBLAS_ERR_INVALID otherwise). */
+int sblas_ctx_matrix_upload_ex(sblas_ctx ctx, int m, int n, const long long *rowptr,
+                               const int *col, const double *val, int algo, int partition,
+                               int exchange);
+/* Device d's share: rows, entries, and the algorithmic bytes of its SpMV
+ * launch with beta != 0 (sblas_spmv_algorithmic_bytes).  Any may be NULL. */
+int sblas_ctx_slice_info(sblas_ctx ctx, int d, long long *rows, long long *nnz,
+                         long long *alg_bytes_beta);
 int sblas_ctx_set_x(sblas_ctx ctx, const double *x); /* host x -> every device */
 int sblas_ctx_set_y(sblas_ctx ctx, const double *y); /* host y (beta input) */
 /* y = alpha*A*x + beta*y on every device; afterwards each device holds the
  * full y, which is also the next call's y input.  stats (optional, 3
- * doubles, ms, max over devices): kernel, exchange (all-gather + placement),
+ * doubles, ms, max over devices): kernel, exchange (collective + placement),
  * whole step. */
 int sblas_ctx_spmv(sblas_ctx ctx, double alpha, double beta, double *stats);
+/* sblas_ctx_spmv for timing.  delay_us > 0: every device's stream first
+ * waits delay_us on the device (the host enqueues the whole step meanwhile)
+ * and then joins a one-word all-reduce that lines the devices up; each
+ * device's span then runs from its start event to the end of its exchange,
+ * without the host's launch latency.  wait = 0 returns once the step is
+ * enqueued (sblas_ctx_sync waits).  stats (3 + 3g doubles, ms): max over
+ * devices of kernel / exchange / step, then kernel / exchange / step of
+ * device 0, 1, ... */
+int sblas_ctx_spmv_ex(sblas_ctx ctx, double alpha, double beta, double delay_us, int wait,
+                      double *stats);
+/* Waits for the last step and returns its stats (3 + 3g doubles, as above). */
+int sblas_ctx_sync(sblas_ctx ctx, double *stats);
 int sblas_ctx_get_y(sblas_ctx ctx, int device_index, double *y); /* -> host */
 /* Bind (or unbind with NULL) a context for the reference API: while bound,
  * sblas_spMV_mgpu_v1 / spMV_mgpu_v1 with ngpu == the context's size run on
- * it (RCCL exchange) instead of the host merge. */
+ * it (RCCL exchange) instead of the host merge.  Binding LENDS the context:
+ * each such call uploads and analyses its matrix into the context (nnz
+ * partition, all-gather), replacing whatever matrix the caller had resident
+ * there, and that matrix stays allocated after the call. */
 int sblas_ctx_bind(sblas_ctx ctx);
 /* The cyclic distribution's plan: chunk_rows = ceil(m/(g*chunks_per_rank)),
  * stride = rows of one device's padded slice.  No GPU needed. */

@@ -173,6 +173,8 @@ int sblas_csr_destroy(sblas_csr A)
     {
         DeviceGuard g(A->device);
         free_plans(*A);
+        (void)hipFree(A->spmm_bt);
+        (void)hipFree(A->spmm_part);
         (void)hipFree(A->rowptr);
         (void)hipFree(A->col);
         (void)hipFree(A->val);

@@ -33,13 +33,19 @@ struct sblas_ctx_s {
     std::vector<hipEvent_t> ev;  // [g][3]: start, after kernel, after exchange + placement
     // the matrix (absent until sblas_ctx_matrix_upload)
     bool loaded = false;
-    int m = 0, n = 0, algo = 0, partition = 0;
+    int m = 0, n = 0, algo = 0, partition = 0, exchange = 0;
     long long nnz = 0, stride = 0, chunk_rows = 0;
+    long long ylen = 0;                // doubles in each ylocal buffer
     std::vector<sblas_csr> A;
     std::vector<double *> x, ylocal, gathered, yfull;
     std::vector<int *> meta;           // nnz partition: {row0, nrows, cont} per partition
     std::vector<int> h_meta;
+    std::vector<double *> bar;         // one word per device: the timing protocol's aligning all-reduce
     std::vector<long long> lrows;      // rows per device
+    std::vector<long long> lnnz;       // entries per device
+    std::vector<long long> yoff;       // the kernel's y = ylocal[d] + yoff[d]
+    std::vector<double> last;          // stats of the last sblas_ctx_spmv_ex (3 + 3g)
+    bool pending = false;              // a step was issued without waiting (wait = 0)
 };
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
@@ -65,6 +71,40 @@ using namespace sblas;
         }                                                                       \
     } while (0)
 
+// Inside ncclGroupStart/End: on failure close the group before returning, so
+// the calling thread's later collectives are not queued into a group that
+// never runs.
+#define SBLAS_NCCL_G(expr)                                                      \
+    do {                                                                        \
+        ncclResult_t r_ = (expr);                                               \
+        if (r_ != ncclSuccess) {                                                \
+            (void)ncclGroupEnd();                                               \
+            ::sblas::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,     \
+                               ncclGetErrorString(r_));                         \
+            return SBLAS_ERR_RCCL;                                              \
+        }                                                                       \
+    } while (0)
+
+// Timing aid of sblas_ctx_spmv_ex: hold the stream for `ticks` of the 100-MHz
+// constant clock, so that the host can enqueue every device's step before any
+// device starts it (the host's launch latency then stays out of the spans).
+__global__ void k_ctx_delay(unsigned long long ticks)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// allreduce exchange: after the sum, the device's own rows of the full y
+// become its next input (a continuation row restarts from 0: the previous
+// partition adds beta*y for it).
+__global__ void k_ctx_reprime(const double *__restrict__ yfull, double *__restrict__ ysend, long long nr,
+                              int cont)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nr) return;
+    ysend[i] = (i == 0 && cont) ? 0.0 : yfull[i];
+}
+
 void free_matrix(sblas_ctx_s &C)
 {
     for (int d = 0; d < (int)C.A.size(); ++d) {
@@ -75,6 +115,7 @@ void free_matrix(sblas_ctx_s &C)
         (void)hipFree(C.gathered[d]);
         (void)hipFree(C.yfull[d]);
         (void)hipFree(C.meta[d]);
+        (void)hipFree(C.bar[d]);
     }
     C.A.clear();
     C.x.clear();
@@ -82,8 +123,13 @@ void free_matrix(sblas_ctx_s &C)
     C.gathered.clear();
     C.yfull.clear();
     C.meta.clear();
+    C.bar.clear();
     C.h_meta.clear();
     C.lrows.clear();
+    C.lnnz.clear();
+    C.yoff.clear();
+    C.last.clear();
+    C.pending = false;
     C.loaded = false;
 }
 
@@ -198,11 +244,17 @@ int sblas_ctx_ngpu(sblas_ctx C, int *ngpu)
     return SBLAS_OK;
 }
 
-int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
-                            const double *val, int algo, int partition)
+int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
+                               const double *val, int algo, int partition, int exchange)
 {
     if (!C || m < 0 || n < 0 || !rowptr || (partition != 0 && partition != 1)) return SBLAS_ERR_INVALID;
     if (algo < SBLAS_SPMV_ROWSPLIT || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
+    if (exchange != SBLAS_CTX_ALLGATHER && exchange != SBLAS_CTX_ALLREDUCE) return SBLAS_ERR_INVALID;
+    if (exchange == SBLAS_CTX_ALLREDUCE && partition != 1) {
+        set_error("sblas_ctx_matrix_upload: the allreduce exchange needs the nnz partition (1): each "
+                  "device's rows must be one contiguous range of the zero-padded y");
+        return SBLAS_ERR_INVALID;
+    }
     free_matrix(*C);
     const int g = C->g;
     C->m = m;
@@ -210,13 +262,17 @@ int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, 
     C->nnz = rowptr[m];
     C->algo = algo;
     C->partition = partition;
+    C->exchange = exchange;
     C->A.assign(g, nullptr);
     C->x.assign(g, nullptr);
     C->ylocal.assign(g, nullptr);
     C->gathered.assign(g, nullptr);
     C->yfull.assign(g, nullptr);
     C->meta.assign(g, nullptr);
+    C->bar.assign(g, nullptr);
     C->lrows.assign(g, 0);
+    C->lnnz.assign(g, 0);
+    C->yoff.assign(g, 0);
     std::vector<long long> si(g), ei(g);
     std::vector<int> sr(g), er(g), sf(g);
     if (partition == 0) {
@@ -235,6 +291,9 @@ int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, 
         }
         C->stride = mx;
     }
+    // allgather: each device's padded slice of `stride` rows; allreduce: a
+    // zero-padded full-length y whose own rows the kernel writes in place
+    C->ylen = exchange == SBLAS_CTX_ALLREDUCE ? std::max(m, 1) : C->stride;
     int st = SBLAS_OK;
     for (int d = 0; d < g && st == SBLAS_OK; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -248,10 +307,13 @@ int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, 
             SBLAS_TRY(sblas_cyclic_local_csr(m, rowptr, col, val, g, C->chunk_rows, d, &lm, &lz,
                                              lrp.data(), lcol.data(), lval.data()));
             C->lrows[d] = lm;
+            C->lnnz[d] = lz;
             st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, lrp.data(), lcol.data(), lval.data(), 0,
                                         (int)lm, 0, lz, C->st[d]);
         } else {
             C->lrows[d] = std::max(0, er[d] - sr[d] + 1);
+            C->lnnz[d] = C->lrows[d] > 0 ? ei[d] + 1 - si[d] : 0;
+            if (exchange == SBLAS_CTX_ALLREDUCE) C->yoff[d] = sr[d];
             st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, rowptr, col, val, sr[d], er[d] + 1,
                                         si[d], ei[d] + 1, C->st[d]);
         }
@@ -259,10 +321,13 @@ int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, 
         st = sblas_csr_analyse(C->A[d], algo, C->st[d]);
         if (st != SBLAS_OK) break;
         hipError_t e = hipMalloc(&C->x[d], sizeof(double) * std::max(n, 1));
-        if (e == hipSuccess) e = hipMalloc(&C->ylocal[d], sizeof(double) * C->stride);
-        if (e == hipSuccess) e = hipMalloc(&C->gathered[d], sizeof(double) * C->stride * g);
+        if (e == hipSuccess) e = hipMalloc(&C->ylocal[d], sizeof(double) * C->ylen);
+        if (e == hipSuccess && exchange == SBLAS_CTX_ALLGATHER)
+            e = hipMalloc(&C->gathered[d], sizeof(double) * C->stride * g);
         if (e == hipSuccess) e = hipMalloc(&C->yfull[d], sizeof(double) * std::max(m, 1));
-        if (e == hipSuccess) e = hipMemsetAsync(C->ylocal[d], 0, sizeof(double) * C->stride, C->st[d]);
+        if (e == hipSuccess) e = hipMalloc(&C->bar[d], sizeof(double));
+        if (e == hipSuccess) e = hipMemsetAsync(C->bar[d], 0, sizeof(double), C->st[d]);
+        if (e == hipSuccess) e = hipMemsetAsync(C->ylocal[d], 0, sizeof(double) * C->ylen, C->st[d]);
         if (e == hipSuccess && partition == 1) {
             e = hipMalloc(&C->meta[d], sizeof(int) * 3 * g);
             if (e == hipSuccess)
@@ -279,7 +344,23 @@ int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, 
         free_matrix(*C);
         return st;
     }
+    C->last.assign((size_t)3 + 3 * g, 0.0);
     C->loaded = true;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_matrix_upload(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
+                            const double *val, int algo, int partition)
+{
+    return sblas_ctx_matrix_upload_ex(C, m, n, rowptr, col, val, algo, partition, SBLAS_CTX_ALLGATHER);
+}
+
+int sblas_ctx_slice_info(sblas_ctx C, int d, long long *rows, long long *nnz, long long *alg_bytes_beta)
+{
+    if (!C || !C->loaded || d < 0 || d >= C->g) return SBLAS_ERR_INVALID;
+    if (rows) *rows = C->lrows[d];
+    if (nnz) *nnz = C->lnnz[d];
+    if (alg_bytes_beta) *alg_bytes_beta = sblas_spmv_algorithmic_bytes(C->A[d], 1);
     return SBLAS_OK;
 }
 
@@ -295,7 +376,7 @@ int sblas_ctx_set_x(sblas_ctx C, const double *x)
     SBLAS_NCCL(ncclGroupStart());
     for (int d = 0; d < C->g; ++d) {
         DeviceGuard g(C->dev[d]);
-        SBLAS_NCCL(ncclBroadcast(C->x[d], C->x[d], (size_t)C->n, ncclDouble, 0, C->comm[d], C->st[d]));
+        SBLAS_NCCL_G(ncclBroadcast(C->x[d], C->x[d], (size_t)C->n, ncclDouble, 0, C->comm[d], C->st[d]));
     }
     SBLAS_NCCL(ncclGroupEnd());
     for (int d = 0; d < C->g; ++d) {
@@ -308,7 +389,7 @@ int sblas_ctx_set_x(sblas_ctx C, const double *x)
 int sblas_ctx_set_y(sblas_ctx C, const double *y)
 {
     if (!C || !C->loaded || !y) return SBLAS_ERR_INVALID;
-    std::vector<double> h((size_t)C->stride);
+    std::vector<double> h((size_t)C->ylen);
     for (int d = 0; d < C->g; ++d) {
         std::fill(h.begin(), h.end(), 0.0);
         long long o = 0;
@@ -321,46 +402,23 @@ int sblas_ctx_set_y(sblas_ctx C, const double *y)
             }
         } else {
             const int r0 = C->h_meta[(size_t)3 * d], nr = C->h_meta[(size_t)3 * d + 1];
-            if (nr > 0) std::memcpy(h.data(), y + r0, sizeof(double) * nr);
-            if (nr > 0 && C->h_meta[(size_t)3 * d + 2]) h[0] = 0.0;  // continuation: partial only
+            double *dst = h.data() + C->yoff[d];
+            if (nr > 0) std::memcpy(dst, y + r0, sizeof(double) * nr);
+            if (nr > 0 && C->h_meta[(size_t)3 * d + 2]) dst[0] = 0.0;  // continuation: partial only
         }
         DeviceGuard g(C->dev[d]);
-        SBLAS_HIP(hipMemcpyAsync(C->ylocal[d], h.data(), sizeof(double) * C->stride, hipMemcpyHostToDevice,
+        SBLAS_HIP(hipMemcpyAsync(C->ylocal[d], h.data(), sizeof(double) * C->ylen, hipMemcpyHostToDevice,
                                  C->st[d]));
         SBLAS_HIP(hipStreamSynchronize(C->st[d]));
     }
     return SBLAS_OK;
 }
 
-int sblas_ctx_spmv(sblas_ctx C, double alpha, double beta, double *stats)
+// Waits for the step issued last and fills C->last (3 + 3g doubles, ms):
+// max over devices of kernel / exchange / step, then per device the same.
+static int ctx_collect(sblas_ctx_s *C)
 {
-    if (!C || !C->loaded) return SBLAS_ERR_INVALID;
     const int g = C->g;
-    for (int d = 0; d < g; ++d) {
-        DeviceGuard gd(C->dev[d]);
-        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d], C->st[d]));
-        if (C->lrows[d] > 0)
-            SBLAS_TRY(sblas_spmv(C->A[d], C->algo, alpha, C->x[d], beta, C->ylocal[d], C->st[d]));
-        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 1], C->st[d]));
-    }
-    // the exchange: one all-gather of equal padded slices over xGMI
-    SBLAS_NCCL(ncclGroupStart());
-    for (int d = 0; d < g; ++d) {
-        DeviceGuard gd(C->dev[d]);
-        SBLAS_NCCL(ncclAllGather(C->ylocal[d], C->gathered[d], (size_t)C->stride, ncclDouble, C->comm[d],
-                                 C->st[d]));
-    }
-    SBLAS_NCCL(ncclGroupEnd());
-    for (int d = 0; d < g; ++d) {
-        DeviceGuard gd(C->dev[d]);
-        if (C->partition == 0)
-            SBLAS_TRY(sblas_assemble_cyclic(C->gathered[d], g, C->stride, C->chunk_rows, C->m, C->yfull[d],
-                                            C->st[d]));
-        else  // also re-primes this device's slice as the next call's y input
-            SBLAS_TRY(sblas_assemble_slices(C->gathered[d], g, C->stride, C->meta[d], C->yfull[d], d,
-                                            C->ylocal[d], C->st[d]));
-        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 2], C->st[d]));
-    }
     double kmax = 0.0, xmax = 0.0, tmax = 0.0;
     for (int d = 0; d < g; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -368,15 +426,101 @@ int sblas_ctx_spmv(sblas_ctx C, double alpha, double beta, double *stats)
         float k = 0.f, t = 0.f;
         SBLAS_HIP(hipEventElapsedTime(&k, C->ev[(size_t)3 * d], C->ev[(size_t)3 * d + 1]));
         SBLAS_HIP(hipEventElapsedTime(&t, C->ev[(size_t)3 * d], C->ev[(size_t)3 * d + 2]));
+        C->last[(size_t)3 + 3 * d] = k;
+        C->last[(size_t)4 + 3 * d] = (double)t - k;
+        C->last[(size_t)5 + 3 * d] = t;
         kmax = std::max(kmax, (double)k);
         xmax = std::max(xmax, (double)(t - k));
         tmax = std::max(tmax, (double)t);
     }
-    if (stats) {
-        stats[0] = kmax;  // kernel, max over devices (ms)
-        stats[1] = xmax;  // all-gather + placement, max over devices
-        stats[2] = tmax;  // whole step, max over devices
+    C->last[0] = kmax;
+    C->last[1] = xmax;
+    C->last[2] = tmax;
+    C->pending = false;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_spmv_ex(sblas_ctx C, double alpha, double beta, double delay_us, int wait, double *stats)
+{
+    if (!C || !C->loaded || delay_us < 0.0 || delay_us > 1e5) return SBLAS_ERR_INVALID;
+    const int g = C->g;
+    if (delay_us > 0.0) {
+        // timing protocol: every stream waits on the device while the host
+        // enqueues the whole step, then a one-element all-reduce lines the
+        // devices up, so each device's span (start event .. after the
+        // exchange) starts together with the others'
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C->dev[d]);
+            hipLaunchKernelGGL(k_ctx_delay, dim3(1), dim3(1), 0, C->st[d],
+                               (unsigned long long)(delay_us * 100.0));
+            SBLAS_HIP(hipGetLastError());
+        }
+        SBLAS_NCCL(ncclGroupStart());
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C->dev[d]);
+            SBLAS_NCCL_G(ncclAllReduce(C->bar[d], C->bar[d], 1, ncclDouble, ncclSum, C->comm[d],
+                                       C->st[d]));
+        }
+        SBLAS_NCCL(ncclGroupEnd());
     }
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d], C->st[d]));
+        if (C->lrows[d] > 0)
+            SBLAS_TRY(sblas_spmv(C->A[d], C->algo, alpha, C->x[d], beta, C->ylocal[d] + C->yoff[d],
+                                 C->st[d]));
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 1], C->st[d]));
+    }
+    SBLAS_NCCL(ncclGroupStart());
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        if (C->exchange == SBLAS_CTX_ALLGATHER)  // one all-gather of equal padded slices over xGMI
+            SBLAS_NCCL_G(ncclAllGather(C->ylocal[d], C->gathered[d], (size_t)C->stride, ncclDouble,
+                                       C->comm[d], C->st[d]));
+        else  // BASELINE configs[2]: the literal all-reduce of the zero-padded y
+            SBLAS_NCCL_G(ncclAllReduce(C->ylocal[d], C->yfull[d], (size_t)C->m, ncclDouble, ncclSum,
+                                       C->comm[d], C->st[d]));
+    }
+    SBLAS_NCCL(ncclGroupEnd());
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C->dev[d]);
+        if (C->exchange == SBLAS_CTX_ALLREDUCE) {
+            const long long nr = C->lrows[d];
+            if (nr > 0) {
+                hipLaunchKernelGGL(k_ctx_reprime, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, C->st[d],
+                                   C->yfull[d] + C->yoff[d], C->ylocal[d] + C->yoff[d], nr,
+                                   C->h_meta[(size_t)3 * d + 2]);
+                SBLAS_HIP(hipGetLastError());
+            }
+        } else if (C->partition == 0) {
+            SBLAS_TRY(sblas_assemble_cyclic(C->gathered[d], g, C->stride, C->chunk_rows, C->m, C->yfull[d],
+                                            C->st[d]));
+        } else {  // also re-primes this device's slice as the next call's y input
+            SBLAS_TRY(sblas_assemble_slices(C->gathered[d], g, C->stride, C->meta[d], C->yfull[d], d,
+                                            C->ylocal[d], C->st[d]));
+        }
+        SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 2], C->st[d]));
+    }
+    C->pending = true;
+    if (!wait) return SBLAS_OK;
+    SBLAS_TRY(ctx_collect(C));
+    if (stats) std::copy(C->last.begin(), C->last.end(), stats);
+    return SBLAS_OK;
+}
+
+int sblas_ctx_sync(sblas_ctx C, double *stats)
+{
+    if (!C || !C->loaded) return SBLAS_ERR_INVALID;
+    if (C->pending) SBLAS_TRY(ctx_collect(C));
+    if (stats) std::copy(C->last.begin(), C->last.end(), stats);
+    return SBLAS_OK;
+}
+
+int sblas_ctx_spmv(sblas_ctx C, double alpha, double beta, double *stats)
+{
+    if (!C || !C->loaded) return SBLAS_ERR_INVALID;
+    SBLAS_TRY(sblas_ctx_spmv_ex(C, alpha, beta, 0.0, 1, nullptr));
+    if (stats) std::copy(C->last.begin(), C->last.begin() + 3, stats);
     return SBLAS_OK;
 }
 

@@ -262,6 +262,13 @@ struct sblas_csr_s {
     sblas::SpmmPlan mm;
     sblas::XsPlan xs;
     std::vector<int> h_rowptr;  // host copy (analysis)
+    // SpMM per-call scratch, owned by the handle so that distinct handles
+    // never share it (row-major copy of a column-major B; C-tile partials).
+    // Grown on demand; one SpMM per handle in flight (as for sblas_spmv).
+    mutable double *spmm_bt = nullptr;
+    mutable size_t spmm_bt_bytes = 0;
+    mutable double *spmm_part = nullptr;
+    mutable size_t spmm_part_bytes = 0;
     long long plan_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device bytes per algorithm's plan
 };
 

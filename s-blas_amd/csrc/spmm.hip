@@ -1018,12 +1018,17 @@ __global__ void k_transpose_B(const double *__restrict__ B, long long ldb, int k
     }
 }
 
-struct SpmmScratch {
-    double *bt = nullptr;
-    size_t bytes = 0;
-};
-static thread_local SpmmScratch g_scratch[64];
-static thread_local SpmmScratch g_ctpart[64];  // C-tile partials per device
+// grow a handle-owned scratch buffer (sblas_csr_s::spmm_*)
+static int grow_scratch(double *&buf, size_t &bytes, size_t need)
+{
+    if (bytes >= need) return SBLAS_OK;
+    (void)hipFree(buf);
+    buf = nullptr;
+    bytes = 0;
+    SBLAS_HIP(hipMalloc(&buf, need));
+    bytes = need;
+    return SBLAS_OK;
+}
 
 int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int ldb,
                 int b_layout, double beta, double *C, int ldc, hipStream_t s)
@@ -1032,20 +1037,12 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     const double *Brow = B;
     long long ldr = ldb;
     if (b_layout == 0) {
-        SpmmScratch &S = g_scratch[A.device & 63];
-        const size_t need = sizeof(double) * (size_t)A.n * (size_t)n;
-        if (S.bytes < need) {
-            (void)hipFree(S.bt);
-            S.bt = nullptr;
-            S.bytes = 0;
-            SBLAS_HIP(hipMalloc(&S.bt, need));
-            S.bytes = need;
-        }
+        SBLAS_TRY(grow_scratch(A.spmm_bt, A.spmm_bt_bytes, sizeof(double) * (size_t)A.n * (size_t)n));
         if (A.n > 0) {
             dim3 grid((A.n + 63) / 64, (n + 63) / 64);
-            hipLaunchKernelGGL(k_transpose_B, grid, dim3(256), 0, s, B, (long long)ldb, A.n, n, S.bt);
+            hipLaunchKernelGGL(k_transpose_B, grid, dim3(256), 0, s, B, (long long)ldb, A.n, n, A.spmm_bt);
         }
-        Brow = S.bt;
+        Brow = A.spmm_bt;
         ldr = n;
     }
     const SpmmPlan &P = A.mm;
@@ -1053,15 +1050,9 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     if (P.ready && P.ct_nrb > 0) {
         const int ncg = (n + kCtCols - 1) / kCtCols;
         const int nslot = 8 * P.ct_ns;
-        SpmmScratch &S = g_ctpart[A.device & 63];
-        const size_t need = sizeof(double) * (size_t)nslot * (size_t)n * (size_t)A.m;
-        if (S.bytes < need) {
-            (void)hipFree(S.bt);
-            S.bt = nullptr;
-            S.bytes = 0;
-            SBLAS_HIP(hipMalloc(&S.bt, need));
-            S.bytes = need;
-        }
+        SBLAS_TRY(grow_scratch(A.spmm_part, A.spmm_part_bytes,
+                               sizeof(double) * (size_t)nslot * (size_t)n * (size_t)A.m));
+        double *const part = A.spmm_part;
         const long long nwg = 8LL * P.ct_ns * P.ct_nrb * ncg;
         const size_t lds = sizeof(double) * (size_t)P.ct_R * kCtPad;
         static thread_local bool attr_set[64] = {};
@@ -1089,7 +1080,7 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
             const size_t lds_o = sizeof(double) * (size_t)(P.ct_R + kCoWaves) * kCoPad;
             hipLaunchKernelGGL(fast ? k_spmm_ctown<true> : k_spmm_ctown<false>, dim3((unsigned)nwg),
                                dim3(kCtThreads), lds_o, s, P.ct_key, P.ct_val, P.ct_woff, P.ct_ns, P.ct_nrb,
-                               P.ct_R, P.ct_rbits, ncg, Brow, ldr, n, A.m, S.bt);
+                               P.ct_R, P.ct_rbits, ncg, Brow, ldr, n, A.m, part);
         } else {
         using K = void (*)(const unsigned *, const double *, const unsigned *, const double *, const long long *,
                            int, int, int, int, int, int, const double *, long long, int, int, double *);
@@ -1102,14 +1093,14 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
                                : (fast ? k_spmm_ctile<false, true, false> : k_spmm_ctile<false, false, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_key2,
                            P.ct_val2, P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr,
-                           n, A.m, S.bt);
+                           n, A.m, part);
         }
         const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
         if (beta != 0.0)
-            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,
+            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
                                beta, C, (long long)ldc);
         else
-            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, S.bt, nslot, A.m, n, alpha,
+            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
                                beta, C, (long long)ldc);
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;

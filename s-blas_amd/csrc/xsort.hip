@@ -1242,9 +1242,11 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.vstride = P.vstride;
     a.qitems = P.qitems;
     a.xrec = P.xrec;
+    // parity and epoch advance only once the launch is known to be queued: a
+    // launch that failed never re-armed the other parity's heads, so the
+    // next launch must reuse this parity's (still armed) heads
     a.qhead = P.qhead + 16 * P.parity;        // this launch's claim heads
     a.qreset = P.qhead + 16 * (1 - P.parity);  // re-armed for the next launch
-    P.parity ^= 1;
     a.partial = P.partial;
     for (int k = 0; k < 8; ++k) {
         a.qlen[k] = P.qlen[k];
@@ -1255,8 +1257,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.rtasks = P.rtasks;
     a.nrtasks = P.nrtasks;
     a.arrive = P.arrive;
-    if (P.fused) ++P.epoch;
-    a.epoch = (unsigned)P.epoch;
+    a.epoch = (unsigned)(P.epoch + (P.fused ? 1 : 0));
     a.qstride = P.qstride;
     a.G = P.G;
     a.q = P.q;
@@ -1332,6 +1333,9 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         htrace.resize(len);
     }
     SBLAS_LAUNCH(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
+    SBLAS_HIP(hipGetLastError());
+    P.parity ^= 1;
+    if (P.fused) ++P.epoch;
     if (trace_path) {  // debugging aid: rows {subA, subB, block<<4|xcc, t0, endA, endB}
         SBLAS_HIP(hipMemcpyAsync(htrace.data(), a.trace, sizeof(long long) * htrace.size(),
                                  hipMemcpyDeviceToHost, s));

@@ -110,6 +110,10 @@ _sig("sblas_ctx_matrix_upload", _i, _p, _i, _i, _p, _p, _p, _i, _i)
 _sig("sblas_ctx_set_x", _i, _p, _p)
 _sig("sblas_ctx_set_y", _i, _p, _p)
 _sig("sblas_ctx_spmv", _i, _p, _d, _d, _p)
+_sig("sblas_ctx_matrix_upload_ex", _i, _p, _i, _i, _p, _p, _p, _i, _i, _i)
+_sig("sblas_ctx_slice_info", _i, _p, _i, _p, _p, _p)
+_sig("sblas_ctx_spmv_ex", _i, _p, _d, _d, _d, _i, _p)
+_sig("sblas_ctx_sync", _i, _p, _p)
 _sig("sblas_ctx_get_y", _i, _p, _i, _p)
 _sig("sblas_ctx_bind", _i, _p)
 _sig("sblas_cyclic_plan", _i, _ll, _i, _i, _p, _p)
@@ -425,9 +429,14 @@ class DeviceCSR:
             pass
 
 
+CTX_ALLGATHER = 0  # sblas_ctx_exchange
+CTX_ALLREDUCE = 1
+
+
 class DeviceCtx:
     """Single-process multi-GPU SpMV context (sblas_ctx: RCCL communicator
-    over `ngpu` distinct devices, resident slices, ncclAllGather exchange)."""
+    over `ngpu` distinct devices, resident slices, ncclAllGather or
+    ncclAllReduce exchange)."""
 
     def __init__(self, ngpu: int, devices=None):
         self.h = C.c_void_p()
@@ -436,13 +445,32 @@ class DeviceCtx:
         self.ngpu = ngpu
         self.m = 0
 
-    def upload(self, m: int, n: int, rowptr, col, val, algo: int, partition: int = 0) -> None:
-        self._keep = (np.ascontiguousarray(rowptr, np.int64), np.ascontiguousarray(col, np.int32),
-                      np.ascontiguousarray(val, np.float64))
-        rp, ci, v = self._keep
-        check(lib.sblas_ctx_matrix_upload(self.h, m, n, ptr(rp), ptr(ci), ptr(v), algo, partition),
-              "ctx_matrix_upload")
+    def upload(self, m: int, n: int, rowptr, col, val, algo: int, partition: int = 0,
+               exchange: int = CTX_ALLGATHER) -> None:
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        ci = np.ascontiguousarray(col, np.int32)
+        v = np.ascontiguousarray(val, np.float64)
+        check(lib.sblas_ctx_matrix_upload_ex(self.h, m, n, ptr(rp), ptr(ci), ptr(v), algo, partition,
+                                             exchange), "ctx_matrix_upload")
         self.m = m
+
+    def slice_info(self, d: int):
+        """(rows, nnz, algorithmic bytes with beta != 0) of device d's share."""
+        r, z, b = C.c_longlong(), C.c_longlong(), C.c_longlong()
+        check(lib.sblas_ctx_slice_info(self.h, d, C.byref(r), C.byref(z), C.byref(b)), "ctx_slice_info")
+        return r.value, z.value, b.value
+
+    def spmv_ex(self, alpha: float, beta: float, delay_us: float = 0.0, wait: bool = True):
+        """Timing form (sblas_ctx_spmv_ex).  Returns the 3 + 3g stats (ms) when
+        wait, else None (sync() collects them)."""
+        st = np.zeros(3 + 3 * self.ngpu)
+        check(lib.sblas_ctx_spmv_ex(self.h, alpha, beta, delay_us, int(wait), ptr(st)), "ctx_spmv_ex")
+        return st if wait else None
+
+    def sync(self) -> np.ndarray:
+        st = np.zeros(3 + 3 * self.ngpu)
+        check(lib.sblas_ctx_sync(self.h, ptr(st)), "ctx_sync")
+        return st
 
     def set_x(self, x) -> None:
         check(lib.sblas_ctx_set_x(self.h, ptr(np.ascontiguousarray(x, np.float64))), "ctx_set_x")

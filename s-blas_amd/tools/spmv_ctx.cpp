@@ -3,6 +3,10 @@
 // the y slices, device placement).  No Python anywhere on this path.
 //
 //   spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0=cyclic|1=nnz] [reps]
+//            [exchange 0=allgather|1=allreduce (needs partition 1)]
+//
+// `spmv_ctx 8 2000000 2 1 20 1` is BASELINE configs[2] from C++: the CSR5
+// kernel on spMV_mgpu_v1's nnz split over 8 GPUs, y merged by ncclAllReduce.
 //
 // Matrix: the config-2 synthetic (rows < n/8: 96 nnz, others 9, uniform
 // random sorted columns, seed 42), x U[0,1) seed 43, y0 U[0,1) seed 44,
@@ -22,7 +26,7 @@
 int main(int argc, char **argv)
 {
     if (argc < 3) {
-        printf("Usage: ./spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0|1] [reps]\n");
+        printf("Usage: ./spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0|1] [reps] [exchange 0|1]\n");
         return -1;
     }
     const int ngpu = atoi(argv[1]);
@@ -30,6 +34,7 @@ int main(int argc, char **argv)
     const int algo = argc > 3 ? atoi(argv[3]) : SBLAS_SPMV_XSORT;
     const int part = argc > 4 ? atoi(argv[4]) : 0;
     const int reps = argc > 5 ? atoi(argv[5]) : 10;
+    const int xchg = argc > 6 ? atoi(argv[6]) : SBLAS_CTX_ALLGATHER;
     std::vector<long long> rp((size_t)n + 1);
     sblas_gen_synth_rowptr(n, 96, 9, rp.data());
     const long long nnz = rp[(size_t)n];
@@ -39,8 +44,8 @@ int main(int argc, char **argv)
     sblas_gen_vector(n, 43, x.data());
     sblas_gen_vector(n, 44, y0.data());
     double alpha = 0.8401877171547095, beta = 0.39438292681909304;
-    printf("m: %d n: %d nnz: %lld, %d GPU(s), algo %d, partition %s\n", n, n, nnz, ngpu, algo,
-           part ? "nnz" : "cyclic");
+    printf("m: %d n: %d nnz: %lld, %d GPU(s), algo %d, partition %s, exchange %s\n", n, n, nnz, ngpu, algo,
+           part ? "nnz" : "cyclic", xchg ? "allreduce" : "allgather");
 
     sblas_ctx ctx = nullptr;
     int st = sblas_ctx_create(&ctx, ngpu, nullptr);
@@ -49,7 +54,7 @@ int main(int argc, char **argv)
         return 1;
     }
     const double t0 = sblas_get_time();
-    st = sblas_ctx_matrix_upload(ctx, n, n, rp.data(), col.data(), val.data(), algo, part);
+    st = sblas_ctx_matrix_upload_ex(ctx, n, n, rp.data(), col.data(), val.data(), algo, part, xchg);
     const double t_up = sblas_get_time() - t0;
     if (st == SBLAS_OK) st = sblas_ctx_set_x(ctx, x.data());
     if (st != SBLAS_OK) {
@@ -74,6 +79,13 @@ int main(int argc, char **argv)
     if (reps > 0)
         printf("ctx spmv: kernel %.4f ms, exchange %.4f ms, step %.4f ms = %.1f GFLOP/s\n", sk / reps,
                sx / reps, stt / reps, 2.0 * nnz / (stt / reps * 1e-3) / 1e9);
+    // the timing protocol (device-side hold + aligning all-reduce) once
+    std::vector<double> tst((size_t)3 + 3 * ngpu);
+    if ((st = sblas_ctx_spmv_ex(ctx, alpha, beta, 500.0, 1, tst.data())) != SBLAS_OK) {
+        printf("spmv_ex failed: %s (%s)\n", sblas_status_string(st), sblas_last_error());
+        return 1;
+    }
+    printf("ctx aligned step: kernel max %.4f ms, step max %.4f ms\n", tst[0], tst[2]);
     // one checked step from y0
     sblas_ctx_set_y(ctx, y0.data());
     sblas_ctx_spmv(ctx, alpha, beta, nullptr);

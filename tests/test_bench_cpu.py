@@ -1,0 +1,53 @@
+"""bench.py's driver routing (no GPU): `python bench.py --gpus N` must measure
+N GPUs or exit non-zero -- one process per GPU under a launcher (WORLD_SIZE
+set), else one process driving N GPUs through the C-ABI context (sblas_ctx),
+mirroring the reference's single host call over every GPU
+(spmv/test/dspmv_test.cu:355-383 -> spmv/src/dspmv_mgpu_v1.cu:16-280)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("gpus,env,ndev,req,want", [
+    (1, {}, 1, "auto", "single"),
+    (1, {}, 8, "ctx", "ctx"),
+    (2, {}, 8, "auto", "ctx"),
+    (8, {}, 8, "auto", "ctx"),
+    (8, {"WORLD_SIZE": "8"}, 8, "auto", "torch"),
+    (1, {"WORLD_SIZE": "1"}, 1, "auto", "torch"),
+    (1, {"WORLD_SIZE": "1"}, 1, "ctx", "ctx"),
+])
+def test_choose_driver(gpus, env, ndev, req, want):
+    assert bench.choose_driver(gpus, env, ndev, req) == want
+
+
+@pytest.mark.parametrize("gpus,env,ndev,req", [
+    (9, {}, 8, "auto"),                   # more GPUs than visible
+    (2, {}, 1, "auto"),
+    (1, {}, 0, "auto"),
+    (0, {}, 8, "auto"),
+    (4, {"WORLD_SIZE": "2"}, 8, "auto"),  # launcher disagrees with --gpus
+    (8, {"WORLD_SIZE": "8"}, 8, "ctx"),   # ctx is one process: no launcher
+    (4, {}, 8, "torch"),                  # torch ranks need a launcher
+])
+def test_choose_driver_refuses(gpus, env, ndev, req):
+    with pytest.raises(ValueError):
+        bench.choose_driver(gpus, env, ndev, req)
+
+
+def test_bench_exits_nonzero_when_gpus_exceed_devices():
+    """--gpus above the visible device count exits 2 with a message before
+    any data is generated (here: no GPU at all, or one on the box)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "refusing to measure fewer GPUs" in r.stderr
+    assert r.stdout.strip() == ""

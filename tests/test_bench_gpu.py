@@ -1,0 +1,41 @@
+"""bench.py through the single-process C-ABI context (`--driver ctx`): the
+path `python bench.py --gpus N` takes without a launcher.  At N = 1 on this
+pool: allgather over cyclic chunks (xsort, row split) and BASELINE
+configs[2]'s literal form (CSR5 kernel, nnz-balanced rows, ncclAllReduce of
+the zero-padded y).  --check compares device 0's y with the oracle under the
+per-row fp64 bound and requires every device's y to be
+bit-identical."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("algo,partition,exchange", [
+    ("xsort", "cyclic", "allgather"),
+    ("rowsplit", "nnz", "allgather"),
+    ("csr5", "nnz", "allreduce"),
+    ("panel", "cyclic", "allgather"),
+])
+def test_bench_ctx_driver(algo, partition, exchange):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--driver", "ctx", "--check",
+           "--nrows", "200000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--algo", algo,
+           "--partition", partition, "--exchange", exchange]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout  # the contract: ONE JSON line on stdout
+    line = json.loads(lines[0])
+    assert line["check_vs_oracle"] is True
+    assert line["n_gpus"] == 1
+    assert line["config"]["driver"].startswith("ctx")
+    assert line["config"]["exchange"] == exchange
+    assert line["ms_per_step"] > 0 and line["kernel_ms_max_over_ranks"] > 0
+    assert line["ms_per_step"] >= line["kernel_ms_max_over_ranks"]

@@ -30,10 +30,11 @@ def rand_csr(rng, m, n, maxlen, long_rows=()):
 
 
 @pytest.mark.parametrize("algo", [1, 2, 4, 5])
-@pytest.mark.parametrize("partition", [0, 1])
-def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition):
+@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
+def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition, exchange):
     """Two chained steps (the second's beta input is the first's y, kept on
-    the devices by the context) against the oracle."""
+    the devices by the context) against the oracle; exchange 1 is the
+    literal all-reduce of the zero-padded y (BASELINE configs[2])."""
     rng = np.random.default_rng(algo + 10 * partition)
     m, n = 5000, 7000
     rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(3, 6000), (4000, 2500)])
@@ -41,7 +42,7 @@ def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition):
     y0 = rng.standard_normal(m)
     alpha, beta = orc.alpha_beta()
     ctx = sb.DeviceCtx(1)
-    ctx.upload(m, n, rp, col, val, algo, partition)
+    ctx.upload(m, n, rp, col, val, algo, partition, exchange)
     ctx.set_x(x)
     ctx.set_y(y0)
     k, xch, tot = ctx.spmv(alpha, beta)
@@ -72,6 +73,46 @@ def test_ctx_config2_full_size(torch_cuda, sb, orc, algo):
     got = ctx.get_y()
     want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
     assert np.all(np.abs(got - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+    ctx.close()
+
+
+def test_ctx_timed_steps_and_slice_info(torch_cuda, sb, orc):
+    """sblas_ctx_spmv_ex's timing protocol (device-side hold + aligning
+    all-reduce), the non-waiting form + sblas_ctx_sync, and slice_info."""
+    rng = np.random.default_rng(7)
+    m, n = 3000, 4000
+    rp, col, val = rand_csr(rng, m, n, 30)
+    x = rng.standard_normal(n)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(1)
+    ctx.upload(m, n, rp, col, val, 5, 1, sb.CTX_ALLREDUCE)
+    rows, nnz, byts = ctx.slice_info(0)
+    assert (rows, nnz) == (m, int(rp[-1]))
+    assert byts == 12 * nnz + 4 * (m + 1) + 8 * n + 16 * m
+    ctx.set_x(x)
+    y = np.zeros(m)
+    ctx.set_y(y)
+    st = ctx.spmv_ex(alpha, beta, delay_us=200.0)
+    assert st.shape == (6,) and st[0] > 0 and st[2] >= st[0] and st[2] < 50.0
+    assert st[3] == st[0] and st[5] == st[2]
+    y = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+    for _ in range(3):
+        assert ctx.spmv_ex(alpha, beta, wait=False) is None
+        y_prev = y
+        y = orc.csr_spmv(rp, col, val, x, alpha, beta, y_prev)
+    last = ctx.sync()
+    assert last[2] > 0
+    got = ctx.get_y()
+    assert np.allclose(got, y, rtol=1e-12, atol=1e-12)
+    ctx.close()
+
+
+def test_ctx_allreduce_needs_nnz_partition(torch_cuda, sb):
+    rng = np.random.default_rng(8)
+    rp, col, val = rand_csr(rng, 100, 100, 5)
+    ctx = sb.DeviceCtx(1)
+    with pytest.raises(sb.SblasError):
+        ctx.upload(100, 100, rp, col, val, 2, 0, sb.CTX_ALLREDUCE)
     ctx.close()
 
 
@@ -107,13 +148,14 @@ def test_ctx_rejects_shared_devices(torch_cuda, sb):
         sb.DeviceCtx(2, devices=[0, 0])
 
 
-@pytest.mark.parametrize("algo,partition", [(5, 0), (2, 1), (1, 0)])
-def test_cli_spmv_ctx(algo, partition):
+@pytest.mark.parametrize("algo,partition,exchange", [(5, 0, 0), (2, 1, 0), (1, 0, 0), (2, 1, 1)])
+def test_cli_spmv_ctx(algo, partition, exchange):
     """The C++ driver (tools/spmv_ctx.cpp): a C caller reaching the RCCL path
     with no Python; it checks device agreement, the host-merge reference API
     and the bound reference API."""
     exe = os.path.join(ROOT, "s-blas_amd", "bin", "spmv_ctx")
-    r = subprocess.run([exe, "1", "2000000", str(algo), str(partition), "5"], capture_output=True,
+    r = subprocess.run([exe, "1", "2000000", str(algo), str(partition), "5", str(exchange)],
+                       capture_output=True,
                        text=True, timeout=120, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ctx devices agree: PASS" in r.stdout

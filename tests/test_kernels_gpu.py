@@ -89,6 +89,43 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     A.close()
 
 
+@pytest.mark.parametrize("layout", [0, 1])
+def test_spmm_two_handles_two_streams(torch_cuda, sb, orc, monkeypatch, layout):
+    """Two handles of different matrices on two streams of one device, launched
+    back to back without synchronising: each keeps its own scratch (B copy,
+    C-tile partials: sblas_csr_s::spmm_*), so both C match the oracle."""
+    torch = torch_cuda
+    monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
+    ncols, k = 64, 6000
+    outs = []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i, m in enumerate((900, 1300)):
+        rng = np.random.default_rng(50 + i)
+        rp, col, val = rand_csr(rng, m, k, 60)
+        B = rng.standard_normal((k, ncols))
+        C0 = rng.standard_normal((m, ncols))
+        A = sb.DeviceCSR.upload(0, k, rp, col, val)
+        if layout == 0:
+            Bd = torch.from_numpy(np.asfortranarray(B).ravel(order="F")).cuda()
+            ldb = k
+        else:
+            Bd = torch.from_numpy(np.ascontiguousarray(B).ravel()).cuda()
+            ldb = ncols
+        Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
+        outs.append((A, Bd, ldb, Cd, rp, col, val, B, C0, m))
+    torch.cuda.synchronize()
+    for rep in range(3):  # C <- alpha*A*B + beta*C, three times on each stream
+        for (A, Bd, ldb, Cd, *_), st in zip(outs, streams):
+            A.spmm(ncols, 0.5, Bd.data_ptr(), ldb, layout, 0.0 if rep else 1.0, Cd.data_ptr(),
+                   Cd.numel() // ncols, st.cuda_stream)
+    torch.cuda.synchronize()
+    for A, Bd, ldb, Cd, rp, col, val, B, C0, m in outs:
+        want = orc.spmm(m, ncols, k, 0.5, rp, col, val, B, 0.0, C0)
+        got = Cd.cpu().numpy().reshape((ncols, m)).T
+        assert np.all(np.abs(got - want) <= spmm_bound(rp, col, val, B, 0.5, 0.0, C0))
+        A.close()
+
+
 @pytest.mark.parametrize("split", ["rows", "cols"])
 @pytest.mark.parametrize("ngpu", [1, 2, 3])
 def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
