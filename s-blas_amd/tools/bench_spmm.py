@@ -122,6 +122,10 @@ def main():
                          "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0 compares EVERY entry of C with the oracle (orc_spmm_omp) under the "
+                         "per-entry fp64 bound (DESIGN.md §3), as dspmm_baseline_test.cu:544-549 "
+                         "checks every entry; test infrastructure, after the timed steps")
     ap.add_argument("--split", choices=["rows", "cols"], default="rows",
                     help="rows: whole-row blocks of A by nnz (north star); cols: A replicated, "
                          "B/C columns split (the reference's dspmm_mgpu_baseline.cu:147-150)")
@@ -218,6 +222,15 @@ def main():
             a, b_ = rp[r], rp[r + 1]
             want = -0.7 * (val[a:b_] @ Bh[col[a:b_], :]) + 0.8 * C0h[:, r]
             err = max(err, float(np.max(np.abs(got[:, r] - want) / (np.abs(want) + 1e-300))))
+        check = None
+        if args.check:
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "tests"))
+            import orc  # oracle: checker only
+            want, bound = orc.spmm_checked(m, n, -0.7, rp, col, val, Bh, 0.8, C0h.T)
+            diff = np.abs(got.T - want)
+            check = {"entries": int(diff.size), "pass": bool(np.all(diff <= bound)),
+                     "max_excess_over_bound": float(np.max(diff - bound)),
+                     "abs_1e-3": bool(np.all(diff < 1e-3 * np.maximum(1.0, np.abs(want))))}
         ms = el / args.steps * 1e3
         abytes = 12 * nnz + 4 * (m + 1) + 8 * k * n + 16 * m * n
         out = {
@@ -244,6 +257,8 @@ def main():
             "plan_build_s_rank0": round(plan_s, 3),
             "plan_build_note": "wall time of the first call (host plan build + one product)",
         }
+        if check is not None:
+            out["check_vs_oracle"] = check
         if world == 1 and not args.blocky and lay == 1:
             out["roofline"]["traffic"] = pmc_traffic_spmm()
         if world == 1 and not args.no_cpu_baseline:
