@@ -156,6 +156,15 @@ struct SpmmPlan {
     long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets
     bool ct_own = false;                 // rows owned by waves, plain LDS read-add-write
     long long *ct_woff = nullptr;        // own: [8*ns*nrb][17] per-wave entry offsets
+    // Tall-tile form (spmm.hip "tall tile"): C tile = all m rows x 4 columns
+    // in LDS; A's entries as column-run pieces grouped 16 at a time.
+    bool tt = false;
+    int tt_nlist = 0;                    // lists = 8 XCDs x 2 halves
+    int2 *tt_gdesc = nullptr;            // per group {first slot, slots per piece column L}
+    unsigned *tt_gcol = nullptr;         // per group 16 x (column | piece length << 24)
+    unsigned *tt_key = nullptr;          // per slot: row
+    double *tt_val = nullptr;            // per slot: value
+    int *tt_loff = nullptr;              // [nlist + 1] group offsets of the lists
     double fill_thresh = 0.25;
     bool ready = false;
 };

@@ -149,14 +149,22 @@ def cfg4(orc):
                 want=want, bound=bound)
 
 
-@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ctown"),
+@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ttile"), ("col", "ttile"),
+                                         ("row", "ttpiece4"), ("row", "ttwin1"), ("row", "ctown"),
                                          ("row", "ctslot"), ("row", "l2slice")])
 def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form):
     """BASELINE configs[3]: C = -0.7 A B + 0.8 C on the rail4284-shaped matrix,
     all 4284 x 64 entries of C checked (B row-major as resident in HBM, and
     the reference's column-major host layout), with the default column-sorted
-    C-tile form and the L2-slice form it replaced."""
+    C-tile form, the tall-tile form (opt-in: all rows x 4 columns per tile,
+    column-run pieces in bank-scheduled slots) and the L2-slice form."""
     torch = torch_cuda
+    if form.startswith("tt"):
+        monkeypatch.setenv("SBLAS_SPMM_TTILE", "1")
+    if form == "ttpiece4":
+        monkeypatch.setenv("SBLAS_SPMM_TTPIECE", "4")
+    if form == "ttwin1":  # consecutive pieces, no residue balancing
+        monkeypatch.setenv("SBLAS_SPMM_TTWIN", "1")
     if form == "l2slice":
         monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     if form == "ctslot":
