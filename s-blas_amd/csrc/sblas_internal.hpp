@@ -85,6 +85,31 @@ struct Csr5Plan {
     int nempty = 0;
     double *carry = nullptr;       // [ntiles] tile head partial sums
     bool ready = false;
+    // XCD-affine form (spmv.hip "CSR5 over column panels"): one tile plan per
+    // column panel of the panel plan, panel p's tiles dealt to the XCDs with
+    // blockIdx % P == p, alpha-scaled partial y per panel, then a reduce.
+    int P = 0;                     // 0: plain CSR5 (this plan's own tiles)
+    std::vector<Csr5Plan> panels;  // host-side sub-plans (device arrays each)
+    struct Csr5Desc *desc = nullptr;  // device [P]
+    long long maxtiles = 0;
+    double *ypart = nullptr;       // [P][m]
+};
+
+// Device-side view of one CSR5 tile plan (the panel form's per-panel plans).
+struct Csr5Desc {
+    const int *tile_row;
+    const uint32_t *flags;
+    const double *tval;
+    const int *tcol;
+    const int *seg_off;
+    const int *seg_row;
+    const int *empty_rows;
+    double *y;        // this panel's partial y
+    double *carry;
+    long long ntiles;
+    long long nnz;
+    int nempty;
+    int pad;
 };
 
 // XCD-panel plan: A split into P column panels (x panel ~2 MiB), each a CSR

@@ -306,17 +306,16 @@ __global__ void k_c5_transpose(const int *__restrict__ col, const double *__rest
     tcol[t * kC5Tile + c5_cpos(l, k)] = in ? col[e] : 0;
 }
 
+// One wave64 tile t of a CSR5 plan (caller: t < ntiles, wave-uniform).
 template <bool kBeta>
-__global__ __launch_bounds__(256) void k_spmv_csr5(
-    const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+__device__ __forceinline__ void csr5_tile(
+    long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
     const double *__restrict__ tval, const int *__restrict__ tcol,
     const int *__restrict__ seg_off, const int *__restrict__ seg_row,
     const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
     double beta, double *__restrict__ y, double *__restrict__ carry)
 {
     const int lane = threadIdx.x & 63;
-    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= ntiles) return;  // wave-uniform
     const double *tv = tval + t * kC5Tile;
     const int *tc = tcol + t * kC5Tile;
     const uint32_t f = flags[t * 64 + lane];
@@ -401,14 +400,41 @@ __global__ __launch_bounds__(256) void k_spmv_csr5(
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
 
+template <bool kBeta>
+__global__ __launch_bounds__(256) void k_spmv_csr5(
+    const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+    const double *__restrict__ tval, const int *__restrict__ tcol,
+    const int *__restrict__ seg_off, const int *__restrict__ seg_row,
+    const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
+    double beta, double *__restrict__ y, double *__restrict__ carry)
+{
+    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;  // wave-uniform
+    csr5_tile<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
+}
+
+// CSR5 over XCD-affine column panels: block b runs tiles of panel b % P (the
+// hardware deals blocks to the XCDs round robin, so an XCD keeps to the
+// panels b % 8 selects: its x gathers stay in ~n*8/P bytes of x), writing
+// the panel's alpha-scaled partial y (beta applied by the reduce).
+__global__ __launch_bounds__(256) void k_spmv_csr5_panel(const Csr5Desc *__restrict__ desc, int P,
+                                                         const double *__restrict__ x, double alpha)
+{
+    const int p = (int)(blockIdx.x % P);
+    const long long t = (long long)(blockIdx.x / P) * 4 + (threadIdx.x >> 6);
+    const Csr5Desc &d = desc[p];
+    if (t >= d.ntiles) return;  // wave-uniform
+    csr5_tile<false>(t, d.tile_row, d.flags, d.tval, d.tcol, d.seg_off, d.seg_row, x, d.ntiles, d.nnz, alpha,
+                     0.0, d.y, d.carry);
+}
+
 // Adds each tile's head (the part of the row that started in an earlier
 // tile) to y, one thread per run of tiles sharing that row: deterministic.
-__global__ void k_csr5_calibrate(const int *__restrict__ tile_row,
-                                 const uint32_t *__restrict__ flags,
-                                 const double *__restrict__ carry, long long ntiles,
-                                 double alpha, double *__restrict__ y)
+__device__ __forceinline__ void csr5_calibrate(long long t, const int *__restrict__ tile_row,
+                                               const uint32_t *__restrict__ flags,
+                                               const double *__restrict__ carry, long long ntiles,
+                                               double alpha, double *__restrict__ y)
 {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     auto has_head = [&](long long u) { return (flags[u * 64] & 1u) == 0u; };
     if (!has_head(t)) return;
@@ -418,6 +444,22 @@ __global__ void k_csr5_calibrate(const int *__restrict__ tile_row,
     for (long long u = t; u < ntiles && (tile_row[u] & 0x7fffffff) == R && has_head(u); ++u)
         s += carry[u];
     y[R] += alpha * s;
+}
+
+__global__ void k_csr5_calibrate(const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+                                 const double *__restrict__ carry, long long ntiles, double alpha,
+                                 double *__restrict__ y)
+{
+    csr5_calibrate((long long)blockIdx.x * blockDim.x + threadIdx.x, tile_row, flags, carry, ntiles, alpha, y);
+}
+
+// panel form: blockIdx.y = panel; also zeroes the panel's empty rows
+__global__ void k_csr5_calibrate_panel(const Csr5Desc *__restrict__ desc, double alpha)
+{
+    const Csr5Desc &d = desc[blockIdx.y];
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.nempty) d.y[d.empty_rows[i]] = 0.0;
+    csr5_calibrate(i, d.tile_row, d.flags, d.carry, d.ntiles, alpha, d.y);
 }
 
 template <bool kBeta>
@@ -495,11 +537,9 @@ __global__ void k_c5_segrows(const int *__restrict__ rp, int m, long long nnz, l
         if (rp[q + 1] > rp[q] && rp[q] >= e && rp[q] <= elast) seg_row[o++] = q;
 }
 
-static int build_csr5_plan_device(sblas_csr_s &A, hipStream_t s)
+static int build_csr5_plan_device(Csr5Plan &P, const int *rowptr, int m, long long nnz, hipStream_t s)
 {
-    Csr5Plan &P = A.c5;
-    const long long nnz = A.nnz, nt = P.ntiles;
-    const int m = A.m;
+    const long long nt = P.ntiles;
     SBLAS_HIP(hipMalloc(&P.tile_row, sizeof(int) * (nt + 1)));
     SBLAS_HIP(hipMalloc(&P.flags, sizeof(uint32_t) * std::max<long long>(nt * 64, 1)));
     SBLAS_HIP(hipMalloc(&P.seg_off, sizeof(int) * (nt + 1)));
@@ -509,10 +549,10 @@ static int build_csr5_plan_device(sblas_csr_s &A, hipStream_t s)
     SBLAS_HIP(hipMemsetAsync(P.seg_off, 0, sizeof(int) * (nt + 1), s));
     SBLAS_HIP(hipMemsetAsync(nempty, 0, sizeof(int), s));
     if (m > 0)
-        hipLaunchKernelGGL(k_c5_flags, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+        hipLaunchKernelGGL(k_c5_flags, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, rowptr, m,
                            P.flags, P.empty_rows, nempty);
     // seg_off[0] = 0, seg_off[1..nt] = inclusive scan of the per-tile counts
-    hipLaunchKernelGGL(k_c5_tiles, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+    hipLaunchKernelGGL(k_c5_tiles, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, s, rowptr, m,
                        nnz, nt, P.flags, P.tile_row, P.seg_off + 1);
     SBLAS_HIP(hipGetLastError());
     int *scratch = nullptr;
@@ -529,9 +569,84 @@ static int build_csr5_plan_device(sblas_csr_s &A, hipStream_t s)
     P.nempty = h[1];
     SBLAS_HIP(hipMalloc(&P.seg_row, sizeof(int) * std::max(h[0], 1)));
     if (h[0] > 0)
-        hipLaunchKernelGGL(k_c5_segrows, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, A.rowptr, m,
+        hipLaunchKernelGGL(k_c5_segrows, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, rowptr, m,
                            nnz, nt, P.flags, P.tile_row, P.seg_off + 1, P.seg_row);
     SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+template <bool kBeta>
+__global__ void k_panel_reduce(const double *__restrict__ ypart, int P, long long m, double beta,
+                               double *__restrict__ y);
+
+// the device builder over raw CSR arrays (the whole matrix or one panel)
+static int build_csr5_core(Csr5Plan &P, const int *rowptr, const int *col, const double *val, int m,
+                           long long nnz, hipStream_t s)
+{
+    P.ntiles = (nnz + kC5Tile - 1) / kC5Tile;
+    SBLAS_TRY(build_csr5_plan_device(P, rowptr, m, nnz, s));
+    const long long nt = P.ntiles, total = nt * kC5Tile;
+    SBLAS_HIP(hipMalloc(&P.tval, sizeof(double) * std::max<long long>(total, 1)));
+    SBLAS_HIP(hipMalloc(&P.tcol, sizeof(int) * std::max<long long>(total, 1)));
+    SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
+    if (total) {
+        hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, col, val, nnz,
+                           total, P.tcol, P.tval);
+        SBLAS_HIP(hipGetLastError());
+    }
+    SBLAS_HIP(hipStreamSynchronize(s));
+    P.ready = true;
+    return SBLAS_OK;
+}
+
+static void free_csr5_arrays(Csr5Plan &P)
+{
+    (void)hipFree(P.tile_row);
+    (void)hipFree(P.flags);
+    (void)hipFree(P.tval);
+    (void)hipFree(P.tcol);
+    (void)hipFree(P.seg_off);
+    (void)hipFree(P.seg_row);
+    (void)hipFree(P.empty_rows);
+    (void)hipFree(P.carry);
+    for (Csr5Plan &Q : P.panels) free_csr5_arrays(Q);
+    (void)hipFree(P.desc);
+    (void)hipFree(P.ypart);
+}
+
+// CSR5 over the panel plan's column panels (XCD-affine x gathers): one tile
+// plan per non-empty panel.  Opt-in (SBLAS_CSR5_PANEL=1; SBLAS_PANELS sets
+// the panel count).  Measured on config 2 (profiles/r03/csr5_panel/): P = 2 /
+// 4 / 8 run 309 / 349 / 427 us against 329 us for the plain form, and the
+// N = 8 slice 49.6 against 50.1 us: a panel row holds ~2.25 entries, so each
+// tile ends ~7 rows per lane (scattered 8-B partial-y writes) and nearly
+// every tile holds empty rows (the seg_row path), which eats what the
+// XCD-local gathers save.
+static int build_csr5_panels(sblas_csr_s &A, hipStream_t s)
+{
+    Csr5Plan &P = A.c5;
+    SBLAS_TRY(build_panel_plan(A, s));
+    const PanelPlan &Q = A.pn;
+    if (Q.degenerate || Q.P < 2) return SBLAS_ERR_UNSUPPORTED;
+    std::vector<PanelDesc> pd((size_t)Q.P);
+    SBLAS_HIP(hipMemcpy(pd.data(), Q.desc, sizeof(PanelDesc) * Q.P, hipMemcpyDeviceToHost));
+    const long long m = A.m;
+    P.panels.assign((size_t)Q.P, Csr5Plan{});
+    std::vector<Csr5Desc> hd((size_t)Q.P);
+    SBLAS_HIP(hipMalloc(&P.ypart, sizeof(double) * std::max<long long>(Q.P * m, 1)));
+    for (int q = 0; q < Q.P; ++q) {
+        int nz = 0;
+        SBLAS_HIP(hipMemcpy(&nz, pd[(size_t)q].rowptr + m, sizeof(int), hipMemcpyDeviceToHost));
+        Csr5Plan &S = P.panels[(size_t)q];
+        SBLAS_TRY(build_csr5_core(S, pd[(size_t)q].rowptr, pd[(size_t)q].col, pd[(size_t)q].val, (int)m, nz, s));
+        hd[(size_t)q] = Csr5Desc{S.tile_row, S.flags, S.tval, S.tcol, S.seg_off, S.seg_row, S.empty_rows,
+                                 P.ypart + (size_t)q * m, S.carry, S.ntiles, (long long)nz, S.nempty, 0};
+        P.maxtiles = std::max(P.maxtiles, S.ntiles);
+    }
+    SBLAS_HIP(hipMalloc(&P.desc, sizeof(Csr5Desc) * Q.P));
+    SBLAS_HIP(hipMemcpy(P.desc, hd.data(), sizeof(Csr5Desc) * Q.P, hipMemcpyHostToDevice));
+    P.P = Q.P;
+    P.ready = true;
     return SBLAS_OK;
 }
 
@@ -541,22 +656,15 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     DeviceGuard g(A.device);
     Csr5Plan &P = A.c5;
     const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
-    if (!(hp && atoi(hp) == 1)) {
-        P.ntiles = (A.nnz + kC5Tile - 1) / kC5Tile;
-        SBLAS_TRY(build_csr5_plan_device(A, s));
-        const long long nt = P.ntiles, total = nt * kC5Tile;
-        SBLAS_HIP(hipMalloc(&P.tval, sizeof(double) * std::max<long long>(total, 1)));
-        SBLAS_HIP(hipMalloc(&P.tcol, sizeof(int) * std::max<long long>(total, 1)));
-        SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
-        if (total) {
-            hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                               A.col, A.val, A.nnz, total, P.tcol, P.tval);
-            SBLAS_HIP(hipGetLastError());
-        }
-        SBLAS_HIP(hipStreamSynchronize(s));
-        P.ready = true;
-        return SBLAS_OK;
+    const char *pe = getenv("SBLAS_CSR5_PANEL");
+    if (pe && atoi(pe) == 1 && !(hp && atoi(hp) == 1)) {
+        const int rc = build_csr5_panels(A, s);
+        if (rc == SBLAS_OK) return SBLAS_OK;
+        free_csr5_arrays(P);
+        A.c5 = Csr5Plan{};
+        if (rc != SBLAS_ERR_UNSUPPORTED) return rc;
     }
+    if (!(hp && atoi(hp) == 1)) return build_csr5_core(P, A.rowptr, A.col, A.val, A.m, A.nnz, s);
     const long long nnz = A.nnz;
     const std::vector<int> &rp = A.h_rowptr;
     P.ntiles = (nnz + kC5Tile - 1) / kC5Tile;
@@ -632,6 +740,24 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
 {
     const Csr5Plan &P = A.c5;
     if (!P.ready) return SBLAS_ERR_INVALID;
+    if (P.P > 0) {  // XCD-affine panels
+        if (A.m == 0) return SBLAS_OK;
+        const long long grid = (P.maxtiles + 3) / 4 * P.P;
+        if (grid > 0)
+            SBLAS_LAUNCH(k_spmv_csr5_panel, dim3((unsigned)grid), dim3(256), 0, s, P.desc, P.P, x, alpha);
+        long long mc = P.maxtiles;
+        for (const Csr5Plan &Q : P.panels) mc = std::max<long long>(mc, Q.nempty);
+        if (mc > 0)
+            SBLAS_LAUNCH(k_csr5_calibrate_panel, dim3((unsigned)((mc + 255) / 256), (unsigned)P.P), dim3(256), 0, s,
+                         P.desc, alpha);
+        const unsigned rb = (unsigned)((A.m + 255) / 256);
+        if (beta != 0.0)
+            SBLAS_LAUNCH(k_panel_reduce<true>, dim3(rb), dim3(256), 0, s, P.ypart, P.P, (long long)A.m, beta, y);
+        else
+            SBLAS_LAUNCH(k_panel_reduce<false>, dim3(rb), dim3(256), 0, s, P.ypart, P.P, (long long)A.m, beta, y);
+        SBLAS_HIP(hipGetLastError());
+        return SBLAS_OK;
+    }
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
         if (beta != 0.0)
@@ -890,15 +1016,7 @@ void free_plans(sblas_csr_s &A)
     (void)hipFree(A.rs.long_rows);
     (void)hipFree(A.rs.partial);
     A.rs = RsPlan{};
-    Csr5Plan &P = A.c5;
-    (void)hipFree(P.tile_row);
-    (void)hipFree(P.flags);
-    (void)hipFree(P.tval);
-    (void)hipFree(P.tcol);
-    (void)hipFree(P.seg_off);
-    (void)hipFree(P.seg_row);
-    (void)hipFree(P.empty_rows);
-    (void)hipFree(P.carry);
+    free_csr5_arrays(A.c5);
     A.c5 = Csr5Plan{};
     PanelPlan &Q = A.pn;
     (void)hipFree(Q.rowptr);

@@ -73,10 +73,10 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
 
 
 @pytest.mark.parametrize("algo,env", [
-    (1, {}), (2, {}), (3, {}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
+    (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
     (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_K24": "0"}),
     (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2"})],
-    ids=["rowsplit", "csr5", "csr5_alt", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused",
+    ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused",
          "xsort_k32", "xsort_k24_u2"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
@@ -87,7 +87,8 @@ def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
 
 
 def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
-    """beta = 0 must not read y (y pre-filled with NaN), xsort and row split."""
+    """beta = 0 must not read y (y pre-filled with NaN): xsort, row split and
+    CSR5."""
     torch = torch_cuda
     if cfg2["prefix"]:
         pytest.skip("random columns only")
@@ -96,7 +97,7 @@ def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     bound = orc.spmv_bound(cfg2["rp"], cfg2["col"], cfg2["val"], cfg2["xd"].cpu().numpy(), 1.5,
                            0.0, np.zeros(N2))
     A = sb.DeviceCSR.upload(0, N2, cfg2["rp"], cfg2["col"], cfg2["val"])
-    for algo in (1, 5):
+    for algo in (1, 5, 2):
         A.analyse(algo)
         yd = torch.full((N2,), float("nan"), dtype=torch.float64, device="cuda")
         A.spmv(algo, 1.5, cfg2["xd"].data_ptr(), 0.0, yd.data_ptr())

@@ -24,7 +24,9 @@ pytestmark = pytest.mark.gpu
 # with each other), and PAIR=0 runs one sub-item per workgroup.  Q = 2 / 3
 # column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
 # cover the wide sub-items' group ranges and the narrow wrap at q > 1.
-ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}), (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
+ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
+         (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "3"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "8"}),
+         (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
@@ -35,7 +37,7 @@ ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}), (4, {}), (4, {"SBL
          (5, {"SBLAS_XS_K24": "2"}), (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K24": "0"})]
-ALGO_IDS = ["rowsplit", "csr5", "csr5_hostplan", "panel", "panel3", "panel8", "xsort", "xsort_w50",
+ALGO_IDS = ["rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_k24", "xsort_k24_w50", "xsort_k24_q3_w50", "xsort_k24_u2_w50", "xsort_k32"]
