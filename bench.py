@@ -113,7 +113,7 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
     }
 
 
-def choose_driver(gpus: int, env, ndev: int, requested: str = "auto") -> str:
+def choose_driver(gpus: int, env, ndev: int, requested: str = "auto", loopback: bool = False) -> str:
     """How `bench.py --gpus N` runs: "torch" (one process per GPU, started by
     a launcher that set WORLD_SIZE), "ctx" (one process driving N GPUs through
     sblas_ctx), or "single" (one process, one GPU, the persistent device
@@ -128,6 +128,10 @@ def choose_driver(gpus: int, env, ndev: int, requested: str = "auto") -> str:
         if world != gpus:
             raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE {world} ranks")
         return "ctx" if requested == "ctx" else "torch"
+    if loopback:  # rehearsal of the ctx path: N context ranks wrapped onto the visible GPUs
+        if ndev < 1:
+            raise ValueError("--ctx-loopback needs at least one GPU")
+        return "ctx"
     if gpus > ndev:
         raise ValueError(f"--gpus {gpus} but {ndev} GPU(s) visible: refusing to measure fewer GPUs")
     if requested == "torch" and gpus > 1:
@@ -165,6 +169,9 @@ def run_ctx(args) -> int:
     import sblas
 
     N = args.gpus
+    ndev = torch.cuda.device_count()
+    if args.ctx_loopback:
+        os.environ["SBLAS_CTX_LOOPBACK"] = "1"  # read by sblas_ctx_create
     algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
                 "xsort": sblas.XSORT}
     n = args.nrows
@@ -209,10 +216,11 @@ def run_ctx(args) -> int:
     delay_us = 300.0 + 150.0 * N
     for _ in range(args.warmup):
         ctx.spmv_ex(ALPHA, BETA)
-    scrubs = [torch.zeros(1 << 30, dtype=torch.uint8, device=torch.device("cuda", d)) for d in range(N)]
+    devs = sorted({d % ndev for d in range(N)})  # physical devices (wrapped in loopback)
+    scrubs = [torch.zeros(1 << 30, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
 
     def sync_all():
-        for d in range(N):
+        for d in devs:
             torch.cuda.synchronize(d)
 
     def evict():
@@ -329,7 +337,10 @@ def run_ctx(args) -> int:
         out["ms_per_step"] = round(warm_el / args.steps * 1e3, 5)
     if check is not None:
         out["check_vs_oracle"] = check
-    if N == 1 and not args.no_cpu_baseline:
+    if args.ctx_loopback:
+        out["note"] = (f"loopback rehearsal: {N} context ranks on {ndev} GPU(s), collectives as "
+                       "stream-ordered device copies (no RCCL); not a measurement")
+    if N == 1 and not args.no_cpu_baseline and not args.ctx_loopback:
         out["cpu_baseline"] = cpu_baseline(rowptr, col, val, x_h, n, nnz, args.cpu_budget)
     print(json.dumps(out), flush=True)
     ctx.close()
@@ -380,6 +391,11 @@ def main() -> int:
                     help="join a process group even at WORLD_SIZE 1 (torchrun --nproc-per-node 1): "
                          "runs the N > 1 exchange and timing path, RCCL included, on one GPU")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--ctx-loopback", action="store_true",
+                    help="rehearsal only: the ctx driver with its N ranks wrapped onto the visible "
+                         "GPUs and the collectives done as stream-ordered device copies instead of "
+                         "RCCL (SBLAS_CTX_LOOPBACK=1); checks the N > 1 partition / exchange / "
+                         "placement logic on a one-GPU box (use with --check)")
     ap.add_argument("--driver", choices=["auto", "ctx", "torch"], default="auto",
                     help="auto: torch.distributed ranks under a launcher, else one process over "
                          "sblas_ctx for --gpus > 1 (the persistent single-GPU path at N = 1); "
@@ -390,7 +406,7 @@ def main() -> int:
 
     ndev = torch.cuda.device_count()  # does not initialise the GPU
     try:
-        driver = choose_driver(args.gpus, os.environ, ndev, args.driver)
+        driver = choose_driver(args.gpus, os.environ, ndev, args.driver, args.ctx_loopback)
     except ValueError as e:
         print(f"bench.py: {e}", file=sys.stderr)
         return 2

@@ -46,6 +46,11 @@ struct sblas_ctx_s {
     std::vector<long long> yoff;       // the kernel's y = ylocal[d] + yoff[d]
     std::vector<double> last;          // stats of the last sblas_ctx_spmv_ex (3 + 3g)
     bool pending = false;              // a step was issued without waiting (wait = 0)
+    // loopback rehearsal (SBLAS_CTX_LOOPBACK=1): ranks may share a GPU, no
+    // communicator; the collectives are stream-ordered device copies / sums
+    bool loopback = false;
+    std::vector<hipEvent_t> evx, evy;  // [g] cross-stream sync events
+    std::vector<const double **> yptr; // allreduce: per device, the g send buffers
 };
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
@@ -105,6 +110,101 @@ __global__ void k_ctx_reprime(const double *__restrict__ yfull, double *__restri
     ysend[i] = (i == 0 && cont) ? 0.0 : yfull[i];
 }
 
+// loopback allreduce: dst = sum of the g send buffers, in rank order
+__global__ void k_ctx_sum(const double *const *__restrict__ src, int g, long long m, double *__restrict__ dst)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double s = 0.0;
+    for (int r = 0; r < g; ++r) s += src[r][i];
+    dst[i] = s;
+}
+
+// loopback: every stream waits for everything issued so far on every stream
+int lb_barrier(sblas_ctx_s &C, std::vector<hipEvent_t> &ev)
+{
+    for (int d = 0; d < C.g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        SBLAS_HIP(hipEventRecord(ev[d], C.st[d]));
+    }
+    for (int d = 0; d < C.g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        for (int e = 0; e < C.g; ++e)
+            if (e != d) SBLAS_HIP(hipStreamWaitEvent(C.st[d], ev[e], 0));
+    }
+    return SBLAS_OK;
+}
+
+// x from device 0 to every device (ncclBroadcast)
+int xchg_broadcast_x(sblas_ctx_s &C)
+{
+    if (!C.loopback) {
+        SBLAS_NCCL(ncclGroupStart());
+        for (int d = 0; d < C.g; ++d) {
+            DeviceGuard g(C.dev[d]);
+            SBLAS_NCCL_G(ncclBroadcast(C.x[d], C.x[d], (size_t)C.n, ncclDouble, 0, C.comm[d], C.st[d]));
+        }
+        SBLAS_NCCL(ncclGroupEnd());
+        return SBLAS_OK;
+    }
+    SBLAS_TRY(lb_barrier(C, C.evx));
+    for (int d = 1; d < C.g; ++d) {
+        DeviceGuard g(C.dev[d]);
+        SBLAS_HIP(hipMemcpyAsync(C.x[d], C.x[0], sizeof(double) * C.n, hipMemcpyDeviceToDevice, C.st[d]));
+    }
+    return lb_barrier(C, C.evy);
+}
+
+// the timing protocol's aligning one-word all-reduce
+int xchg_barrier(sblas_ctx_s &C)
+{
+    if (!C.loopback) {
+        SBLAS_NCCL(ncclGroupStart());
+        for (int d = 0; d < C.g; ++d) {
+            DeviceGuard gd(C.dev[d]);
+            SBLAS_NCCL_G(ncclAllReduce(C.bar[d], C.bar[d], 1, ncclDouble, ncclSum, C.comm[d], C.st[d]));
+        }
+        SBLAS_NCCL(ncclGroupEnd());
+        return SBLAS_OK;
+    }
+    return lb_barrier(C, C.evx);
+}
+
+// the step's exchange: all-gather of the padded slices or all-reduce of the
+// zero-padded y
+int xchg_spmv(sblas_ctx_s &C)
+{
+    const int g = C.g;
+    if (!C.loopback) {
+        SBLAS_NCCL(ncclGroupStart());
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C.dev[d]);
+            if (C.exchange == SBLAS_CTX_ALLGATHER)  // one all-gather of equal padded slices over xGMI
+                SBLAS_NCCL_G(ncclAllGather(C.ylocal[d], C.gathered[d], (size_t)C.stride, ncclDouble, C.comm[d],
+                                           C.st[d]));
+            else  // BASELINE configs[2]: the literal all-reduce of the zero-padded y
+                SBLAS_NCCL_G(ncclAllReduce(C.ylocal[d], C.yfull[d], (size_t)C.m, ncclDouble, ncclSum, C.comm[d],
+                                           C.st[d]));
+        }
+        SBLAS_NCCL(ncclGroupEnd());
+        return SBLAS_OK;
+    }
+    SBLAS_TRY(lb_barrier(C, C.evx));  // every slice written
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        if (C.exchange == SBLAS_CTX_ALLGATHER) {
+            for (int r = 0; r < g; ++r)
+                SBLAS_HIP(hipMemcpyAsync(C.gathered[d] + (size_t)r * C.stride, C.ylocal[r], sizeof(double) * C.stride,
+                                         hipMemcpyDeviceToDevice, C.st[d]));
+        } else if (C.m > 0) {
+            hipLaunchKernelGGL(k_ctx_sum, dim3((unsigned)((C.m + 255) / 256)), dim3(256), 0, C.st[d], C.yptr[d], g,
+                               (long long)C.m, C.yfull[d]);
+            SBLAS_HIP(hipGetLastError());
+        }
+    }
+    return lb_barrier(C, C.evy);  // every slice read before any is re-primed
+}
+
 void free_matrix(sblas_ctx_s &C)
 {
     for (int d = 0; d < (int)C.A.size(); ++d) {
@@ -116,7 +216,9 @@ void free_matrix(sblas_ctx_s &C)
         (void)hipFree(C.yfull[d]);
         (void)hipFree(C.meta[d]);
         (void)hipFree(C.bar[d]);
+        if (d < (int)C.yptr.size()) (void)hipFree(C.yptr[d]);
     }
+    C.yptr.clear();
     C.A.clear();
     C.x.clear();
     C.ylocal.clear();
@@ -179,15 +281,18 @@ int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist)
     if (!out || ngpu <= 0) return SBLAS_ERR_INVALID;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
+    // loopback rehearsal: ranks may share GPUs (ordinals wrap), no RCCL
+    const char *lbe = getenv("SBLAS_CTX_LOOPBACK");
+    const bool loopback = lbe && atoi(lbe) != 0;
     std::vector<int> dev(ngpu);
     for (int d = 0; d < ngpu; ++d) {
-        dev[d] = devlist ? devlist[d] : d;
+        dev[d] = devlist ? devlist[d] : loopback ? d % count : d;
         if (dev[d] < 0 || dev[d] >= count) {
             set_error("sblas_ctx_create: device %d of %d visible (one rank per GPU: no wrapping)",
                       dev[d], count);
             return SBLAS_ERR_INVALID;
         }
-        for (int e = 0; e < d; ++e)
+        for (int e = 0; e < d && !loopback; ++e)
             if (dev[e] == dev[d]) {
                 set_error("sblas_ctx_create: device %d listed twice", dev[d]);
                 return SBLAS_ERR_INVALID;
@@ -196,20 +301,27 @@ int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist)
     auto *C = new sblas_ctx_s();
     C->g = ngpu;
     C->dev = dev;
+    C->loopback = loopback;
     C->comm.assign(ngpu, nullptr);
-    ncclResult_t r = ncclCommInitAll(C->comm.data(), ngpu, dev.data());
-    if (r != ncclSuccess) {
-        set_error("ncclCommInitAll(%d): %s", ngpu, ncclGetErrorString(r));
-        C->comm.clear();
-        sblas_ctx_destroy(C);
-        return SBLAS_ERR_RCCL;
+    if (!loopback) {
+        ncclResult_t r = ncclCommInitAll(C->comm.data(), ngpu, dev.data());
+        if (r != ncclSuccess) {
+            set_error("ncclCommInitAll(%d): %s", ngpu, ncclGetErrorString(r));
+            C->comm.clear();
+            sblas_ctx_destroy(C);
+            return SBLAS_ERR_RCCL;
+        }
     }
     C->st.assign(ngpu, nullptr);
     C->ev.assign((size_t)3 * ngpu, nullptr);
+    C->evx.assign(ngpu, nullptr);
+    C->evy.assign(ngpu, nullptr);
     for (int d = 0; d < ngpu; ++d) {
         DeviceGuard g(dev[d]);
         hipError_t e = hipStreamCreateWithFlags(&C->st[d], hipStreamNonBlocking);
         for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreate(&C->ev[(size_t)3 * d + k]);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&C->evx[d], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&C->evy[d], hipEventDisableTiming);
         if (e != hipSuccess) {
             set_error("sblas_ctx_create: %s", hipGetErrorString(e));
             sblas_ctx_destroy(C);
@@ -232,6 +344,8 @@ int sblas_ctx_destroy(sblas_ctx C)
         for (int k = 0; k < 3; ++k)
             if ((size_t)3 * d + k < C->ev.size() && C->ev[(size_t)3 * d + k])
                 (void)hipEventDestroy(C->ev[(size_t)3 * d + k]);
+        if (d < (int)C->evx.size() && C->evx[d]) (void)hipEventDestroy(C->evx[d]);
+        if (d < (int)C->evy.size() && C->evy[d]) (void)hipEventDestroy(C->evy[d]);
     }
     delete C;
     return SBLAS_OK;
@@ -340,6 +454,18 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             st = SBLAS_ERR_HIP;
         }
     }
+    if (st == SBLAS_OK && C->loopback && exchange == SBLAS_CTX_ALLREDUCE) {
+        C->yptr.assign(g, nullptr);
+        for (int d = 0; d < g && st == SBLAS_OK; ++d) {
+            DeviceGuard gd(C->dev[d]);
+            std::vector<const double *> h(C->ylocal.begin(), C->ylocal.end());
+            if (hipMalloc(&C->yptr[d], sizeof(double *) * g) != hipSuccess ||
+                hipMemcpy(C->yptr[d], h.data(), sizeof(double *) * g, hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("sblas_ctx_matrix_upload: loopback pointer table");
+                st = SBLAS_ERR_HIP;
+            }
+        }
+    }
     if (st != SBLAS_OK) {
         free_matrix(*C);
         return st;
@@ -373,12 +499,7 @@ int sblas_ctx_set_x(sblas_ctx C, const double *x)
         SBLAS_HIP(hipMemcpyAsync(C->x[0], x, sizeof(double) * C->n, hipMemcpyHostToDevice, C->st[0]));
     }
     // replicate x from device 0 over xGMI
-    SBLAS_NCCL(ncclGroupStart());
-    for (int d = 0; d < C->g; ++d) {
-        DeviceGuard g(C->dev[d]);
-        SBLAS_NCCL_G(ncclBroadcast(C->x[d], C->x[d], (size_t)C->n, ncclDouble, 0, C->comm[d], C->st[d]));
-    }
-    SBLAS_NCCL(ncclGroupEnd());
+    SBLAS_TRY(xchg_broadcast_x(*C));
     for (int d = 0; d < C->g; ++d) {
         DeviceGuard g(C->dev[d]);
         SBLAS_HIP(hipStreamSynchronize(C->st[d]));
@@ -455,13 +576,7 @@ int sblas_ctx_spmv_ex(sblas_ctx C, double alpha, double beta, double delay_us, i
                                (unsigned long long)(delay_us * 100.0));
             SBLAS_HIP(hipGetLastError());
         }
-        SBLAS_NCCL(ncclGroupStart());
-        for (int d = 0; d < g; ++d) {
-            DeviceGuard gd(C->dev[d]);
-            SBLAS_NCCL_G(ncclAllReduce(C->bar[d], C->bar[d], 1, ncclDouble, ncclSum, C->comm[d],
-                                       C->st[d]));
-        }
-        SBLAS_NCCL(ncclGroupEnd());
+        SBLAS_TRY(xchg_barrier(*C));
     }
     for (int d = 0; d < g; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -471,17 +586,7 @@ int sblas_ctx_spmv_ex(sblas_ctx C, double alpha, double beta, double delay_us, i
                                  C->st[d]));
         SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 1], C->st[d]));
     }
-    SBLAS_NCCL(ncclGroupStart());
-    for (int d = 0; d < g; ++d) {
-        DeviceGuard gd(C->dev[d]);
-        if (C->exchange == SBLAS_CTX_ALLGATHER)  // one all-gather of equal padded slices over xGMI
-            SBLAS_NCCL_G(ncclAllGather(C->ylocal[d], C->gathered[d], (size_t)C->stride, ncclDouble,
-                                       C->comm[d], C->st[d]));
-        else  // BASELINE configs[2]: the literal all-reduce of the zero-padded y
-            SBLAS_NCCL_G(ncclAllReduce(C->ylocal[d], C->yfull[d], (size_t)C->m, ncclDouble, ncclSum,
-                                       C->comm[d], C->st[d]));
-    }
-    SBLAS_NCCL(ncclGroupEnd());
+    SBLAS_TRY(xchg_spmv(*C));
     for (int d = 0; d < g; ++d) {
         DeviceGuard gd(C->dev[d]);
         if (C->exchange == SBLAS_CTX_ALLREDUCE) {

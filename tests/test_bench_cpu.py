@@ -42,6 +42,13 @@ def test_choose_driver_refuses(gpus, env, ndev, req):
         bench.choose_driver(gpus, env, ndev, req)
 
 
+def test_choose_driver_loopback():
+    """the ctx rehearsal wraps N ranks onto the visible GPUs (never measures)"""
+    assert bench.choose_driver(8, {}, 1, "auto", loopback=True) == "ctx"
+    with pytest.raises(ValueError):
+        bench.choose_driver(8, {}, 0, "auto", loopback=True)
+
+
 def test_bench_exits_nonzero_when_gpus_exceed_devices():
     """--gpus above the visible device count exits 2 with a message before
     any data is generated (here: no GPU at all, or one on the box)."""

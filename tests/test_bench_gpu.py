@@ -39,3 +39,33 @@ def test_bench_ctx_driver(algo, partition, exchange):
     assert line["config"]["exchange"] == exchange
     assert line["ms_per_step"] > 0 and line["kernel_ms_max_over_ranks"] > 0
     assert line["ms_per_step"] >= line["kernel_ms_max_over_ranks"]
+
+
+@pytest.mark.parametrize("gpus,algo,partition,exchange", [
+    (2, "xsort", "cyclic", "allgather"),
+    (3, "csr5", "nnz", "allreduce"),
+    (8, "xsort", "cyclic", "allgather"),
+    (8, "rowsplit", "nnz", "allgather"),
+    (8, "csr5", "nnz", "allreduce"),
+    (4, "panel", "nnz", "allreduce"),
+])
+def test_bench_ctx_loopback(gpus, algo, partition, exchange):
+    """`bench.py --gpus N` through the ctx driver with N > 1 context ranks
+    wrapped onto the box's GPU (SBLAS_CTX_LOOPBACK: the collectives become
+    stream-ordered device copies / a rank-order sum instead of RCCL), so the
+    N > 1 partitions, split-row carries, cyclic placement, re-priming of the
+    next step's y and the per-device timing all run and are checked against
+    the oracle; every rank's y must be bit-identical."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--ctx-loopback", "--check",
+           "--nrows", "200000", "--steps", "2", "--warmup", "2", "--no-cpu-baseline", "--algo", algo,
+           "--partition", partition, "--exchange", exchange]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["check_vs_oracle"] is True, line
+    assert line["n_gpus"] == gpus and "loopback" in line["note"]
+    assert len(line["kernel_ms_per_device"]) == gpus
+    assert sum(line["nnz_per_device"]) == line["config"]["nnz"]

@@ -161,3 +161,36 @@ def test_cli_spmv_ctx(algo, partition, exchange):
     assert "ctx devices agree: PASS" in r.stdout
     assert "(RCCL): PASS" in r.stdout
     assert "ctx spmv: kernel" in r.stdout
+
+
+@pytest.mark.parametrize("g", [2, 3, 5])
+@pytest.mark.parametrize("algo", [1, 2, 5])
+@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
+def test_ctx_loopback_multi_rank(torch_cuda, sb, orc, monkeypatch, g, algo, partition, exchange):
+    """g > 1 context ranks on the one GPU (SBLAS_CTX_LOOPBACK=1: no RCCL, the
+    collectives are stream-ordered device copies): three chained steps, long
+    rows split across ranks by the nnz partition, every rank's y compared with
+    the oracle and with rank 0's bit for bit."""
+    monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    rng = np.random.default_rng(100 * g + 10 * algo + partition)
+    m, n = 6000, 9000
+    rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(2, 7000), (3000, 8000), (5999, 3000)])
+    x = rng.standard_normal(n)
+    y = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(g)
+    ctx.upload(m, n, rp, col, val, algo, partition, exchange)
+    ctx.set_x(x)
+    ctx.set_y(y)
+    for step in range(3):
+        st = ctx.spmv_ex(alpha, beta, delay_us=100.0 if step == 1 else 0.0)
+        assert st.shape == (3 + 3 * g,)
+        want = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+        bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y)
+        got = [ctx.get_y(d) for d in range(g)]
+        assert np.all(np.abs(got[0] - want) <= bound), (step, np.max(np.abs(got[0] - want) - bound))
+        for d in range(1, g):
+            assert np.array_equal(got[0], got[d]), (step, d)
+        y = got[0]
+    assert sum(ctx.slice_info(d)[1] for d in range(g)) == int(rp[-1])
+    ctx.close()
