@@ -239,6 +239,20 @@ int sblas_trsv_mgpu_solve_tasks(const int *colptr, const int *rowidx, const doub
                                 int n, int substitution, int rhs, const double *b, double *x,
                                 int ngpu, int tasks, int balance, double *solve_ms);
 
+/* Persistent form of the multi-GPU solve: create builds the blocks once
+ * (CSC -> CSR of L on the host, ngpu*tasks blocks of the solve order, block d
+ * on device d % ngpu, its rows and a fine-grained x uploaded); run uploads b
+ * (HOST n x rhs row-major), resets x and the control words, solves and copies
+ * x back (solve_ms: wall time of the kernels); repeated runs redo no O(nnz)
+ * host work.  The one-shot sblas_trsv_mgpu_solve* above are create + run +
+ * destroy. */
+typedef struct sblas_trsv_mgpu_s *sblas_trsv_mgpu;
+int sblas_trsv_mgpu_create(sblas_trsv_mgpu *out, const int *colptr, const int *rowidx,
+                           const double *val, int n, int substitution, int rhs, int ngpu,
+                           int tasks, int balance);
+int sblas_trsv_mgpu_run(sblas_trsv_mgpu h, const double *b, double *x, double *solve_ms);
+int sblas_trsv_mgpu_destroy(sblas_trsv_mgpu h);
+
 /* Multi-partition y assembly after an allgather of padded slices: partition
  * r's slice starts at d_gathered + r*stride; d_meta (DEVICE, 3*g ints) holds
  * {row0, nrows, cont} per partition; cont = first row continues partition

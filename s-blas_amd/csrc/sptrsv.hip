@@ -1070,9 +1070,13 @@ int sblas_trsv_destroy(sblas_trsv T)
 namespace {
 
 // Multi-device solve from HOST CSC (diagonal first / last per column as in the
-// reference).  Returns x on the host.  nblocks blocks of the solve order;
-// block d runs on ordinal (d % ndev) % count.  balance 0 = nnz-balanced
-// blocks (sptrsv_v1/v2's intent), 1 = equal row counts (sptrsv_v3's
+// reference), as a persistent handle: sblas_trsv_mgpu_create builds the
+// blocks once (CSC -> CSR of L, nnz-balanced blocks of the solve order, each
+// block's CSR rows uploaded to its device, fine-grained x per block), and
+// every sblas_trsv_mgpu_run only uploads b, resets x / the control words,
+// launches and copies x back.  nblocks blocks of the solve order; block d
+// runs on ordinal (d % ndev) % count.  balance 0 = nnz-balanced blocks
+// (sptrsv_v1/v2's intent), 1 = equal row counts (sptrsv_v3's
 // floor(d*m/(np*task)), sptrsv_v3/src/sptrsv_syncfree_cuda.h:276-300).
 // Every block has its own stream and all are launched before any is waited
 // for, so blocks that share a GPU run CONCURRENTLY like blocks on different
@@ -1081,18 +1085,74 @@ namespace {
 // waits for lower blocks, which were enqueued first on every hardware queue,
 // so streams sharing a queue cannot deadlock.  SBLAS_TRSV_MGPU_SERIAL=1 runs
 // the blocks of one device in order on one stream instead (A/B timing).
-static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *val, int n,
-                          int substitution, int rhs, const double *b, double *x, int nblocks,
-                          int ndev, int balance, double *solve_ms)
+struct TrsvMgpuDev {
+    int phys = 0;
+    int nloc = 0;
+    int *rowptr = nullptr, *col = nullptr;
+    double *val = nullptr, *b = nullptr;
+    unsigned long long *x = nullptr;
+    unsigned long long **xs = nullptr;
+    unsigned *ctl = nullptr;
+    std::vector<double> hb;  // staging of the block's b rows
+};
+
+}  // namespace
+
+struct sblas_trsv_mgpu_s {
+    int n = 0, rhs = 1, nblocks = 0, ndev = 0;
+    bool bwd = false, serial = false, trace = false;
+    std::vector<int> ob;                  // block boundaries in the solve order
+    std::vector<TrsvMgpuDev> D;
+    std::vector<hipStream_t> streams;     // per block (serial: per device's first block)
+    std::vector<int> on_phys, first_on;
+    hipStream_t stream_of(int d) const { return streams[serial ? first_on[D[d].phys] : d]; }
+};
+
+namespace {
+
+void trsv_mgpu_free(sblas_trsv_mgpu_s *H)
 {
-    if (n < 0 || nblocks <= 0 || ndev <= 0 || rhs <= 0 || !colptr || !b || !x) return SBLAS_ERR_INVALID;
+    for (auto &q : H->D) {
+        DeviceGuard g(q.phys);
+        (void)hipFree(q.rowptr);
+        (void)hipFree(q.col);
+        (void)hipFree(q.val);
+        (void)hipFree(q.b);
+        (void)hipFree(q.x);
+        (void)hipFree(q.xs);
+        (void)hipFree(q.ctl);
+    }
+    for (int d = 0; d < (int)H->streams.size(); ++d)
+        if (H->streams[d]) {
+            DeviceGuard g(H->D[d].phys);
+            (void)hipStreamDestroy(H->streams[d]);
+        }
+    delete H;
+}
+
+#define MG(expr)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error("trsv_mgpu: %s -> %s", #expr, hipGetErrorString(e_));    \
+            return SBLAS_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+
+int trsv_mgpu_build(sblas_trsv_mgpu_s *H, const int *colptr, const int *rowidx, const double *val, int n,
+                    int substitution, int rhs, int nblocks, int ndev, int balance)
+{
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SBLAS_ERR_NODEV;
     const int ngpu = nblocks;
-    const bool serial = getenv("SBLAS_TRSV_MGPU_SERIAL") && atoi(getenv("SBLAS_TRSV_MGPU_SERIAL")) != 0;
-    const bool trace = getenv("SBLAS_TRSV_TRACE") != nullptr;
+    H->n = n;
+    H->rhs = rhs;
+    H->nblocks = nblocks;
+    H->ndev = ndev;
+    H->serial = getenv("SBLAS_TRSV_MGPU_SERIAL") && atoi(getenv("SBLAS_TRSV_MGPU_SERIAL")) != 0;
+    H->trace = getenv("SBLAS_TRSV_TRACE") != nullptr;
     const int nnz = colptr[n];
-    const bool bwd = substitution == 1;
+    const bool bwd = H->bwd = substitution == 1;
     // CSC of L == CSR of L^T; stable transpose gives CSR of L with columns
     // ascending (diagonal last for lower, first for upper)
     std::vector<int> rp((size_t)n + 1, 0), cl((size_t)std::max(nnz, 1));
@@ -1110,7 +1170,8 @@ static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *va
     }
     // order index o -> row i; nnz-balanced blocks of the order
     auto row_of = [&](int o) { return bwd ? n - 1 - o : o; };
-    std::vector<int> ob(ngpu + 1, n);
+    std::vector<int> &ob = H->ob;
+    ob.assign((size_t)ngpu + 1, n);
     ob[0] = 0;
     if (balance == 1) {
         for (int d = 1; d < ngpu; ++d) ob[d] = (int)((long long)d * n / ngpu);
@@ -1124,57 +1185,22 @@ static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *va
         }
         for (; d < ngpu; ++d) ob[d] = n;
     }
-    struct Dev {
-        int phys;
-        int *rowptr = nullptr, *col = nullptr;
-        double *val = nullptr, *b = nullptr;
-        unsigned long long *x = nullptr;
-        unsigned long long **xs = nullptr;
-        unsigned *ctl = nullptr;
-    };
-    std::vector<Dev> D(ngpu);
-    std::vector<hipStream_t> streams(ngpu, nullptr);  // per block
-    int st = SBLAS_OK;
-    auto cleanup = [&]() {
-        for (auto &q : D) {
-            DeviceGuard g(q.phys);
-            (void)hipFree(q.rowptr);
-            (void)hipFree(q.col);
-            (void)hipFree(q.val);
-            (void)hipFree(q.b);
-            (void)hipFree(q.x);
-            (void)hipFree(q.xs);
-            (void)hipFree(q.ctl);
-        }
-        for (int d = 0; d < ngpu; ++d)
-            if (streams[d]) {
-                DeviceGuard g(D[d].phys);
-                (void)hipStreamDestroy(streams[d]);
-            }
-    };
-#define MG(expr)                                                               \
-    do {                                                                       \
-        hipError_t e_ = (expr);                                                \
-        if (e_ != hipSuccess) {                                                \
-            set_error("trsv_mgpu: %s -> %s", #expr, hipGetErrorString(e_));    \
-            cleanup();                                                         \
-            return SBLAS_ERR_HIP;                                              \
-        }                                                                      \
-    } while (0)
+    H->D.assign(ngpu, TrsvMgpuDev{});
+    H->streams.assign(ngpu, nullptr);
+    H->on_phys.assign(count, 0);
+    H->first_on.assign(count, -1);
     const int nphys = std::min(count, ndev);
-    std::vector<int> on_phys(count, 0), first_on(count, -1);
     for (int d = 0; d < ngpu; ++d) {
-        D[d].phys = (d % ndev) % count;
-        on_phys[D[d].phys]++;
-        if (first_on[D[d].phys] < 0) first_on[D[d].phys] = d;
+        H->D[d].phys = (d % ndev) % count;
+        H->on_phys[H->D[d].phys]++;
+        if (H->first_on[H->D[d].phys] < 0) H->first_on[H->D[d].phys] = d;
     }
     for (int d = 0; d < ngpu; ++d) {
         // serial mode: the blocks of one device share its first block's stream
-        if (serial && first_on[D[d].phys] != d) continue;
-        DeviceGuard g(D[d].phys);
-        MG(hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking));
+        if (H->serial && H->first_on[H->D[d].phys] != d) continue;
+        DeviceGuard g(H->D[d].phys);
+        MG(hipStreamCreateWithFlags(&H->streams[d], hipStreamNonBlocking));
     }
-    auto stream_of = [&](int d) { return streams[serial ? first_on[D[d].phys] : d]; };
     for (int p = 0; p < nphys; ++p) {
         DeviceGuard g(p);
         for (int q = 0; q < nphys; ++q) {
@@ -1189,11 +1215,11 @@ static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *va
     }
     std::vector<unsigned long long *> xs(ngpu);
     for (int d = 0; d < ngpu; ++d) {
-        Dev &q = D[d];
+        TrsvMgpuDev &q = H->D[d];
         DeviceGuard g(q.phys);
-        const int nloc = ob[d + 1] - ob[d];
+        const int nloc = q.nloc = ob[d + 1] - ob[d];
         std::vector<int> lrp((size_t)nloc + 1, 0), lcol;
-        std::vector<double> lval, lb((size_t)std::max(nloc, 1) * rhs);
+        std::vector<double> lval;
         for (int t = 0; t < nloc; ++t) {
             const int i = row_of(ob[d] + t);
             for (int e = rp[(size_t)i]; e < rp[(size_t)i + 1]; ++e) {
@@ -1201,8 +1227,8 @@ static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *va
                 lval.push_back(vl[(size_t)e]);
             }
             lrp[(size_t)t + 1] = (int)lcol.size();
-            for (int k = 0; k < rhs; ++k) lb[(size_t)t * rhs + k] = b[(size_t)i * rhs + k];
         }
+        q.hb.assign((size_t)std::max(nloc, 1) * rhs, 0.0);
         MG(hipMalloc(&q.rowptr, sizeof(int) * ((size_t)nloc + 1)));
         MG(hipMalloc(&q.col, sizeof(int) * std::max<size_t>(lcol.size(), 1)));
         MG(hipMalloc(&q.val, sizeof(double) * std::max<size_t>(lval.size(), 1)));
@@ -1216,69 +1242,109 @@ static int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *va
             MG(hipMemcpy(q.col, lcol.data(), sizeof(int) * lcol.size(), hipMemcpyHostToDevice));
             MG(hipMemcpy(q.val, lval.data(), sizeof(double) * lval.size(), hipMemcpyHostToDevice));
         }
-        if (nloc) MG(hipMemcpy(q.b, lb.data(), sizeof(double) * nloc * rhs, hipMemcpyHostToDevice));
         xs[d] = q.x;
     }
     for (int d = 0; d < ngpu; ++d) {
-        DeviceGuard g(D[d].phys);
-        MG(hipMemcpy(D[d].xs, xs.data(), sizeof(void *) * ngpu, hipMemcpyHostToDevice));
+        DeviceGuard g(H->D[d].phys);
+        MG(hipMemcpy(H->D[d].xs, xs.data(), sizeof(void *) * ngpu, hipMemcpyHostToDevice));
     }
-    // reset: sentinel x everywhere, zero control words
+    return SBLAS_OK;
+}
+
+int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solve_ms)
+{
+    const int ngpu = H->nblocks, n = H->n, rhs = H->rhs;
+    const bool bwd = H->bwd;
+    const std::vector<int> &ob = H->ob;
+    auto row_of = [&](int o) { return bwd ? n - 1 - o : o; };
+    // b rows of each block in its solve order; reset: sentinel x everywhere,
+    // zero control words
     for (int d = 0; d < ngpu; ++d) {
-        DeviceGuard g(D[d].phys);
-        hipStream_t s = stream_of(d);
-        fill_pending(D[d].x, (long long)n * rhs, s);
-        MG(hipMemsetAsync(D[d].ctl, 0, kCtlBytes, s));
+        TrsvMgpuDev &q = H->D[d];
+        DeviceGuard g(q.phys);
+        hipStream_t s = H->stream_of(d);
+        for (int t = 0; t < q.nloc; ++t) {
+            const int i = row_of(ob[d] + t);
+            for (int k = 0; k < rhs; ++k) q.hb[(size_t)t * rhs + k] = b[(size_t)i * rhs + k];
+        }
+        if (q.nloc)
+            MG(hipMemcpyAsync(q.b, q.hb.data(), sizeof(double) * q.nloc * rhs, hipMemcpyHostToDevice, s));
+        fill_pending(q.x, (long long)n * rhs, s);
+        MG(hipMemsetAsync(q.ctl, 0, kCtlBytes, s));
     }
     for (int d = 0; d < ngpu; ++d) {
-        DeviceGuard g(D[d].phys);
-        MG(hipStreamSynchronize(stream_of(d)));
+        DeviceGuard g(H->D[d].phys);
+        MG(hipStreamSynchronize(H->stream_of(d)));
     }
     const double t0 = sblas_get_time();
     for (int d = 0; d < ngpu; ++d) {
-        Dev &q = D[d];
+        TrsvMgpuDev &q = H->D[d];
         DeviceGuard g(q.phys);
-        const int nloc = ob[d + 1] - ob[d];
+        const int nloc = q.nloc;
         // co-resident blocks: the device's workgroup budget split between them
-        const int grid = serial ? grid_for(q.phys) : std::max(1, grid_for(q.phys) / on_phys[q.phys]);
+        const int grid = H->serial ? grid_for(q.phys) : std::max(1, grid_for(q.phys) / H->on_phys[q.phys]);
         if (nloc > 0 && rhs == 1) {
             TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
-            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, stream_of(d), P, q.ctl);
+            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, H->stream_of(d), P, q.ctl);
         } else if (nloc > 0) {
             TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0};
-            launch_trsm(P, q.ctl, grid, stream_of(d));
+            launch_trsm(P, q.ctl, grid, H->stream_of(d));
         }
         MG(hipGetLastError());
     }
     for (int d = 0; d < ngpu; ++d) {
-        DeviceGuard g(D[d].phys);
-        MG(hipStreamSynchronize(stream_of(d)));
+        DeviceGuard g(H->D[d].phys);
+        MG(hipStreamSynchronize(H->stream_of(d)));
     }
     if (solve_ms) *solve_ms = (sblas_get_time() - t0) * 1e3;
-    for (int d = 0; d < ngpu && st == SBLAS_OK; ++d) {
-        Dev &q = D[d];
+    for (int d = 0; d < ngpu; ++d) {
+        TrsvMgpuDev &q = H->D[d];
         DeviceGuard g(q.phys);
         unsigned h[kCtlBytes / 4] = {0};
         MG(hipMemcpy(h, q.ctl, kCtlBytes, hipMemcpyDeviceToHost));
         if (h[kAbort]) {
             set_error("trsv_mgpu: partition %d exceeded its spin limit", d);
-            st = SBLAS_ERR_HIP;
-            break;
+            return SBLAS_ERR_HIP;
         }
-        if (trace && ob[d + 1] > ob[d]) {  // debugging aid: block d's span on its device's clock
+        if (H->trace && q.nloc > 0) {  // debugging aid: block d's span on its device's clock
             const unsigned long long *h64 = (const unsigned long long *)h;
-            printf("trsv_block %d dev %d rows %d start_us %.3f end_us %.3f\n", d, q.phys,
-                   ob[d + 1] - ob[d], (double)(~0ULL - h64[kTStart64]) * 1e-2,
-                   (double)h64[kTEnd64] * 1e-2);
+            printf("trsv_block %d dev %d rows %d start_us %.3f end_us %.3f\n", d, q.phys, q.nloc,
+                   (double)(~0ULL - h64[kTStart64]) * 1e-2, (double)h64[kTEnd64] * 1e-2);
         }
         // x rows of this block: contiguous rows in row space
-        const int nloc = ob[d + 1] - ob[d];
-        if (nloc == 0) continue;
+        if (q.nloc == 0) continue;
         const size_t ia = (size_t)(bwd ? n - ob[d + 1] : ob[d]) * rhs;
-        MG(hipMemcpy(x + ia, (double *)q.x + ia, sizeof(double) * nloc * rhs, hipMemcpyDeviceToHost));
+        MG(hipMemcpy(x + ia, (double *)q.x + ia, sizeof(double) * q.nloc * rhs, hipMemcpyDeviceToHost));
     }
+    return SBLAS_OK;
+}
 #undef MG
-    cleanup();
+
+int trsv_mgpu_create(sblas_trsv_mgpu *out, const int *colptr, const int *rowidx, const double *val, int n,
+                     int substitution, int rhs, int nblocks, int ndev, int balance)
+{
+    if (!out || n < 0 || nblocks <= 0 || ndev <= 0 || rhs <= 0 || !colptr || (substitution != 0 && substitution != 1) ||
+        (balance != 0 && balance != 1))
+        return SBLAS_ERR_INVALID;
+    auto *H = new sblas_trsv_mgpu_s();
+    const int st = trsv_mgpu_build(H, colptr, rowidx, val, n, substitution, rhs, nblocks, ndev, balance);
+    if (st != SBLAS_OK) {
+        trsv_mgpu_free(H);
+        return st;
+    }
+    *out = H;
+    return SBLAS_OK;
+}
+
+// one-shot form: create, run once, destroy
+int trsv_mgpu_impl(const int *colptr, const int *rowidx, const double *val, int n, int substitution, int rhs,
+                   const double *b, double *x, int nblocks, int ndev, int balance, double *solve_ms)
+{
+    if (!b || !x) return SBLAS_ERR_INVALID;
+    sblas_trsv_mgpu H = nullptr;
+    SBLAS_TRY(trsv_mgpu_create(&H, colptr, rowidx, val, n, substitution, rhs, nblocks, ndev, balance));
+    const int st = trsv_mgpu_run(H, b, x, solve_ms);
+    trsv_mgpu_free(H);
     return st;
 }
 }  // namespace
@@ -1299,5 +1365,24 @@ int sblas_trsv_mgpu_solve_tasks(const int *colptr, const int *rowidx, const doub
     if (tasks <= 0 || ngpu <= 0 || (balance != 0 && balance != 1)) return SBLAS_ERR_INVALID;
     return trsv_mgpu_impl(colptr, rowidx, val, n, substitution, rhs, b, x, ngpu * tasks, ngpu,
                           balance, solve_ms);
+}
+
+int sblas_trsv_mgpu_create(sblas_trsv_mgpu *out, const int *colptr, const int *rowidx, const double *val,
+                           int n, int substitution, int rhs, int ngpu, int tasks, int balance)
+{
+    if (tasks <= 0 || ngpu <= 0) return SBLAS_ERR_INVALID;
+    return trsv_mgpu_create(out, colptr, rowidx, val, n, substitution, rhs, ngpu * tasks, ngpu, balance);
+}
+
+int sblas_trsv_mgpu_run(sblas_trsv_mgpu H, const double *b, double *x, double *solve_ms)
+{
+    if (!H || !b || !x) return SBLAS_ERR_INVALID;
+    return trsv_mgpu_run(H, b, x, solve_ms);
+}
+
+int sblas_trsv_mgpu_destroy(sblas_trsv_mgpu H)
+{
+    if (H) trsv_mgpu_free(H);
+    return SBLAS_OK;
 }
 }  // extern "C"

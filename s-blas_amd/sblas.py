@@ -103,6 +103,9 @@ _sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)
 _sig("sblas_coo_sortbyrow", _i, _i, _ll, _p, _p, _p, _p)
+_sig("sblas_trsv_mgpu_create", _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i)
+_sig("sblas_trsv_mgpu_run", _i, _p, _p, _p, _p)
+_sig("sblas_trsv_mgpu_destroy", _i, _p)
 _sig("sblas_ctx_create", _i, _p, _i, _p)
 _sig("sblas_ctx_destroy", _i, _p)
 _sig("sblas_ctx_ngpu", _i, _p, _p)
@@ -278,6 +281,42 @@ def trsv_mgpu_solve(colptr, rowidx, val, n: int, b, ngpu: int, substitution: int
                                     ptr(x), ngpu, C.byref(ms)), "trsv_mgpu_solve")
     x = x[:n * rhs]
     return (x if rhs == 1 else x.reshape(n, rhs)), ms.value
+
+
+class TrsvMgpu:
+    """Persistent multi-GPU sync-free solve (sblas_trsv_mgpu_create/run/
+    destroy): the blocks are built and uploaded once; each run uploads b and
+    solves."""
+
+    def __init__(self, colptr, rowidx, val, n: int, ngpu: int, substitution: int = 0, rhs: int = 1,
+                 tasks: int = 1, balance: int = 0):
+        self.h = C.c_void_p()
+        self.n, self.rhs = n, rhs
+        cp = np.ascontiguousarray(colptr, np.int32)
+        ri = np.ascontiguousarray(rowidx, np.int32)
+        v = np.ascontiguousarray(val, np.float64)
+        check(lib.sblas_trsv_mgpu_create(C.byref(self.h), ptr(cp), ptr(ri), ptr(v), n, substitution, rhs,
+                                         ngpu, tasks, balance), "trsv_mgpu_create")
+
+    def run(self, b):
+        """Returns (x, kernel ms)."""
+        bb = np.ascontiguousarray(b, np.float64)
+        x = np.zeros(max(self.n, 1) * self.rhs, np.float64)
+        ms = C.c_double(0.0)
+        check(lib.sblas_trsv_mgpu_run(self.h, ptr(bb), ptr(x), C.byref(ms)), "trsv_mgpu_run")
+        x = x[:self.n * self.rhs]
+        return (x if self.rhs == 1 else x.reshape(self.n, self.rhs)), ms.value
+
+    def close(self):
+        if self.h:
+            lib.sblas_trsv_mgpu_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def trsv_mgpu_solve_tasks(colptr, rowidx, val, n: int, b, ngpu: int, tasks: int,

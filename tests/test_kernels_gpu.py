@@ -528,6 +528,29 @@ def _block_spans(out):
     return [spans[d] for d in sorted(spans)]
 
 
+@pytest.mark.parametrize("blocks,rhs,sub", [(1, 1, 0), (4, 1, 0), (3, 1, 1), (4, 3, 0), (2, 5, 1)])
+def test_sptrsv_mgpu_persistent_handle(torch_cuda, sb, orc, blocks, rhs, sub):
+    """sblas_trsv_mgpu_create / run / destroy: blocks built once, then several
+    right-hand sides solved on the same handle; each x bit-identical to the
+    one-shot sblas_trsv_mgpu_solve and within 1e-12 of the reference's serial
+    executor (rhs 1)."""
+    n = 120_000
+    cp, ri, v, b0, xref = _banded_system(sb, n)
+    if sub == 1:  # the upper triangle: U = L^T (CSC of U = CSR of L), diagonal last
+        cp, ri, v = orc.transpose(n, n, cp, ri, v)
+    H = sb.TrsvMgpu(cp, ri, v, n, blocks, substitution=sub, rhs=rhs)
+    rng = np.random.default_rng(blocks * 10 + rhs)
+    for k in range(3):
+        b = rng.standard_normal(n * rhs) if k else np.tile(b0[:, None], (1, rhs)).ravel()
+        x, ms = H.run(b)
+        want, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, blocks, sub, rhs)
+        assert np.array_equal(x, want) and ms > 0.0
+        if rhs == 1:
+            ser = orc.sptrsv_serial(cp, ri, v, b, sub)
+            assert np.abs(x - ser).sum() / np.abs(ser).sum() <= 1e-12
+    H.close()
+
+
 @pytest.mark.parametrize("blocks", [2, 4])
 def test_sptrsv_blocks_run_concurrently(torch_cuda, sb, monkeypatch, capfd, blocks):
     """Blocks of the multi-device executor that wrap onto ONE GPU run at the
