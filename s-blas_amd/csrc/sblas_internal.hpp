@@ -224,6 +224,7 @@ struct XsArgs {
     int qstat[8];           // items per queue taken statically (block b: queue b%8, index b/8)
     int dynamic;            // items beyond the static share exist (claims needed)
     int sc1part;            // experiments: agent-scope partial stores without the fused reduce
+    int ntstore;            // y and partials written with non-temporal (streaming) stores
     int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
     int nrtasks;
     const int2 *rtasks;     // (range, first row) reduce tasks

@@ -644,6 +644,12 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                         const int r = ht + e * NT;
                         if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
+                } else if (a.ntstore) {
+#pragma unroll
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        if (r < R.nrows) __builtin_nontemporal_store(acc[r], out + r);
+                    }
                 } else {
 #pragma unroll
                     for (int e = 0; e < kEp; ++e) {
@@ -661,10 +667,19 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                         y0[e] = r < R.nrows ? yr[r] : 0.0;
                     }
                 }
+                if (a.ntstore) {
 #pragma unroll
-                for (int e = 0; e < kEp; ++e) {
-                    const int r = ht + e * NT;
-                    if (r < R.nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        if (r < R.nrows)
+                            __builtin_nontemporal_store(kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r], yr + r);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < kEp; ++e) {
+                        const int r = ht + e * NT;
+                        if (r < R.nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
+                    }
                 }
             }
         }
@@ -1268,6 +1283,11 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         return e ? atoi(e) : 0;
     }();
     a.sc1part = sc1part;
+    static const int ntstore = [] {
+        const char *e = getenv("SBLAS_XS_NTSTORE");
+        return e ? atoi(e) : 0;
+    }();
+    a.ntstore = ntstore;
     using K = void (*)(const XsArgs, const double *, double, double, double *);
     K kern;
     const bool b = beta != 0.0;
