@@ -269,6 +269,8 @@ struct XsPlan {
     int split = 8;               // waves of a pair's first team (of 16)
     bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
     int u = 1;                   // chunks per dynamic claim (planner; SBLAS_XS_U)
+    bool batch = false;          // small static items: k_spmv_xsort_batch (xsort.hip)
+    int maxc = 0;                // most chunks of one item (both sub-items)
     bool ready = false;
 };
 

@@ -696,6 +696,160 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     }
 }
 
+// Batch form for small items (a rank's slice at N = 8: ~5 chunks per wave).
+// The persistent kernel's per-wave chain -- claim, key/value load, dependent
+// x gather, LDS add, with two chunks in flight -- is repeated only a few
+// times per wave there, so its fill and drain dominate.  Here every item is
+// static (one per workgroup, the plan has no dynamic claims), the item's
+// chunks of both sub-items are listed once in LDS (chunk id, x offset of its
+// column group, team), and wave w takes entries w, w+16, ... in batches of
+// KB: all KB chunks' key/value loads are issued together, then all their
+// gathers, then the adds (into the owning team's LDS rows).  Same products
+// and epilogue as k_spmv_xsort.
+constexpr int kXsBatchKB = 4;       // chunks per batch and wave
+constexpr int kXsBatchMax = 16 * kXsBatchKB * 3;  // at most 3 batches per wave
+template <bool kBeta>
+__global__ __launch_bounds__(kXsThreads) void k_spmv_xsort_batch(const XsArgs a, const double *__restrict__ x,
+                                                                 double alpha, double beta,
+                                                                 double *__restrict__ y)
+{
+    constexpr int KB = kXsBatchKB;
+    constexpr int NT = kXsThreads / 2;  // threads of a team (epilogue)
+    __shared__ double acc_all[kXsRows];
+    __shared__ long long s_rec_all[2][128 + 5];
+    __shared__ int4 s_tab[kXsBatchMax];  // chunk id, x offset, team
+    __shared__ int s_seg[4][4];          // per segment: team, first group, groups, prefix
+    __shared__ int s_nc;
+    const int qb = (int)(blockIdx.x & 7), ib = (int)(blockIdx.x >> 3);
+    if (ib >= a.qstat[qb]) return;  // workgroup-uniform
+    const int slot = qb * a.qstride + ib;
+    const int xcc = a.use_xcc ? xs_xcc_id() : qb;
+    const int RL = a.G + 5;
+    for (int j = threadIdx.x; j < 2 * RL; j += kXsThreads) {
+        const int h = j / RL;
+        s_rec_all[h][j - h * RL] = a.xrec[(long long)(2 * slot + h) * RL + (j - h * RL)];
+    }
+    __syncthreads();
+    // zero the teams' rows; segments of the two sub-items (thread 0)
+    for (int h = 0; h < 2; ++h) {
+        const int sub = (int)s_rec_all[h][0];
+        const int nr = sub >= 0 ? (int)(s_rec_all[h][1] >> 32) : 0;
+        for (int r = threadIdx.x; r < nr; r += kXsThreads) acc_all[h * kXsHalfRows + r] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+        int ns = 0, tot = 0;
+        for (int h = 0; h < 2; ++h) {
+            const int sub = (int)s_rec_all[h][0];
+            if (sub < 0) continue;
+            const int k1 = sub & 255;
+            const long long *bo = s_rec_all[h] + 4;
+            const int g0 = k1 ? (k1 - 1) * a.q : xcc * a.q;
+            const int n1 = k1 ? a.q : a.G - g0;
+            // segment 1: groups [g0, g0 + n1); a narrow sub-item's segment 2: [0, g0)
+            const int sg[2][2] = {{g0, n1}, {0, k1 ? 0 : g0}};
+            for (int q = 0; q < 2; ++q) {
+                const int c = (int)(bo[sg[q][0] + sg[q][1]] - bo[sg[q][0]]);
+                if (sg[q][1] == 0 || c == 0) continue;
+                s_seg[ns][0] = h;
+                s_seg[ns][1] = sg[q][0];
+                s_seg[ns][2] = sg[q][1];
+                s_seg[ns][3] = tot;
+                tot += c;
+                ++ns;
+            }
+        }
+        for (int q = ns; q < 4; ++q) s_seg[q][3] = tot;
+        s_nc = tot;
+    }
+    __syncthreads();
+    const int C = s_nc;  // <= kXsBatchMax (planner)
+    for (int i = threadIdx.x; i < C; i += kXsThreads) {
+        int q = 0;
+        while (q < 3 && s_seg[q + 1][3] <= i) ++q;
+        const int h = s_seg[q][0], gs = s_seg[q][1], ng = s_seg[q][2];
+        const long long *bo = s_rec_all[h] + 4;
+        const long long cid = bo[gs] + (i - s_seg[q][3]);
+        int g = gs;
+        while (g + 1 < gs + ng && bo[g + 1] <= cid) ++g;
+        s_tab[i] = make_int4((int)cid, g * a.Wg, h, 0);
+    }
+    __syncthreads();
+    const v4u *key4 = reinterpret_cast<const v4u *>(a.key);
+    const v2d *val2 = reinterpret_cast<const v2d *>(a.val);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int b0 = wave; b0 < C; b0 += 16 * KB) {  // wave-uniform
+        v4u kk[KB];
+        v2d va[KB], vb[KB];
+        int xo[KB], tm[KB];
+        bool live[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int idx = b0 + 16 * u;
+            live[u] = idx < C;
+            const int4 t = s_tab[live[u] ? idx : b0];
+            const long long ci = t.x;
+            kk[u] = __builtin_nontemporal_load(key4 + ci * a.kstride + lane);
+            va[u] = __builtin_nontemporal_load(val2 + ci * a.vstride + lane);
+            vb[u] = __builtin_nontemporal_load(val2 + ci * a.vstride + 64 + lane);
+            xo[u] = t.y;
+            tm[u] = t.z;
+        }
+        double xx[KB][4];
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                xx[u][j] = x[k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits)];
+            }
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const double v[4] = {va[u].x, va[u].y, vb[u].x, vb[u].y};
+            double *acc = acc_all + tm[u] * kXsHalfRows;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = kk[u][j];
+                const double p = (live[u] && k != kXsPad) ? v[j] * xx[u][j] : 0.0;
+                atomicAdd(&acc[k & ((1u << kXsRowBits) - 1)], p);
+            }
+        }
+    }
+    __syncthreads();
+    // epilogue: team h's rows by the threads of half h (as k_spmv_xsort)
+    const int h = (int)(threadIdx.x >= (unsigned)NT);
+    const int ht = (int)threadIdx.x - h * NT;
+    const long long *rec = s_rec_all[h];
+    const int sub = (int)rec[0];
+    if (sub < 0) return;
+    const int k1 = sub & 255;
+    const int row0 = (int)(rec[1] & 0xffffffffLL), nrows = (int)(rec[1] >> 32);
+    const double *acc = acc_all + h * kXsHalfRows;
+    constexpr int kEp = kXsHalfRows / NT;
+    if (k1) {
+        double *out = a.partial + rec[2] + (long long)(k1 - 1) * nrows;
+#pragma unroll
+        for (int e = 0; e < kEp; ++e) {
+            const int r = ht + e * NT;
+            if (r < nrows) out[r] = acc[r];
+        }
+    } else {
+        double *yr = y + row0;
+        double y0[kEp];
+        if constexpr (kBeta) {
+#pragma unroll
+            for (int e = 0; e < kEp; ++e) {
+                const int r = ht + e * NT;
+                y0[e] = r < nrows ? yr[r] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kEp; ++e) {
+            const int r = ht + e * NT;
+            if (r < nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
+        }
+    }
+}
+
 // Wide ranges: y = alpha * sum_k partial[k] (+ beta*y), XCD slots in order.
 // All 8 partial loads (and y) of a row are issued before the first add.
 // wr[] holds the wide ranges' records in wide order: one scalar load ahead of
@@ -1164,6 +1318,26 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         nstat += P.qstat[k];
     }
     P.dynamic = nstat < P.nitems ? 1 : 0;
+    // batch form (k_spmv_xsort_batch, opt-in SBLAS_XS_BATCH=1) when every
+    // item is static and small.  Not the default: on rank 0's cyclic slice of
+    // config 2 it is slower than the persistent kernel (cold span N = 4: 54.8
+    // vs 50.4 us, N = 8: 39.0 vs 34.9; profiles/r03/xsort/slice_batch*.jsonl):
+    // issuing a wave's loads together leaves HBM idle during the gathers.
+    {
+        auto nch = [&](int sub) -> long long {
+            if (sub < 0) return 0;
+            const size_t i = (size_t)(sub >> 8) * G;
+            const int k1 = sub & 255;
+            return k1 ? blk[i + (size_t)k1 * P.q] - blk[i + (size_t)(k1 - 1) * P.q] : blk[i + G] - blk[i];
+        };
+        long long mc = 0;
+        for (int k = 0; k < 8; ++k)
+            for (const auto &it : q[k]) mc = std::max(mc, nch(it.first) + nch(it.second));
+        P.maxc = (int)std::min<long long>(mc, 1 << 30);
+        const char *be = getenv("SBLAS_XS_BATCH");
+        P.batch = be && atoi(be) != 0 && P.pair && P.nt == kXsThreads && !P.k24 && !P.dynamic &&
+                  mc <= kXsBatchMax;
+    }
     std::vector<int> qflat((size_t)16 * P.qstride, -1);
     for (int k = 0; k < 8; ++k)
         for (size_t j = 0; j < q[k].size(); ++j) {
@@ -1345,6 +1519,8 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;
     }
+    if (P.batch && !P.fused && mode == 0 && !trace_path)
+        kern = b ? k_spmv_xsort_batch<true> : k_spmv_xsort_batch<false>;
     std::vector<long long> htrace;
     if (trace_path) {
         const size_t len = 1 + (size_t)kXsTrace * (P.nitems + P.grid);

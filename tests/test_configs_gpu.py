@@ -86,6 +86,40 @@ def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
 
 
+@pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}], ids=["default", "batch"])
+def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world, rank, env):
+    """A rank's cyclic slice of config 2 (bench.py's N > 1 share) with the
+    persistent column-sorted kernel and its opt-in batch form (SBLAS_XS_BATCH=1,
+    taken where every item is static and small: N >= 4 here), three launches
+    on one plan against the oracle, and the beta = 0 form on a NaN-filled y."""
+    import sblas_dist
+    torch = torch_cuda
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rp, col, val = cfg2["rp"], cfg2["col"], cfg2["val"]
+    plan = sblas_dist.make_cyclic_plan(rp, N2, world)
+    lrp, lcol, lval = sblas_dist.cyclic_local_csr(rp, plan, rank, lambda a, b: (col[rp[a]:rp[b]], val[rp[a]:rp[b]]))
+    m = len(lrp) - 1
+    x = cfg2["xd"].cpu().numpy()
+    y0 = sb.gen_vector(m, 45)
+    alpha, beta = cfg2["alpha"], cfg2["beta"]
+    A = sb.DeviceCSR.upload(0, N2, lrp, lcol, lval)
+    try:
+        A.analyse(5)
+        for b in (beta, 0.0):
+            want = orc.csr_spmv_omp(lrp, lcol, lval, x, alpha, b, y0.copy())
+            bound = orc.spmv_bound(lrp, lcol, lval, x, alpha, b, y0)
+            for it in range(3 if b else 1):
+                yd = torch.from_numpy(y0).cuda() if b else torch.full((m,), float("nan"), dtype=torch.float64,
+                                                                      device="cuda")
+                A.spmv(5, alpha, cfg2["xd"].data_ptr(), b, yd.data_ptr())
+                torch.cuda.synchronize()
+                _check_spmv(want, bound, yd.cpu().numpy(), f"world {world} rank {rank} beta {b} launch {it}")
+    finally:
+        A.close()
+
+
 def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     """beta = 0 must not read y (y pre-filled with NaN): xsort, row split and
     CSR5."""
