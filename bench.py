@@ -24,8 +24,10 @@ beside it under `warm`.
   python bench.py [--gpus N --steps K --warmup W] [--algo auto|xsort|panel|rowsplit|csr5]
                   [--cache cold|warm] [--partition cyclic|nnz]
 
-Default kernel (`auto`): `xsort` while a rank holds >= 2M nonzeros (every N
-<= 8 on config 2, one-chunk claims), else `panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
+Default kernel (`auto`): the library's choice per rank slice (sblas_csr_pick):
+`rowsplit` where consecutive entries of a row share x lines (e.g. --cols prefix),
+else `xsort` while a rank holds >= 2M nonzeros (every N <= 8 on config 2), else
+`panel`.  `xsort` (csrc/xsort.hip) = entries sorted by column inside
 (row range x column group) blocks, column groups dealt to the XCDs so every
 x gather stays in the XCD's own L2, lane-consecutive gathers, LDS fp64 row
 accumulators.  Within the fp64 error bound of the sequential row sum but not
@@ -184,9 +186,7 @@ def run_ctx(args) -> int:
     t_gen = time.perf_counter() - t_gen
     exchange = sblas.CTX_ALLREDUCE if args.exchange == "allreduce" else sblas.CTX_ALLGATHER
     partition = 1 if (args.partition == "nnz" or exchange == sblas.CTX_ALLREDUCE) else 0
-    auto = args.algo == "auto"
-    if auto:
-        args.algo = "xsort" if nnz / N >= 2e6 and n * 8 <= 120 * 2**20 else "panel"
+    algo = sblas.AUTO if args.algo == "auto" else algo_ids[args.algo]
     # RCCL prints its version banner on stdout at communicator creation; the
     # contract's stdout is ONE JSON line, so fd 1 points at stderr meanwhile
     sys.stdout.flush()
@@ -199,14 +199,13 @@ def run_ctx(args) -> int:
         os.dup2(saved_fd, 1)
         os.close(saved_fd)
     t0 = time.perf_counter()
-    try:
-        ctx.upload(n, n, rowptr, col, val, algo_ids[args.algo], partition, exchange)
-    except sblas.SblasError:
-        if not (auto and args.algo == "xsort"):
-            raise
-        args.algo = "panel"
-        ctx.upload(n, n, rowptr, col, val, algo_ids[args.algo], partition, exchange)
+    ctx.upload(n, n, rowptr, col, val, algo, partition, exchange)
     plan_s = time.perf_counter() - t0
+    # AUTO: each device's slice decided by the library (sblas_csr_pick); the
+    # line names device 0's and lists all of them
+    names = {v: k for k, v in algo_ids.items()}
+    dev_algos = [names[ctx.slice_algo(d)] for d in range(N)]
+    args.algo = dev_algos[0]
     ctx.set_x(x_h)
     ctx.set_y(np.zeros(n))
     info = [ctx.slice_info(d) for d in range(N)]
@@ -316,6 +315,7 @@ def run_ctx(args) -> int:
         "algorithmic_bytes_per_launch": int(dev_bytes[0]),
         "algorithmic_bytes_all_ranks": int(sum(dev_bytes)),
         "nnz_per_device": [int(z) for _, z, _ in info],
+        "algo_per_device": dev_algos,
         "host_gen_s": round(t_gen, 2),
         "plan": {"upload_and_build_s": round(plan_s, 3)},
         "exchange_ms_max_over_ranks": round(xch_max, 5),
@@ -353,8 +353,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--algo", choices=["auto", "rowsplit", "csr5", "panel", "xsort"], default="auto",
-                    help="auto (default): xsort when a rank holds >= 2M nonzeros, else panel "
-                         "(s-blas_amd/tools/bench_slice.py: per-rank kernel times at N = 1..8)")
+                    help="auto (default): the library's per-slice choice (sblas_csr_pick): rowsplit "
+                         "for coalescing columns, else xsort from 2M nonzeros, else panel")
     ap.add_argument("--nrows", type=int, default=2_000_000)
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
@@ -437,17 +437,10 @@ def main() -> int:
     nnz = int(rowptr[-1])
     prefix = args.cols == "prefix"
     t_gen = time.perf_counter()
-    auto = args.algo == "auto"
-    if auto:
-        # the column-sorted kernel's per-item costs (padding to 256-entry
-        # chunks, item set-up) need a few chunks per wave: with one-chunk
-        # claims it wins at every N <= 8 on config 2 (slice cold spans
-        # 35.6 vs 42.8 us at N = 8, 51.3 vs 70.3 at N = 4), so
-        # the XCD-panel row split is kept for slices under ~2M nonzeros.  Its
-        # column groups cover at most 127 x 2^18 columns; past ~120 MiB of x
-        # the panel kernel is used as well.
-        args.algo = "xsort" if nnz / world >= 2e6 and n * 8 <= 120 * 2**20 else "panel"
-    algo = algo_ids[args.algo]
+    # auto: the library decides per rank slice (sblas_csr_pick: row split
+    # where consecutive entries share x lines, else xsort from ~2M nonzeros,
+    # else the XCD-panel row split; DESIGN.md §4 "Algorithm choice")
+    algo = sblas.AUTO if args.algo == "auto" else algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
         lrp, col, val = sblas_dist.cyclic_local_csr(
@@ -455,15 +448,8 @@ def main() -> int:
             lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, args.heavy, args.light,
                                               prefix=prefix, seed=42))
         t_gen = time.perf_counter() - t_gen
-        try:
-            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
-                                           overlap=args.overlap)
-        except sblas.SblasError:
-            if not (auto and algo == sblas.XSORT):
-                raise
-            args.algo, algo = "panel", sblas.PANEL  # the layout does not apply: fall back
-            op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
-                                           overlap=args.overlap)
+        op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
+                                       overlap=args.overlap)
         local_nnz = int(lrp[-1])
         partition = f"cyclic row chunks ({plan.chunk_rows} rows, {plan.nchunks} chunks)"
         if op.overlap:
@@ -481,6 +467,8 @@ def main() -> int:
                                  args.exchange)
         local_nnz = i1 - i0
         partition = "nnz-balanced (spMV_mgpu_v1)"
+    algo = op.algo  # resolved (AUTO: rank 0's slice decides the reported name)
+    args.algo = {v: k for k, v in algo_ids.items()}[algo]
     x_h = sblas.gen_vector(n, 43)
     x = torch.from_numpy(x_h).to(dev)
 

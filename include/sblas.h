@@ -37,6 +37,7 @@ typedef enum {
  * (spmv/test/dspmv_test.cu:80): 1 = csrmv (row split), 2 = csrmv_mp
  * (nnz-balanced), 3 = CSR5 (disabled in the reference, enabled here). */
 typedef enum {
+    SBLAS_SPMV_AUTO = 0,     /* chosen per handle by sblas_csr_pick (below) */
     SBLAS_SPMV_ROWSPLIT = 1, /* CSR-adaptive row blocks, wave64, LDS stream */
     SBLAS_SPMV_CSR5 = 2,     /* wave64 CSR5-style tiles, segmented sum */
     SBLAS_SPMV_CSR5_ALT = 3, /* same kernel as 2 */
@@ -148,6 +149,17 @@ int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x,
  * host's launch latency and event-record gaps.  Waits for the call. */
 int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
                      double beta, double *d_y, void *stream, float *ms);
+/* The algorithm SBLAS_SPMV_AUTO runs for this handle (decided once, cached;
+ * analyse / spmv / spmv_timed with SBLAS_SPMV_AUTO resolve through it).  A
+ * device probe measures column locality: over up to 65,536 sampled rows, the
+ * share of entries whose column is within 16 columns (one 128-B line of x)
+ * of the previous entry's.  >= 1/2 (e.g. the reference generator's
+ * contiguous columns, banded or blocked rows): ROWSPLIT, whose gathers then
+ * coalesce; otherwise XSORT when the handle holds >= 2M nonzeros and
+ * n*8 <= 120 MiB (its column groups), else PANEL.  If the XSORT analysis is
+ * unsupported for the matrix, sblas_csr_analyse falls back to PANEL and the
+ * choice becomes PANEL.  SBLAS_AUTO=<1..5> overrides the choice. */
+int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
 /* Device bytes held by the analysis of `algo` (free memory before - after
  * sblas_csr_analyse; 0 if not analysed): the layout's cost beside the CSR. */
 long long sblas_csr_plan_bytes(sblas_csr A, int algo);
@@ -311,6 +323,9 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx ctx, int m, int n, const long long *row
  * launch with beta != 0 (sblas_spmv_algorithmic_bytes).  Any may be NULL. */
 int sblas_ctx_slice_info(sblas_ctx ctx, int d, long long *rows, long long *nnz,
                          long long *alg_bytes_beta);
+/* The SpMV algorithm device d's slice runs (its own sblas_csr_pick when the
+ * context was loaded with SBLAS_SPMV_AUTO). */
+int sblas_ctx_slice_algo(sblas_ctx ctx, int d, int *algo);
 int sblas_ctx_set_x(sblas_ctx ctx, const double *x); /* host x -> every device */
 int sblas_ctx_set_y(sblas_ctx ctx, const double *y); /* host y (beta input) */
 /* y = alpha*A*x + beta*y on every device; afterwards each device holds the

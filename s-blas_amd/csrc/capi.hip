@@ -192,12 +192,118 @@ int sblas_csr_info(sblas_csr A, int *m, int *n, long long *nnz)
     return SBLAS_OK;
 }
 
+namespace {
+// SBLAS_SPMV_AUTO's locality probe: one wave per sampled row (rows
+// w*m/S, S <= 65536), at most its first 1024 entries; counts the entries
+// whose column lies within 16 columns (one 128-B line of x) of the previous
+// entry's.  cnt = {adjacent, counted}.
+__global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ rowptr,
+                                                       const int *__restrict__ col, int m, int S,
+                                                       unsigned long long *cnt)
+{
+    const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const int lane = threadIdx.x & 63;
+    if (w >= S) return;  // wave-uniform
+    const int r = (int)((long long)w * m / S);
+    const int a = rowptr[r];
+    const int b = min(rowptr[r + 1], a + 1024);
+    unsigned adj = 0, tot = 0;
+    for (int e = a + 1 + lane; e < b; e += 64) {
+        const int d = col[e] - col[e - 1];
+        adj += (d > -16 && d < 16) ? 1u : 0u;
+        ++tot;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        adj += __shfl_down(adj, o, 64);
+        tot += __shfl_down(tot, o, 64);
+    }
+    if (lane == 0 && tot) {
+        atomicAdd(&cnt[0], (unsigned long long)adj);
+        atomicAdd(&cnt[1], (unsigned long long)tot);
+    }
+}
+
+constexpr long long kAutoXsortMinNnz = 2000000;  // bench slices: xsort leads from ~2M nnz
+
+int pick_algo(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.auto_algo) return A.auto_algo;
+    double adj = 0.0;
+    const int S = (int)std::min<long long>(A.m, 65536);
+    if (S > 0 && A.nnz > A.m) {
+        unsigned long long *d = nullptr, h[2] = {0, 0};
+        hipError_t e = hipMalloc(&d, sizeof(h));
+        if (e == hipSuccess) e = hipMemsetAsync(d, 0, sizeof(h), s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_col_adjacency, dim3((S + 3) / 4), dim3(256), 0, s, A.rowptr, A.col, A.m, S, d);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (d) (void)hipFree(d);
+        if (e != hipSuccess) {
+            set_error("sblas_csr_pick: %s", hipGetErrorString(e));
+            return -SBLAS_ERR_HIP;
+        }
+        adj = h[1] ? (double)h[0] / (double)h[1] : 0.0;
+    }
+    A.col_adjacency = adj;
+    int algo;
+    if (adj >= 0.5) algo = SBLAS_SPMV_ROWSPLIT;
+    else if (A.nnz >= kAutoXsortMinNnz && (long long)A.n * 8 <= (120LL << 20)) algo = SBLAS_SPMV_XSORT;
+    else algo = SBLAS_SPMV_PANEL;
+    if (const char *o = getenv("SBLAS_AUTO")) {
+        const int v = atoi(o);
+        if (v >= SBLAS_SPMV_ROWSPLIT && v <= SBLAS_SPMV_XSORT) algo = v;
+    }
+    A.auto_algo = algo;
+    return algo;
+}
+
+// algo, or AUTO resolved (negative: -status)
+int resolve_algo(sblas_csr_s &A, int algo, hipStream_t s)
+{
+    return algo == SBLAS_SPMV_AUTO ? pick_algo(A, s) : algo;
+}
+
+bool plan_ready(const sblas_csr_s &A, int algo)
+{
+    switch (algo) {
+    case SBLAS_SPMV_ROWSPLIT: return A.rs.ready;
+    case SBLAS_SPMV_CSR5:
+    case SBLAS_SPMV_CSR5_ALT: return A.c5.ready;
+    case SBLAS_SPMV_PANEL: return A.pn.ready;
+    case SBLAS_SPMV_XSORT: return A.xs.ready;
+    default: return false;
+    }
+}
+} // namespace
+
+int sblas_csr_pick(sblas_csr A, void *stream, int *algo)
+{
+    if (!A || !algo) return SBLAS_ERR_INVALID;
+    DeviceGuard g(A->device);
+    const int a = pick_algo(*A, (hipStream_t)stream);
+    if (a < 0) return -a;
+    *algo = a;
+    return SBLAS_OK;
+}
+
 int sblas_csr_analyse(sblas_csr A, int algo, void *stream)
 {
     if (!A) return SBLAS_ERR_INVALID;
     DeviceGuard g(A->device);
     hipStream_t s = (hipStream_t)stream;
+    const bool auto_pick = algo == SBLAS_SPMV_AUTO;
+    algo = resolve_algo(*A, algo, s);
+    if (algo < 0) return -algo;
     if (algo < SBLAS_SPMV_ROWSPLIT || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
+    if (auto_pick && algo == SBLAS_SPMV_XSORT) {
+        const int st = sblas_csr_analyse(A, SBLAS_SPMV_XSORT, stream);
+        if (st != SBLAS_ERR_UNSUPPORTED) return st;
+        A->auto_algo = SBLAS_SPMV_PANEL;  // the column groups do not apply to this matrix
+        algo = SBLAS_SPMV_PANEL;
+    }
     // device bytes the plan holds: free memory before - after (the builders
     // synchronise before returning)
     size_t f0 = 0, f1 = 0, tot = 0;
@@ -227,6 +333,10 @@ int sblas_spmv(sblas_csr A, int algo, double alpha, const double *d_x, double be
     if (!A || (!d_x && A->nnz) || (!d_y && A->m)) return SBLAS_ERR_INVALID;
     DeviceGuard g(A->device);
     hipStream_t s = (hipStream_t)stream;
+    if (algo == SBLAS_SPMV_AUTO) {  // resolve (and analyse, with its fallback) once
+        if (!A->auto_algo || !plan_ready(*A, A->auto_algo)) SBLAS_TRY(sblas_csr_analyse(A, SBLAS_SPMV_AUTO, stream));
+        algo = A->auto_algo;
+    }
     switch (algo) {
     case SBLAS_SPMV_ROWSPLIT:
         if (!A->rs.ready) SBLAS_TRY(build_rowsplit_plan(*A, s));
@@ -256,6 +366,10 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x, dou
     DeviceGuard g(A->device);
     // build any plan first, untimed (the plan build launches its own kernels)
     hipStream_t s = (hipStream_t)stream;
+    if (algo == SBLAS_SPMV_AUTO) {  // resolve (and analyse, with its fallback) once
+        if (!A->auto_algo || !plan_ready(*A, A->auto_algo)) SBLAS_TRY(sblas_csr_analyse(A, SBLAS_SPMV_AUTO, stream));
+        algo = A->auto_algo;
+    }
     switch (algo) {
     case SBLAS_SPMV_ROWSPLIT: if (!A->rs.ready) SBLAS_TRY(build_rowsplit_plan(*A, s)); break;
     case SBLAS_SPMV_CSR5:

@@ -362,7 +362,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
                                const double *val, int algo, int partition, int exchange)
 {
     if (!C || m < 0 || n < 0 || !rowptr || (partition != 0 && partition != 1)) return SBLAS_ERR_INVALID;
-    if (algo < SBLAS_SPMV_ROWSPLIT || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
+    if (algo < SBLAS_SPMV_AUTO || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
     if (exchange != SBLAS_CTX_ALLGATHER && exchange != SBLAS_CTX_ALLREDUCE) return SBLAS_ERR_INVALID;
     if (exchange == SBLAS_CTX_ALLREDUCE && partition != 1) {
         set_error("sblas_ctx_matrix_upload: the allreduce exchange needs the nnz partition (1): each "
@@ -488,6 +488,16 @@ int sblas_ctx_slice_info(sblas_ctx C, int d, long long *rows, long long *nnz, lo
     if (nnz) *nnz = C->lnnz[d];
     if (alg_bytes_beta) *alg_bytes_beta = sblas_spmv_algorithmic_bytes(C->A[d], 1);
     return SBLAS_OK;
+}
+
+int sblas_ctx_slice_algo(sblas_ctx C, int d, int *algo)
+{
+    if (!C || !C->loaded || d < 0 || d >= C->g || !algo) return SBLAS_ERR_INVALID;
+    if (C->algo != SBLAS_SPMV_AUTO) {
+        *algo = C->algo;
+        return SBLAS_OK;
+    }
+    return sblas_csr_pick(C->A[d], C->st[d], algo);
 }
 
 int sblas_ctx_set_x(sblas_ctx C, const double *x)

@@ -307,6 +307,8 @@ struct sblas_csr_s {
     mutable double *spmm_part = nullptr;
     mutable size_t spmm_part_bytes = 0;
     long long plan_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device bytes per algorithm's plan
+    int auto_algo = 0;          // SBLAS_SPMV_AUTO's choice (capi.hip pick_algo), 0 = not yet
+    double col_adjacency = -1;  // its locality probe
 };
 
 namespace sblas {

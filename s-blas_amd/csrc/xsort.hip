@@ -128,7 +128,10 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 // past c1 loads one line (every lane the same address) and adds exact +0.0;
 // padding entries add +0.0 too (a select, not a product: x may be inf/nan).
 // kMode (timing experiments only, SBLAS_XS_MODE): 0 = the product kernel,
-// bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0].
+// bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0],
+// bit 3 (xs_stream_dyn only) = no gather at all (a key-derived constant),
+// bit 4 (xs_stream_dyn only) = gathers folded into x[0, 65536) (same lane
+// pattern, an L2-resident 512 KiB: separates L2 fills from L2 requests).
 template <int kMode, int S>
 __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
                                           const v2d *__restrict__ val2, int ks, int vs, long long c0,
@@ -252,7 +255,7 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
             for (int j = 0; j < 4; ++j) {
                 const uint32_t k = kk[u][j];
                 const int idx = k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits);
-                xx[u][j] = x[(kMode & 2) ? 0 : idx];
+                xx[u][j] = (kMode & 8) ? (double)(k & 1) : x[(kMode & 2) ? 0 : (kMode & 16) ? (idx & 0xffff) : idx];
             }
     };
     auto accumulate = [&](long long cb, const v4u *kk, const v2d *va, const v2d *vb,
@@ -1486,13 +1489,15 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     const int xu = P.u;  // chunks per dynamic claim (planner; SBLAS_XS_U)
     if (P.pair && P.dyn && !b && xu == 1 && mode == 0)
         kern = k_spmv_xsort<false, 0, W, true, 8, false, true, 1>;
-    if (P.pair && P.dyn && b && (xu != kXsUnroll || (mode & 4))) {
+    if (P.pair && P.dyn && b && (xu != kXsUnroll || (mode & 28))) {
 #define XS_DYN(M, U) k_spmv_xsort<true, M, W, true, 8, false, true, U>
         const int mm = mode & 6;
         if (xu == 1) kern = mm == 0 ? XS_DYN(0, 1) : mm == 2 ? XS_DYN(2, 1) : mm == 4 ? XS_DYN(4, 1) : XS_DYN(6, 1);
         else if (xu == 3) kern = mm == 0 ? XS_DYN(0, 3) : mm == 2 ? XS_DYN(2, 3) : mm == 4 ? XS_DYN(4, 3) : XS_DYN(6, 3);
         else if (xu == 4) kern = mm == 0 ? XS_DYN(0, 4) : mm == 2 ? XS_DYN(2, 4) : mm == 4 ? XS_DYN(4, 4) : XS_DYN(6, 4);
         else kern = mm == 4 ? XS_DYN(4, 2) : XS_DYN(6, 2);
+        if ((mode & ~1) == 8 && xu == 1) kern = (mode & 1) ? XS_DYN(9, 1) : XS_DYN(8, 1);  // experiment: no gathers
+        if (mode == 16 && xu == 1) kern = XS_DYN(16, 1);  // experiment: L2-resident gathers
 #undef XS_DYN
     }
     if (P.k24) {  // 24-bit keys: the paired dynamic kernel only (planner)

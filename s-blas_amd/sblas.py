@@ -22,6 +22,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # builds on one box); the default is the in-tree build
 LIB_PATH = os.environ.get("SBLAS_LIB") or os.path.join(_HERE, "libsblas.so")
 
+AUTO = 0      # chosen per handle (sblas_csr_pick: column-locality probe)
 ROWSPLIT = 1  # test_spmv kernel 1 (csrmv)
 CSR5 = 2      # test_spmv kernel 2/3 (csrmv_mp / CSR5)
 PANEL = 4     # XCD-affine column panels (row-split per panel + reduce)
@@ -81,6 +82,7 @@ _sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
 _sig("sblas_spmv_timed", _i, _p, _i, C.c_double, _p, C.c_double, _p, _p, _p)
 _sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
 _sig("sblas_csr_plan_bytes", _ll, _p, _i)
+_sig("sblas_csr_pick", _i, _p, _p, _p)
 _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
 _sig("sblas_csr_transpose", _i, _p, _p, _p, _p, _p)
 _sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
@@ -115,6 +117,7 @@ _sig("sblas_ctx_set_y", _i, _p, _p)
 _sig("sblas_ctx_spmv", _i, _p, _d, _d, _p)
 _sig("sblas_ctx_matrix_upload_ex", _i, _p, _i, _i, _p, _p, _p, _i, _i, _i)
 _sig("sblas_ctx_slice_info", _i, _p, _i, _p, _p, _p)
+_sig("sblas_ctx_slice_algo", _i, _p, _i, _p)
 _sig("sblas_ctx_spmv_ex", _i, _p, _d, _d, _d, _i, _p)
 _sig("sblas_ctx_sync", _i, _p, _p)
 _sig("sblas_ctx_get_y", _i, _p, _i, _p)
@@ -449,6 +452,12 @@ class DeviceCSR:
         check(lib.sblas_csr_transpose(self.h, colptr_ptr, rowidx_ptr, cval_ptr, stream),
               "csr_transpose")
 
+    def pick(self, stream=None) -> int:
+        """The algorithm AUTO runs on this handle (sblas_csr_pick)."""
+        a = C.c_int()
+        check(lib.sblas_csr_pick(self.h, stream, C.byref(a)), "csr_pick")
+        return a.value
+
     def plan_bytes(self, algo: int) -> int:
         """Device bytes the algorithm's analysis holds beside the CSR."""
         return int(lib.sblas_csr_plan_bytes(self.h, algo))
@@ -498,6 +507,12 @@ class DeviceCtx:
         r, z, b = C.c_longlong(), C.c_longlong(), C.c_longlong()
         check(lib.sblas_ctx_slice_info(self.h, d, C.byref(r), C.byref(z), C.byref(b)), "ctx_slice_info")
         return r.value, z.value, b.value
+
+    def slice_algo(self, d: int) -> int:
+        """The SpMV algorithm device d's slice runs (resolved when AUTO)."""
+        a = C.c_int()
+        check(lib.sblas_ctx_slice_algo(self.h, d, C.byref(a)), "ctx_slice_algo")
+        return a.value
 
     def spmv_ex(self, alpha: float, beta: float, delay_us: float = 0.0, wait: bool = True):
         """Timing form (sblas_ctx_spmv_ex).  Returns the 3 + 3g stats (ms) when

@@ -83,6 +83,8 @@ class DistSpMV:
         self.A = sblas.DeviceCSR(h.value)
         t0 = time.perf_counter()
         self.A.analyse(algo)
+        if algo == sblas.AUTO:  # the library's choice for this slice (sblas_csr_pick)
+            self.algo = algo = self.A.pick()
         self.plan_s = time.perf_counter() - t0
         self.dm = r1 - r0
         stride = plan.stride
@@ -237,6 +239,8 @@ class DistSpMVCyclic:
         self.A = sblas.DeviceCSR.upload(device, plan.n, lrp64, col, val)
         t0 = time.perf_counter()
         self.A.analyse(algo)
+        if algo == sblas.AUTO:  # the library's choice for this slice (sblas_csr_pick)
+            self.algo = algo = self.A.pick()
         self.plan_s = time.perf_counter() - t0
         f64 = torch.float64
         self.y_local = torch.zeros(plan.stride, dtype=f64, device=dev)

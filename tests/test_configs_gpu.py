@@ -120,6 +120,18 @@ def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world,
         A.close()
 
 
+def test_config2_auto(torch_cuda, sb, cfg2):
+    """SBLAS_SPMV_AUTO on config 2: xsort for random columns, the row split
+    for the reference generator's contiguous (prefix) columns; y against the
+    oracle."""
+    A = sb.DeviceCSR.upload(0, N2, cfg2["rp"], cfg2["col"], cfg2["val"])
+    try:
+        assert A.pick() == (sb.ROWSPLIT if cfg2["prefix"] else sb.XSORT)
+    finally:
+        A.close()
+    _run_cfg2(torch_cuda, sb, cfg2, sb.AUTO)
+
+
 def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     """beta = 0 must not read y (y pre-filled with NaN): xsort, row split and
     CSR5."""

@@ -29,7 +29,7 @@ def rand_csr(rng, m, n, maxlen, long_rows=()):
     return rp, col, rng.standard_normal(int(rp[-1]))
 
 
-@pytest.mark.parametrize("algo", [1, 2, 4, 5])
+@pytest.mark.parametrize("algo", [0, 1, 2, 4, 5])
 @pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
 def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition, exchange):
     """Two chained steps (the second's beta input is the first's y, kept on
@@ -43,6 +43,8 @@ def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition, exchange):
     alpha, beta = orc.alpha_beta()
     ctx = sb.DeviceCtx(1)
     ctx.upload(m, n, rp, col, val, algo, partition, exchange)
+    # AUTO resolves per slice (scattered columns, < 2M nonzeros: panel)
+    assert ctx.slice_algo(0) == (algo if algo else sb.PANEL)
     ctx.set_x(x)
     ctx.set_y(y0)
     k, xch, tot = ctx.spmv(alpha, beta)
@@ -57,7 +59,7 @@ def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition, exchange):
     ctx.close()
 
 
-@pytest.mark.parametrize("algo", [2, 5])
+@pytest.mark.parametrize("algo", [0, 2, 5])
 def test_ctx_config2_full_size(torch_cuda, sb, orc, algo):
     n = 2_000_000
     rp = sb.gen_synth_rowptr(n)
@@ -67,6 +69,7 @@ def test_ctx_config2_full_size(torch_cuda, sb, orc, algo):
     alpha, beta = orc.alpha_beta()
     ctx = sb.DeviceCtx(1)
     ctx.upload(n, n, rp, col, val, algo, 0)
+    assert ctx.slice_algo(0) == (algo if algo else sb.XSORT)
     ctx.set_x(x)
     ctx.set_y(y0)
     ctx.spmv(alpha, beta)

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 # with each other), and PAIR=0 runs one sub-item per workgroup.  Q = 2 / 3
 # column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
 # cover the wide sub-items' group ranges and the narrow wrap at q > 1.
-ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
+ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "3"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "8"}),
          (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
@@ -38,7 +38,7 @@ ALGOS = [(1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K24": "0"}),
          (5, {"SBLAS_XS_BATCH": "1"}), (5, {"SBLAS_XS_BATCH": "1", "SBLAS_XS_ALLWIDE": "1"})]
-ALGO_IDS = ["rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
+ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_k24", "xsort_k24_w50", "xsort_k24_q3_w50", "xsort_k24_u2_w50", "xsort_k32",
@@ -268,3 +268,49 @@ def test_spmv_out_of_core(torch_cuda, sb, orc, chunk, nstreams, ngpu, beta_zero)
                      nstreams=nstreams)
     assert st["chunks"] == max(1, -(-int(rp[-1]) // min(chunk, 1 << 30)))
     check(orc, rp, col, val, x, alpha, beta, y0, y)
+
+
+@pytest.mark.parametrize("case", ["random_small", "prefix", "banded_runs", "override"])
+def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
+    """SBLAS_SPMV_AUTO (sblas_csr_pick): coalescing columns -> row split;
+    scattered columns under 2M nonzeros -> panel; SBLAS_AUTO overrides.  The
+    resolved algorithm's analysis is built by analyse(AUTO) and spmv(AUTO)
+    matches the oracle."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    if case == "prefix":
+        rp, col, val = orc.gen_synth(n, prefix=True)
+        want_algo = sb.ROWSPLIT
+    elif case == "banded_runs":
+        # rows of 3 runs of 8 consecutive columns in three disjoint bands
+        lens = np.full(n, 24, np.int64)
+        rp = np.zeros(n + 1, np.int64)
+        rp[1:] = np.cumsum(lens)
+        starts = np.stack([np.arange(n) % 5990, 6000 + np.arange(n) % 5990, 12000 + np.arange(n) % 7990], 1)
+        col = (starts[:, :, None] + np.arange(8)[None, None, :]).reshape(-1).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+        want_algo = sb.ROWSPLIT
+    else:
+        rp, col, val = orc.gen_synth(n)
+        want_algo = sb.PANEL
+    if case == "override":
+        monkeypatch.setenv("SBLAS_AUTO", "2")
+        want_algo = sb.CSR5
+    x = orc.gen_vector(n, 43)
+    alpha, beta = orc.alpha_beta()
+    y0 = orc.gen_vector(n, 44)
+    A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    try:
+        assert A.pick() == want_algo
+        xd = torch_cuda.from_numpy(x).cuda()
+        yd = torch_cuda.from_numpy(y0.copy()).cuda()
+        A.spmv(sb.AUTO, alpha, xd.data_ptr(), beta, yd.data_ptr())  # analyses on first use
+        torch_cuda.cuda.synchronize()
+        assert A.plan_bytes(want_algo) >= 0
+        check(orc, rp, col, val, x, alpha, beta, y0, yd.cpu().numpy())
+        yd2 = torch_cuda.from_numpy(y0.copy()).cuda()
+        ms = A.spmv_timed(sb.AUTO, alpha, xd.data_ptr(), beta, yd2.data_ptr())
+        assert ms > 0
+        check(orc, rp, col, val, x, alpha, beta, y0, yd2.cpu().numpy())
+    finally:
+        A.close()
