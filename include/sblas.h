@@ -153,7 +153,7 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
  * analyse / spmv / spmv_timed with SBLAS_SPMV_AUTO resolve through it).  A
  * device probe measures column locality: over up to 65,536 sampled rows, the
  * share of entries whose column is within 16 columns (one 128-B line of x)
- * of the previous entry's.  >= 1/2 (e.g. the reference generator's
+ * of the previous entry's (the previous row's last, for a row's first).  >= 1/2 (e.g. the reference generator's
  * contiguous columns, banded or blocked rows): ROWSPLIT, whose gathers then
  * coalesce; otherwise XSORT when the handle holds >= 2M nonzeros and
  * n*8 <= 120 MiB (its column groups), else PANEL.  If the XSORT analysis is

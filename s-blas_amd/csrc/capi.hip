@@ -196,7 +196,9 @@ namespace {
 // SBLAS_SPMV_AUTO's locality probe: one wave per sampled row (rows
 // w*m/S, S <= 65536), at most its first 1024 entries; counts the entries
 // whose column lies within 16 columns (one 128-B line of x) of the previous
-// entry's.  cnt = {adjacent, counted}.
+// entry's -- for a row's first entry, the previous row's last (lanes of the
+// row split read neighbouring rows together, so a diagonal counts as local).
+// cnt = {adjacent, counted}.
 __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ rowptr,
                                                        const int *__restrict__ col, int m, int S,
                                                        unsigned long long *cnt)
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ r
     const int a = rowptr[r];
     const int b = min(rowptr[r + 1], a + 1024);
     unsigned adj = 0, tot = 0;
-    for (int e = a + 1 + lane; e < b; e += 64) {
+    for (int e = max(a, 1) + lane; e < b; e += 64) {
         const int d = col[e] - col[e - 1];
         adj += (d > -16 && d < 16) ? 1u : 0u;
         ++tot;
@@ -230,7 +232,7 @@ int pick_algo(sblas_csr_s &A, hipStream_t s)
     if (A.auto_algo) return A.auto_algo;
     double adj = 0.0;
     const int S = (int)std::min<long long>(A.m, 65536);
-    if (S > 0 && A.nnz > A.m) {
+    if (S > 0 && A.nnz > 1) {
         unsigned long long *d = nullptr, h[2] = {0, 0};
         hipError_t e = hipMalloc(&d, sizeof(h));
         if (e == hipSuccess) e = hipMemsetAsync(d, 0, sizeof(h), s);

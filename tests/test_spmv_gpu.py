@@ -270,7 +270,7 @@ def test_spmv_out_of_core(torch_cuda, sb, orc, chunk, nstreams, ngpu, beta_zero)
     check(orc, rp, col, val, x, alpha, beta, y0, y)
 
 
-@pytest.mark.parametrize("case", ["random_small", "prefix", "banded_runs", "override"])
+@pytest.mark.parametrize("case", ["random_small", "prefix", "banded_runs", "diagonal", "override"])
 def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
     """SBLAS_SPMV_AUTO (sblas_csr_pick): coalescing columns -> row split;
     scattered columns under 2M nonzeros -> panel; SBLAS_AUTO overrides.  The
@@ -289,6 +289,11 @@ def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
         starts = np.stack([np.arange(n) % 5990, 6000 + np.arange(n) % 5990, 12000 + np.arange(n) % 7990], 1)
         col = (starts[:, :, None] + np.arange(8)[None, None, :]).reshape(-1).astype(np.int32)
         val = rng.standard_normal(int(rp[-1]))
+        want_algo = sb.ROWSPLIT
+    elif case == "diagonal":  # one entry per row: locality across rows
+        rp = np.arange(n + 1, dtype=np.int64)
+        col = np.arange(n, dtype=np.int32)
+        val = rng.standard_normal(n)
         want_algo = sb.ROWSPLIT
     else:
         rp, col, val = orc.gen_synth(n)
