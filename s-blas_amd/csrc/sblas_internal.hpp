@@ -226,6 +226,7 @@ struct XsArgs {
     int sc1part;            // experiments: agent-scope partial stores without the fused reduce
     int ntstore;            // y and partials written with non-temporal (streaming) stores
     int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
+    int tail;               // wide ranges reduced by their last-arriving sub-item (xs_tail_reduce)
     int nrtasks;
     const int2 *rtasks;     // (range, first row) reduce tasks
     unsigned *arrive;       // per wide range: sub-items counted in, cumulative
@@ -259,6 +260,7 @@ struct XsPlan {
     int qstat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int dynamic = 0;
     bool fused = false;          // in-kernel reduce of the wide ranges
+    bool tail = false;           // last-arriver reduce of the wide ranges (no reduce launch)
     int nrtasks = 0;
     int2 *rtasks = nullptr;
     unsigned *arrive = nullptr;

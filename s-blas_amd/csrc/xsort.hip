@@ -451,6 +451,49 @@ __device__ void xs_reduce_phase(const XsArgs &a, double alpha, double beta, doub
     }
 }
 
+// Last-arriver reduce of a wide range (a.tail; replaces k_xsort_reduce): the
+// team whose sub-item counted in 8th for this launch writes the range's y.
+// Hand-off (MI355X_MICROARCH.md "visibility", first row of the sc1 table):
+// every partial is stored sc1 (8 B) by its team, every storing wave drains
+// (vmcnt(0)) before a workgroup barrier, ONE lane per team adds to the
+// range's unsharded arrival counter, and the team told by its add's return
+// value that it came last loads the other seven partials with sc1 loads only
+// (its own sit in its LDS rows).  Same sum as k_xsort_reduce: slots in XCD
+// order, then alpha * s + beta * y.
+template <bool kBeta, int kEp>
+__device__ __forceinline__ void xs_tail_reduce(const XsArgs &a, const XsRange &R, int k1, const double *acc,
+                                               int ht, int NT, double alpha, double beta,
+                                               double *__restrict__ y)
+{
+    const double *p = a.partial + R.pbase;
+    const int own = k1 - 1;
+    constexpr int B = 2;  // rows per thread in flight: 14 sc1 loads + 2 y loads
+#pragma unroll 1
+    for (int e0 = 0; e0 < kEp; e0 += B) {
+        double v[B][8], y0[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int r = ht + (e0 + u) * NT;
+            const int rr = r < R.nrows ? r : 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                v[u][k] = k == own ? 0.0
+                                   : __hip_atomic_load(p + (long long)k * R.nrows + rr, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            y0[u] = kBeta ? y[R.row0 + rr] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int r = ht + (e0 + u) * NT;
+            if (r >= R.nrows) continue;
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += k == own ? acc[r] : v[u][k];
+            y[R.row0 + r] = kBeta ? alpha * s + beta * y0[u] : alpha * s;
+        }
+    }
+}
+
 // kWG threads per workgroup: 1024 (16384 LDS rows, one workgroup per CU) or
 // 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
 // two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
@@ -472,6 +515,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     __shared__ int s_item;
     __shared__ int s_ctr[2][2];  // kDyn: claimed chunks per (team, segment)
     __shared__ int s_par[2][4];  // kDyn: per team {sub valid, k1, g0, n1}
+    __shared__ int s_last[2];    // a.tail: this team's wide sub-item counted in last
     static_assert(!kDyn || kPair, "dynamic claims pair two sub-items");
     // waves per team: team 0 (the pair's first, normally narrow, sub-item)
     // gets kWA waves, team 1 the rest
@@ -641,7 +685,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                 // on another XCD (whose L2 is not coherent with this one);
                 // plain stores otherwise: the kernel boundary before
                 // k_xsort_reduce publishes them (SBLAS_XS_SC1PART=1 keeps sc1)
-                if (a.fused || a.sc1part) {
+                if (a.fused || a.tail || a.sc1part) {
 #pragma unroll
                     for (int e = 0; e < kEp; ++e) {
                         const int r = ht + e * NT;
@@ -686,13 +730,24 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                 }
             }
         }
-        if (a.fused) {
+        if (a.fused || a.tail) {
             // count this team's wide sub-item in once every wave's partial
             // stores have drained (vmcnt(0), then the barrier)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (sub >= 0 && k1 && ht == 0)
-                __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (sub >= 0 && k1 && ht == 0) {
+                const unsigned old =
+                    __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last[half] = old + 1u == 8u * a.epoch;
+            }
+            if (a.tail) {
+                __syncthreads();
+                if (sub >= 0 && k1 && s_last[half]) {  // team-uniform
+                    constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
+                    constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
+                    xs_tail_reduce<kBeta, kEp>(a, R, k1, acc, ht, NT, alpha, beta, y);
+                }
+            }
         }
         // (the barrier at the loop top orders these reads of acc before the
         // next item's zeroing, and s_bnd's reuse)
@@ -1369,6 +1424,9 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // against 6 us for the separate k_xsort_reduce launch.
     P.fused = P.nt == kXsThreads && !wide.empty() && getenv("SBLAS_XS_FUSE") &&
               atoi(getenv("SBLAS_XS_FUSE")) != 0;
+    // last-arriver reduce (SBLAS_XS_TAIL=1): no reduce launch, no waiting;
+    // the 8th sub-item of a wide range to finish writes its y (xs_tail_reduce)
+    P.tail = !P.fused && !wide.empty() && getenv("SBLAS_XS_TAIL") && atoi(getenv("SBLAS_XS_TAIL")) != 0;
     P.nrtasks = (int)rtasks.size();
     SBLAS_HIP(hipMalloc(&P.rtasks, sizeof(int2) * std::max<size_t>(rtasks.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.arrive, sizeof(unsigned) * std::max<size_t>(wide.size(), 1)));
@@ -1449,7 +1507,9 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.rtasks = P.rtasks;
     a.nrtasks = P.nrtasks;
     a.arrive = P.arrive;
-    a.epoch = (unsigned)(P.epoch + (P.fused ? 1 : 0));
+    const bool tail = P.tail && !P.batch;  // the batch form has no in-kernel reduce
+    a.tail = tail ? 1 : 0;
+    a.epoch = (unsigned)(P.epoch + ((P.fused || tail) ? 1 : 0));
     a.qstride = P.qstride;
     a.G = P.G;
     a.q = P.q;
@@ -1536,7 +1596,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     SBLAS_LAUNCH(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
     SBLAS_HIP(hipGetLastError());
     P.parity ^= 1;
-    if (P.fused) ++P.epoch;
+    if (P.fused || tail) ++P.epoch;
     if (trace_path) {  // debugging aid: rows {subA, subB, block<<4|xcc, t0, endA, endB}
         SBLAS_HIP(hipMemcpyAsync(htrace.data(), a.trace, sizeof(long long) * htrace.size(),
                                  hipMemcpyDeviceToHost, s));
@@ -1551,7 +1611,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
             fclose(f);
         }
     }
-    if (P.nwide && !P.fused) {
+    if (P.nwide && !P.fused && !tail) {
         const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
         if (b)
             SBLAS_LAUNCH(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.wranges, P.partial, alpha, beta,
