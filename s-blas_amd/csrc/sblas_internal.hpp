@@ -270,6 +270,7 @@ struct XsPlan {
     bool pair = true;            // items pair two sub-items (two teams of waves)
     int split = 8;               // waves of a pair's first team (of 16)
     bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
+    bool solo = false;           // narrow ranges are items of their own (16,384 LDS rows)
     int u = 1;                   // chunks per dynamic claim (planner; SBLAS_XS_U)
     bool batch = false;          // small static items: k_spmv_xsort_batch (xsort.hip)
     int maxc = 0;                // most chunks of one item (both sub-items)

@@ -670,7 +670,12 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             a.trace[ts + 4] = (long long)s_tend[0];
             a.trace[ts + 5] = (long long)s_tend[1];
         }
-        if (sub >= 0) {
+        // A narrow sub-item alone in its item (the partner team empty: solo
+        // items, SBLAS_XS_SOLO, or a leftover) is written by the whole
+        // workgroup: its rows may fill both teams' LDS halves.
+        const int s0 = kPair ? (int)s_rec_all[0][0] : -1;
+        const bool solo = kPair && (int)s_rec_all[1][0] < 0 && s0 >= 0 && (s0 & 255) == 0;  // uniform
+        if (sub >= 0 && k1) {
             // epilogue: a team owns <= kXsHalfRows rows, at most kEp per
             // thread; every y load of the thread is issued before the first
             // use, so the y latency is paid once, not once per row (a rolled
@@ -679,54 +684,63 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             // kernel sits at its 128-VGPR cap.)
             constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
             constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
-            if (k1) {
-                double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
-                // agent-scope (sc1) stores when the fused reduce may read them
-                // on another XCD (whose L2 is not coherent with this one);
-                // plain stores otherwise: the kernel boundary before
-                // k_xsort_reduce publishes them (SBLAS_XS_SC1PART=1 keeps sc1)
-                if (a.fused || a.tail || a.sc1part) {
+            double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
+            // agent-scope (sc1) stores when the fused reduce may read them
+            // on another XCD (whose L2 is not coherent with this one);
+            // plain stores otherwise: the kernel boundary before
+            // k_xsort_reduce publishes them (SBLAS_XS_SC1PART=1 keeps sc1)
+            if (a.fused || a.tail || a.sc1part) {
 #pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                } else if (a.ntstore) {
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = ht + e * NT;
+                    if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (a.ntstore) {
 #pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        if (r < R.nrows) __builtin_nontemporal_store(acc[r], out + r);
-                    }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        if (r < R.nrows) out[r] = acc[r];
-                    }
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = ht + e * NT;
+                    if (r < R.nrows) __builtin_nontemporal_store(acc[r], out + r);
                 }
             } else {
-                double *yr = y + R.row0;
-                double y0[kEp];
-                if constexpr (kBeta) {
 #pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        y0[e] = r < R.nrows ? yr[r] : 0.0;
-                    }
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = ht + e * NT;
+                    if (r < R.nrows) out[r] = acc[r];
                 }
-                if (a.ntstore) {
+            }
+        } else if (solo || sub >= 0) {
+            // narrow: y = alpha * acc + beta * y over the sub-item's rows;
+            // a solo item's <= kXsRows rows over all kWG threads, a team's
+            // <= kXsHalfRows over its NT
+            constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
+            constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
+            static_assert(!kPair || kEp * kWG >= kXsRows, "a solo item's rows fit the epilogue");
+            const int et = solo ? (int)threadIdx.x : ht;
+            const int eNT = solo ? kWG : NT;
+            const long long rr = solo ? s_rec_all[0][1] : ((long long)(unsigned)R.row0 | ((long long)R.nrows << 32));
+            const int row0 = (int)(rr & 0xffffffffLL), nrows = (int)(rr >> 32);
+            const double *eacc = solo ? acc_all : acc;
+            double *yr = y + row0;
+            double y0[kEp];
+            if constexpr (kBeta) {
 #pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        if (r < R.nrows)
-                            __builtin_nontemporal_store(kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r], yr + r);
-                    }
-                } else {
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = et + e * eNT;
+                    y0[e] = r < nrows ? yr[r] : 0.0;
+                }
+            }
+            if (a.ntstore) {
 #pragma unroll
-                    for (int e = 0; e < kEp; ++e) {
-                        const int r = ht + e * NT;
-                        if (r < R.nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
-                    }
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = et + e * eNT;
+                    if (r < nrows)
+                        __builtin_nontemporal_store(kBeta ? alpha * eacc[r] + beta * y0[e] : alpha * eacc[r], yr + r);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = et + e * eNT;
+                    if (r < nrows) yr[r] = kBeta ? alpha * eacc[r] + beta * y0[e] : alpha * eacc[r];
                 }
             }
         }
@@ -1012,6 +1026,13 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     const bool nosort = getenv("SBLAS_XS_NOSORT") && atoi(getenv("SBLAS_XS_NOSORT")) != 0;
     int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsRows;
     if (const char *e = getenv("SBLAS_XS_ROWS")) rows_cap = std::max(1, std::min(rows_cap, atoi(e)));
+    // solo narrow items (SBLAS_XS_SOLO=1, paired dynamic kernel): a narrow
+    // range is an item of its own -- both teams' waves and all 16,384 LDS
+    // rows -- so its blocks are twice as dense (fewer x line requests per
+    // entry); wide ranges still pair (wide, wide) at 8,192 rows a team
+    P.solo = P.pair && P.dyn && getenv("SBLAS_XS_SOLO") && atoi(getenv("SBLAS_XS_SOLO")) != 0;
+    const int nrows_cap = P.solo ? kXsRows : rows_cap;  // narrow ranges
+    const double nfac = P.solo ? 2.0 : 1.0;             // a narrow range's cost, in sub-item caps
 
     // Cost model (work units ~ one streamed entry): a sub-item's time is its
     // entries plus lambda per distinct x line its gathers touch; with uniform
@@ -1048,10 +1069,10 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         // cap search below runs build_ranges many times over all m rows).
         auto cut = [&](int r, bool wide, long long &cnt) {
             const int start = r;
-            const int emax = (int)std::min<long long>(m, (long long)start + rows_cap);
+            const int emax = (int)std::min<long long>(m, (long long)start + (wide ? rows_cap : nrows_cap));
             auto fits = [&](int e) {
                 const double c = (double)(rp[e] - rp[start]);
-                return (wide ? wide_cost(c) : narrow_cost(c)) <= cap;
+                return wide ? wide_cost(c) <= cap : narrow_cost(c) <= nfac * cap;
             };
             int lo = start + 1, hi = emax;  // answer in [lo, hi]; lo always taken
             while (lo < hi) {
@@ -1068,7 +1089,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             long long cnt;
             int e = cut(r, true, cnt);
             const bool wide = cnt > 0 && !no_wide &&
-                              (all_wide || (narrow_cost((double)cnt) > cap && cnt >= 16LL * (e - r) &&
+                              (all_wide || (narrow_cost((double)cnt) > nfac * cap && cnt >= 16LL * (e - r) &&
                                             (double)(wide_entries + cnt) <= wbudget * (double)nnz));
             if (wide) wide_entries += cnt;
             if (!wide) e = cut(r, false, cnt);
@@ -1082,7 +1103,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     };
     auto count_subs = [&]() {
         long long c = 0;
-        for (const XsRange &R : ranges) c += R.wide ? 8 : 1;
+        for (const XsRange &R : ranges) c += R.wide ? 8 : P.solo ? 2 : 1;
         return c;
     };
     // grow the sub-item cost until the sub-items fit the resident grid (a
@@ -1146,7 +1167,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
                 }
                 const int g = c / Wg;
                 const uint32_t cp = (uint32_t)(c - g * Wg), lr = (uint32_t)(r - R.row0);
-                if ((long long)cp >= wmax || lr >= (uint32_t)rows_cap) bad = true;
+                if ((long long)cp >= wmax || lr >= (uint32_t)(R.wide ? rows_cap : nrows_cap)) bad = true;
                 bk[(size_t)i * G + g].push_back({(cp << kXsRowBits) | lr, hval[e]});
             }
         }
@@ -1195,7 +1216,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // (only where its chunks are smaller, unless forced with =2)
     bool k24 = false;
     if (const char *e = getenv("SBLAS_XS_K24"))
-        k24 = P.dyn && rows_cap <= (1 << kK24RowBits) && (atoi(e) == 2 || (atoi(e) == 1 && b24 < b32));
+        k24 = P.dyn && !P.solo && rows_cap <= (1 << kK24RowBits) && (atoi(e) == 2 || (atoi(e) == 1 && b24 < b32));
     P.k24 = k24;
     std::vector<long long> blk(nblk + 1, 0);  // chunk offsets
     for (size_t k = 0; k < nblk; ++k) blk[k + 1] = blk[k] + (k24 ? n24[k] : n32[k]);
@@ -1325,6 +1346,19 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
                              [&](const std::pair<int, int> &u, const std::pair<int, int> &v) {
                                  return cost(u.first) > cost(v.first);
                              });
+    } else if (P.solo) {
+        // solo narrow items (narrow, -1); wide sub-items paired within their
+        // XCD; each queue alternates the two kinds
+        std::vector<std::vector<std::pair<int, int>>> qn(8), qw(8);
+        for (size_t j = 0; j < nsub.size(); ++j) qn[j % 8].push_back({nsub[j], -1});
+        for (int k = 0; k < 8; ++k)
+            for (size_t j = 0; j < wsub[k].size(); j += 2)
+                qw[k].push_back({wsub[k][j], j + 1 < wsub[k].size() ? wsub[k][j + 1] : -1});
+        for (int k = 0; k < 8; ++k)
+            for (size_t j = 0; j < std::max(qn[k].size(), qw[k].size()); ++j) {
+                if (j < qn[k].size()) q[k].push_back(qn[k][j]);
+                if (j < qw[k].size()) q[k].push_back(qw[k][j]);
+            }
     } else {
         // a narrow (gather-bound) with a wide (stream-bound) sub-item where
         // possible, the XCDs interleaved so the narrow ones spread evenly;
@@ -1393,7 +1427,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             for (const auto &it : q[k]) mc = std::max(mc, nch(it.first) + nch(it.second));
         P.maxc = (int)std::min<long long>(mc, 1 << 30);
         const char *be = getenv("SBLAS_XS_BATCH");
-        P.batch = be && atoi(be) != 0 && P.pair && P.nt == kXsThreads && !P.k24 && !P.dynamic &&
+        P.batch = be && atoi(be) != 0 && P.pair && !P.solo && P.nt == kXsThreads && !P.k24 && !P.dynamic &&
                   mc <= kXsBatchMax;
     }
     std::vector<int> qflat((size_t)16 * P.qstride, -1);
