@@ -199,12 +199,7 @@ __device__ __forceinline__ void trsv_backoff(int units)
 // analysis (position t holds row lrow[t]; rows of one level are contiguous),
 // so the 64 rows of a wave belong to one level and become ready together
 // instead of a wave waiting on its latest level.  Same sums, same order.
-// kPipe (SBLAS_TRSV_PIPE, 1 = the default): polls of the current dependency
-// kept in flight per lane.  With kPipe > 1 a lane issues the next poll of the
-// same address before it examines the oldest one, so a publication is seen
-// ~RTT/kPipe sooner on average (the loop waits only for the oldest poll);
-// polls of an address the lane has moved past are discarded unread.
-template <bool kLevel, int kPipe = 1>
+template <bool kLevel>
 __global__ __launch_bounds__(256) void k_trsv_pull(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, int n, int backward, const double *__restrict__ b,
@@ -246,27 +241,11 @@ __global__ __launch_bounds__(256) void k_trsv_pull(
         // current dependency cached in registers: a spin costs ONE sc1 load
         int cj = (live && j < jend) ? col[j] : 0;
         double vj = (live && j < jend) ? val[j] : 0.0;
-        unsigned long long xq[kPipe > 1 ? kPipe - 1 : 1];  // polls in flight, oldest first
-        bool have = false;                                  // xq holds polls of cj
         while (__any(pending)) {
             bool adv = false;
             if (pending && j < jend) {
-                unsigned long long x0;
-                if constexpr (kPipe > 1) {
-                    if (!have) {
-#pragma unroll
-                        for (int k = 0; k < kPipe - 1; ++k) xq[k] = ld_sc1_u64(xbits + cj);
-                        have = true;
-                    }
-                    x0 = xq[0];
-#pragma unroll
-                    for (int k = 0; k + 1 < kPipe - 1; ++k) xq[k] = xq[k + 1];
-                    xq[kPipe - 2] = ld_sc1_u64(xbits + cj);  // issued before x0 is examined
-                } else {
-                    x0 = ld_sc1_u64(xbits + cj);
-                }
+                const unsigned long long x0 = ld_sc1_u64(xbits + cj);
                 if (x0 != kXPending) {
-                    have = false;  // cj advances: the polls in flight are stale
                     adv = true;
                     sum += vj * __longlong_as_double((long long)x0);
                     ++j;
@@ -953,14 +932,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     // s_sleep(1) per poll, the measured default
     int slp = 1;
     if (const char *e = getenv("SBLAS_TRSV_SLEEP")) slp = std::max(-10, std::min(64, atoi(e)));
-    int pipe = 1;  // polls in flight per lane (k_trsv_pull kPipe)
-    if (const char *e = getenv("SBLAS_TRSV_PIPE")) pipe = std::max(1, std::min(4, atoi(e)));
-    if (algo == 1 && pipe > 1) {
-        fill_pending((unsigned long long *)d_x, T->n, s);
-        auto kern = pipe == 2 ? k_trsv_pull<false, 2> : pipe == 3 ? k_trsv_pull<false, 3> : k_trsv_pull<false, 4>;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval, T->n, T->substitution, d_b,
-                           (unsigned long long *)d_x, T->ctl, nullptr, slp);
-    } else if (algo == 3) {  // sync-free pull, tickets in level order
+    if (algo == 3) {  // sync-free pull, tickets in level order
         fill_pending((unsigned long long *)d_x, T->n, s);
         hipLaunchKernelGGL(k_trsv_pull<true>, dim3(grid), dim3(256), 0, s, T->lrp, T->lcol, T->lval, T->n,
                            T->substitution, d_b, (unsigned long long *)d_x, T->ctl, T->lrow, slp);
