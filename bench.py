@@ -67,6 +67,58 @@ BETA = 0.39438292681909304  # dspmv_test.cu:282
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+class Workload:
+    """The matrix a run measures.  `synth` (default) is BASELINE configs[1]'s
+    scaled generator (rows generated per slice, as before); the others are
+    SuiteSparse-class matrices generated once on the host: `stencil7` /
+    `stencil27` (3-D finite-difference / FEM-block pattern on a grid^3 mesh,
+    sblas_gen_stencil3d) and `rmat` (power-law graph, 2^scale vertices,
+    sblas_gen_rmat).  rows(a, b) returns the (col, val) of rows [a, b)."""
+
+    def __init__(self, args, sblas):
+        self.kind, self.args, self.sblas = args.matrix, args, sblas
+        if self.kind == "synth":
+            self.n = args.nrows
+            self.rowptr = sblas.gen_synth_rowptr(self.n, args.heavy, args.light)
+            self._cv = None
+        elif self.kind.startswith("stencil"):
+            g = args.grid
+            self.rowptr, col, val = sblas.gen_stencil3d(g, g, g, int(self.kind[7:]), seed=49)
+            self.n = len(self.rowptr) - 1
+            self._cv = (col, val)
+        else:
+            self.rowptr, col, val = sblas.gen_rmat(args.scale, 16, seed=50)
+            self.n = len(self.rowptr) - 1
+            self._cv = (col, val)
+        self.nnz = int(self.rowptr[-1])
+
+    def rows(self, a: int, b: int):
+        if self._cv is None:
+            return self.sblas.gen_synth_rows(self.n, self.rowptr, a, b, self.args.heavy, self.args.light,
+                                             prefix=self.args.cols == "prefix", seed=42)
+        rp = self.rowptr
+        return self._cv[0][rp[a]:rp[b]], self._cv[1][rp[a]:rp[b]]
+
+    @property
+    def default(self) -> bool:
+        """The configuration the committed PMC summaries were collected on."""
+        a = self.args
+        return self.kind == "synth" and a.cols == "random" and self.n == 2_000_000 and \
+            (a.heavy, a.light) == (96, 9)
+
+    def describe(self, algo: str) -> str:
+        a = self.args
+        if self.kind == "synth":
+            return (f"synthetic non-uniform n={self.n} CSR fp64 SpMV, rows<n/8: {a.heavy} "
+                    f"nnz else {a.light}, {a.cols} sorted cols (seed 42), "
+                    f"y=alpha*A*x+beta*y, {algo} kernel")
+        if self.kind.startswith("stencil"):
+            return (f"{self.kind[7:]}-point 3-D stencil on a {a.grid}^3 grid (n={self.n}, nnz={self.nnz}; "
+                    f"SuiteSparse-class structured matrix), y=alpha*A*x+beta*y, {algo} kernel")
+        return (f"R-MAT power-law graph, scale {a.scale} (n={self.n}, nnz={self.nnz}, edge factor 16), "
+                f"y=alpha*A*x+beta*y, {algo} kernel")
+
+
 def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
     """Oracle restatement (oracle/liboracle.so) timed on this host's cores.
     Only this leg of bench.py touches oracle/ (DESIGN.md)."""
@@ -108,7 +160,7 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
     return {
         "value": round(2.0 * nnz / t_mt / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
         "kind": "port", "cpu_model": model,
-        "sample": (f"full config-2 matrix, orc_csr_spmv_omp (OpenMP, schedule dynamic) x{r_mt} "
+        "sample": (f"full matrix of the workload, orc_csr_spmv_omp (OpenMP, schedule dynamic) x{r_mt} "
                    f"reps, {t_mt * 1e3:.1f} ms/SpMV; single-core scalar port orc_csr_spmv "
                    f"x{r_st}: {t_st * 1e3:.1f} ms/SpMV = {2.0 * nnz / t_st / 1e9:.3f} GFLOP/s"),
         "single_core_value": round(2.0 * nnz / t_st / 1e9, 3),
@@ -176,12 +228,10 @@ def run_ctx(args) -> int:
         os.environ["SBLAS_CTX_LOOPBACK"] = "1"  # read by sblas_ctx_create
     algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
                 "xsort": sblas.XSORT}
-    n = args.nrows
-    rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
-    nnz = int(rowptr[-1])
     t_gen = time.perf_counter()
-    col, val = sblas.gen_synth_rows(n, rowptr, 0, n, args.heavy, args.light,
-                                    prefix=args.cols == "prefix", seed=42)
+    W = Workload(args, sblas)
+    n, rowptr, nnz = W.n, W.rowptr, W.nnz
+    col, val = W.rows(0, n)
     x_h = sblas.gen_vector(n, 43)
     t_gen = time.perf_counter() - t_gen
     exchange = sblas.CTX_ALLREDUCE if args.exchange == "allreduce" else sblas.CTX_ALLGATHER
@@ -274,8 +324,7 @@ def run_ctx(args) -> int:
     total_flops = 2.0 * nnz
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
     agg = sum(dev_bytes) / (kern_max * 1e-3) / 1e9
-    profiled = N == 1 and args.cols == "random" and n == 2_000_000 and \
-        (args.heavy, args.light) == (96, 9)
+    profiled = N == 1 and W.default
     out = {
         "metric": METRIC,
         "value": round(total_flops / (step_ms * 1e-3) / 1e9, 3),
@@ -290,10 +339,8 @@ def run_ctx(args) -> int:
         "dtype": "f64",
         "data": "synthetic (deterministic generator, DESIGN.md)",
         "config": {
-            "workload": (f"synthetic non-uniform n={n} CSR fp64 SpMV, rows<n/8: {args.heavy} "
-                         f"nnz else {args.light}, {args.cols} sorted cols (seed 42), "
-                         f"y=alpha*A*x+beta*y, {args.algo} kernel"),
-            "n": n, "nnz": nnz, "algo": args.algo,
+            "workload": W.describe(args.algo),
+            "n": n, "nnz": nnz, "algo": args.algo, "matrix": args.matrix,
             "partition": ("cyclic row chunks" if partition == 0 else "nnz-balanced (spMV_mgpu_v1)"),
             "exchange": args.exchange if exchange == sblas.CTX_ALLREDUCE else "allgather",
             "driver": "ctx (one process, sblas_ctx over RCCL, ncclCommInitAll)",
@@ -359,6 +406,13 @@ def main() -> int:
     ap.add_argument("--heavy", type=int, default=96)
     ap.add_argument("--light", type=int, default=9)
     ap.add_argument("--cols", choices=["random", "prefix"], default="random")
+    ap.add_argument("--matrix", choices=["synth", "stencil7", "stencil27", "rmat"], default="synth",
+                    help="synth (default): BASELINE configs[1]'s scaled generator; stencil7 / "
+                         "stencil27: 3-D finite-difference / FEM-block pattern on a --grid^3 mesh; "
+                         "rmat: power-law graph with 2^--scale vertices (SuiteSparse-class checks "
+                         "of the north star's >= 60% target; not the headline)")
+    ap.add_argument("--grid", type=int, default=160, help="stencil mesh edge (n = grid^3)")
+    ap.add_argument("--scale", type=int, default=21, help="R-MAT scale (n = 2^scale)")
     ap.add_argument("--exchange", choices=["allgather", "allreduce"], default="allgather")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the "
@@ -432,21 +486,16 @@ def main() -> int:
 
     algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
                 "xsort": sblas.XSORT}
-    n = args.nrows
-    rowptr = sblas.gen_synth_rowptr(n, args.heavy, args.light)
-    nnz = int(rowptr[-1])
-    prefix = args.cols == "prefix"
     t_gen = time.perf_counter()
+    W = Workload(args, sblas)
+    n, rowptr, nnz = W.n, W.rowptr, W.nnz
     # auto: the library decides per rank slice (sblas_csr_pick: row split
     # where consecutive entries share x lines, else xsort from ~2M nonzeros,
     # else the XCD-panel row split; DESIGN.md §4 "Algorithm choice")
     algo = sblas.AUTO if args.algo == "auto" else algo_ids[args.algo]
     if args.partition == "cyclic" and args.exchange == "allgather":
         plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
-        lrp, col, val = sblas_dist.cyclic_local_csr(
-            rowptr, plan, rank,
-            lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, args.heavy, args.light,
-                                              prefix=prefix, seed=42))
+        lrp, col, val = sblas_dist.cyclic_local_csr(rowptr, plan, rank, W.rows)
         t_gen = time.perf_counter() - t_gen
         op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
                                        overlap=args.overlap)
@@ -457,8 +506,7 @@ def main() -> int:
     else:
         plan = sblas_dist.make_plan(rowptr, n, world)
         r0, r1, i0, i1, _ = plan.local(rank)
-        col_rows, val_rows = sblas.gen_synth_rows(n, rowptr, r0, r1, args.heavy, args.light,
-                                                  prefix=prefix, seed=42)
+        col_rows, val_rows = W.rows(r0, r1)
         off = i0 - int(rowptr[r0])
         col = np.ascontiguousarray(col_rows[off:off + (i1 - i0)])
         val = np.ascontiguousarray(val_rows[off:off + (i1 - i0)])
@@ -640,8 +688,7 @@ def main() -> int:
         if rank == 0:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import orc  # oracle: checker only
-            col_all, val_all = sblas.gen_synth_rows(n, rowptr, 0, n, args.heavy, args.light,
-                                                    prefix=args.cols == "prefix", seed=42)
+            col_all, val_all = W.rows(0, n)
             want = orc.csr_spmv(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
             bound = orc.spmv_bound(rowptr, col_all, val_all, x_h, ALPHA, BETA, np.zeros(plan.m))
             check = bool(np.all(np.abs(y_dev - want) <= bound))
@@ -670,8 +717,7 @@ def main() -> int:
     if rank == 0:
         achieved = local_bytes / (kern_ms * 1e-3) / 1e9  # rank 0's kernel
         # the committed PMC summary was collected on the default workload only
-        profiled = world == 1 and args.cols == "random" and n == 2_000_000 and \
-            (args.heavy, args.light) == (96, 9)
+        profiled = world == 1 and W.default
         traffic = pmc_traffic(args.algo) if profiled else None
         out = {
             "metric": METRIC,
@@ -687,10 +733,8 @@ def main() -> int:
             "dtype": "f64",
             "data": "synthetic (deterministic generator, DESIGN.md)",
             "config": {
-                "workload": (f"synthetic non-uniform n={n} CSR fp64 SpMV, rows<n/8: {args.heavy} "
-                             f"nnz else {args.light}, {args.cols} sorted cols (seed 42), "
-                             f"y=alpha*A*x+beta*y, {args.algo} kernel"),
-                "n": n, "nnz": nnz, "algo": args.algo,
+                "workload": W.describe(args.algo),
+                "n": n, "nnz": nnz, "algo": args.algo, "matrix": args.matrix,
                 "partition": partition if world > 1 else "single GPU",
                 "exchange": args.exchange if world > 1 else "none",
             },

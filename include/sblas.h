@@ -406,6 +406,16 @@ int sblas_gen_synth_rows(int n, int heavy, int light, int prefix_cols,
                          unsigned long long seed, const long long *rowptr,
                          int row_begin, int row_end, int *col, double *val);
 int sblas_gen_vector(int n, unsigned long long seed, double *v);
+/* 3-D stencil (points = 7 or 27) on an nx*ny*nz grid, natural ordering: the
+ * structured SuiteSparse kind.  Off-diagonals -U[0,1), diagonal 1 + sum|off|.
+ * rowptr int64 (n+1); col == NULL: rowptr only. */
+int sblas_gen_stencil3d(int nx, int ny, int nz, int points, unsigned long long seed,
+                        long long *rowptr, int *col, double *val);
+/* R-MAT power-law graph (a,b,c = 0.57,0.19,0.19), 2^scale vertices,
+ * edge_factor*2^scale draws, labels permuted, duplicates merged, values U[0,1).
+ * col/val hold cap >= edge_factor*2^scale entries; nnz = rowptr[2^scale]. */
+int sblas_gen_rmat(int scale, int edge_factor, unsigned long long seed, long long *rowptr,
+                   int *col, double *val, long long cap);
 /* Unit-lower-triangular CSC (diagonal first) for SpTRSV benchmarks:
  * `offd` distinct rows per column within (j, j+band], values
  * (1 + r%10)/(20*row_len).  rowidx == NULL: colptr only. */

@@ -198,9 +198,11 @@ namespace {
 // whose column lies within 16 columns (one 128-B line of x) of the previous
 // entry's -- for a row's first entry, the previous row's last (lanes of the
 // row split read neighbouring rows together, so a diagonal counts as local).
-// cnt = {adjacent, counted}.
+// cnt = {adjacent, counted, then the sampled entries per eighth of the
+// columns [k*n/8, (k+1)*n/8): how evenly the x gathers would spread over the
+// XCDs' column groups of the column-sorted kernel}.
 __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ rowptr,
-                                                       const int *__restrict__ col, int m, int S,
+                                                       const int *__restrict__ col, int m, int n, int S,
                                                        unsigned long long *cnt)
 {
     const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
@@ -209,20 +211,32 @@ __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ r
     const int r = (int)((long long)w * m / S);
     const int a = rowptr[r];
     const int b = min(rowptr[r + 1], a + 1024);
-    unsigned adj = 0, tot = 0;
-    for (int e = max(a, 1) + lane; e < b; e += 64) {
-        const int d = col[e] - col[e - 1];
-        adj += (d > -16 && d < 16) ? 1u : 0u;
-        ++tot;
+    unsigned adj = 0, tot = 0, h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int e = a + lane; e < b; e += 64) {
+        const int c = col[e];
+        const int k = (int)min(7LL, max(0LL, (long long)c * 8 / max(n, 1)));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[q] += q == k ? 1u : 0u;
+        if (e >= 1) {
+            const int d = c - col[e - 1];
+            adj += (d > -16 && d < 16) ? 1u : 0u;
+            ++tot;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         adj += __shfl_down(adj, o, 64);
         tot += __shfl_down(tot, o, 64);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[q] += __shfl_down(h[q], o, 64);
     }
     if (lane == 0 && tot) {
         atomicAdd(&cnt[0], (unsigned long long)adj);
         atomicAdd(&cnt[1], (unsigned long long)tot);
     }
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (h[q]) atomicAdd(&cnt[2 + q], (unsigned long long)h[q]);
 }
 
 constexpr long long kAutoXsortMinNnz = 2000000;  // bench slices: xsort leads from ~2M nnz
@@ -230,14 +244,14 @@ constexpr long long kAutoXsortMinNnz = 2000000;  // bench slices: xsort leads fr
 int pick_algo(sblas_csr_s &A, hipStream_t s)
 {
     if (A.auto_algo) return A.auto_algo;
-    double adj = 0.0;
+    double adj = 0.0, share = 0.0;
     const int S = (int)std::min<long long>(A.m, 65536);
     if (S > 0 && A.nnz > 1) {
-        unsigned long long *d = nullptr, h[2] = {0, 0};
+        unsigned long long *d = nullptr, h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         hipError_t e = hipMalloc(&d, sizeof(h));
         if (e == hipSuccess) e = hipMemsetAsync(d, 0, sizeof(h), s);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_col_adjacency, dim3((S + 3) / 4), dim3(256), 0, s, A.rowptr, A.col, A.m, S, d);
+            hipLaunchKernelGGL(k_col_adjacency, dim3((S + 3) / 4), dim3(256), 0, s, A.rowptr, A.col, A.m, A.n, S, d);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
@@ -248,11 +262,27 @@ int pick_algo(sblas_csr_s &A, hipStream_t s)
             return -SBLAS_ERR_HIP;
         }
         adj = h[1] ? (double)h[0] / (double)h[1] : 0.0;
+        unsigned long long hs = 0, hm = 0;
+        for (int q = 0; q < 8; ++q) {
+            hs += h[2 + q];
+            hm = std::max(hm, h[2 + q]);
+        }
+        share = hs ? (double)hm / (double)hs : 1.0;
     }
     A.col_adjacency = adj;
+    A.col_maxshare = share;
+    // The column-sorted kernel wherever it applies at size and its column
+    // groups share the work: it leads on random columns (config 2: 0.51 of
+    // 8 TB/s vs 0.21 row split) and on banded / stencil matrices too (3-D
+    // 27-point stencil 0.84 vs 0.55, 7-point 0.71 vs 0.58), but
+    // columns crowded into one eighth (the reference generator's prefix
+    // columns) leave one XCD all of it: the row split there (0.68), as for
+    // any matrix whose rows read neighbouring x lines; the XCD-panel row
+    // split below 2M nonzeros.
+    const bool spread = share <= 0.25;  // no eighth of the columns holds > 2x its share
     int algo;
-    if (adj >= 0.5) algo = SBLAS_SPMV_ROWSPLIT;
-    else if (A.nnz >= kAutoXsortMinNnz && (long long)A.n * 8 <= (120LL << 20)) algo = SBLAS_SPMV_XSORT;
+    if (A.nnz >= kAutoXsortMinNnz && (long long)A.n * 8 <= (120LL << 20) && spread) algo = SBLAS_SPMV_XSORT;
+    else if (adj >= 0.5 || !spread) algo = SBLAS_SPMV_ROWSPLIT;
     else algo = SBLAS_SPMV_PANEL;
     if (const char *o = getenv("SBLAS_AUTO")) {
         const int v = atoi(o);

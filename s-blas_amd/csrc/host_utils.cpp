@@ -692,6 +692,134 @@ int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed, i
     return SBLAS_OK;
 }
 
+// 3-D stencil matrix on an nx x ny x nz grid, natural ordering (row r =
+// (k*ny + j)*nx + i): the structured, banded kind of SuiteSparse matrix
+// (FEM / finite-difference Laplacians).  points = 7 (faces) or 27 (the full
+// 3x3x3 box).  Off-diagonal a_rc = -U[0,1) from a per-entry hash of (seed,
+// r, c); the diagonal is 1 + sum |off|, so the matrix is diagonally dominant.
+// Columns ascend within a row.  col == NULL: rowptr only.
+int sblas_gen_stencil3d(int nx, int ny, int nz, int points, unsigned long long seed, long long *rowptr, int *col,
+                        double *val)
+{
+    if (nx < 1 || ny < 1 || nz < 1 || (points != 7 && points != 27) || !rowptr) return SBLAS_ERR_INVALID;
+    const long long n = (long long)nx * ny * nz;
+    if (n > 0x7fffffffLL) return SBLAS_ERR_INVALID;
+    auto inside = [&](int i, int j, int k) { return i >= 0 && i < nx && j >= 0 && j < ny && k >= 0 && k < nz; };
+    auto is_pt = [&](int di, int dj, int dk) {
+        return points == 27 || (std::abs(di) + std::abs(dj) + std::abs(dk) <= 1);
+    };
+    rowptr[0] = 0;
+    std::vector<int> len((size_t)n);
+#pragma omp parallel for schedule(static)
+    for (long long r = 0; r < n; ++r) {
+        const int i = (int)(r % nx), j = (int)((r / nx) % ny), k = (int)(r / ((long long)nx * ny));
+        int c = 0;
+        for (int dk = -1; dk <= 1; ++dk)
+            for (int dj = -1; dj <= 1; ++dj)
+                for (int di = -1; di <= 1; ++di)
+                    c += is_pt(di, dj, dk) && inside(i + di, j + dj, k + dk);
+        len[(size_t)r] = c;
+    }
+    for (long long r = 0; r < n; ++r) rowptr[r + 1] = rowptr[r] + len[(size_t)r];
+    if (!col) return SBLAS_OK;
+    if (!val) return SBLAS_ERR_INVALID;
+#pragma omp parallel for schedule(static)
+    for (long long r = 0; r < n; ++r) {
+        const int i = (int)(r % nx), j = (int)((r / nx) % ny), k = (int)(r / ((long long)nx * ny));
+        long long e = rowptr[r], de = -1;
+        double off = 0.0;
+        for (int dk = -1; dk <= 1; ++dk)
+            for (int dj = -1; dj <= 1; ++dj)
+                for (int di = -1; di <= 1; ++di) {
+                    if (!is_pt(di, dj, dk) || !inside(i + di, j + dj, k + dk)) continue;
+                    const long long c = r + ((long long)dk * ny + dj) * nx + di;
+                    col[e] = (int)c;
+                    if (c == r) {
+                        de = e;
+                    } else {
+                        unsigned long long h = seed ^ ((unsigned long long)r * 0x9E3779B97F4A7C15ULL) ^
+                                               ((unsigned long long)c * 0xC2B2AE3D27D4EB4FULL);
+                        val[e] = -to_u01(splitmix(h));
+                        off -= val[e];
+                    }
+                    ++e;
+                }
+        val[de] = 1.0 + off;
+    }
+    return SBLAS_OK;
+}
+
+// R-MAT power-law graph (Graph500 generator parameters a, b, c = 0.57, 0.19,
+// 0.19, no per-level noise) with 2^scale vertices and edge_factor * 2^scale
+// edge draws: each draw descends `scale` quadrant levels from its own hashed
+// stream, vertex labels are then permuted (seeded Fisher-Yates) so the heavy
+// rows spread over the matrix, duplicate (row, col) draws are merged (values
+// summed) and columns ascend within a row.  Values U[0,1).  rowptr: 2^scale + 1
+// int64 entries; col/val hold cap entries (edge_factor * 2^scale always
+// suffices); the nonzero count is rowptr[2^scale].
+int sblas_gen_rmat(int scale, int edge_factor, unsigned long long seed, long long *rowptr, int *col, double *val,
+                   long long cap)
+{
+    if (scale < 1 || scale > 30 || edge_factor < 1 || !rowptr || !col || !val) return SBLAS_ERR_INVALID;
+    const long long n = 1LL << scale, E = (long long)edge_factor * n;
+    if (cap < E) return SBLAS_ERR_INVALID;
+    std::vector<int> perm((size_t)n);
+    for (long long v = 0; v < n; ++v) perm[(size_t)v] = (int)v;
+    {
+        unsigned long long st = seed ^ 0xA5A5A5A5DEADBEEFULL;
+        for (long long v = n - 1; v > 0; --v) {
+            const long long w = (long long)(((unsigned __int128)splitmix(st) * (unsigned long long)(v + 1)) >> 64);
+            std::swap(perm[(size_t)v], perm[(size_t)w]);
+        }
+    }
+    std::vector<int> er((size_t)E), ec((size_t)E);
+    std::vector<double> ev((size_t)E);
+#pragma omp parallel for schedule(static)
+    for (long long e = 0; e < E; ++e) {
+        unsigned long long st = seed ^ ((unsigned long long)(e + 1) * 0x9E3779B97F4A7C15ULL);
+        long long r = 0, c = 0;
+        for (int l = 0; l < scale; ++l) {
+            const double u = to_u01(splitmix(st));
+            const int rb = u >= 0.57 + 0.19, cb = (u >= 0.57 && u < 0.57 + 0.19) || u >= 0.57 + 0.19 + 0.19;
+            r = (r << 1) | rb;
+            c = (c << 1) | cb;
+        }
+        er[(size_t)e] = perm[(size_t)r];
+        ec[(size_t)e] = perm[(size_t)c];
+        ev[(size_t)e] = to_u01(splitmix(st));
+    }
+    // bucket the draws by row (stable in draw order), then sort + merge per row
+    std::vector<long long> cnt((size_t)n + 1, 0);
+    for (long long e = 0; e < E; ++e) ++cnt[(size_t)er[(size_t)e] + 1];
+    for (long long v = 0; v < n; ++v) cnt[(size_t)v + 1] += cnt[(size_t)v];
+    std::vector<long long> pos(cnt.begin(), cnt.end() - 1);
+    std::vector<std::pair<int, double>> tmp((size_t)E);
+    for (long long e = 0; e < E; ++e) tmp[(size_t)pos[(size_t)er[(size_t)e]]++] = {ec[(size_t)e], ev[(size_t)e]};
+    std::vector<int> rl((size_t)n);
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (long long v = 0; v < n; ++v) {
+        auto b = tmp.begin() + cnt[(size_t)v], en = tmp.begin() + cnt[(size_t)v + 1];
+        std::stable_sort(b, en, [](const std::pair<int, double> &x, const std::pair<int, double> &y) {
+            return x.first < y.first;
+        });
+        long long w = cnt[(size_t)v];
+        for (auto it = b; it != en; ++it) {
+            if (w > cnt[(size_t)v] && tmp[(size_t)w - 1].first == it->first) tmp[(size_t)w - 1].second += it->second;
+            else tmp[(size_t)w++] = *it;
+        }
+        rl[(size_t)v] = (int)(w - cnt[(size_t)v]);
+    }
+    rowptr[0] = 0;
+    for (long long v = 0; v < n; ++v) rowptr[v + 1] = rowptr[v] + rl[(size_t)v];
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (long long v = 0; v < n; ++v)
+        for (int k = 0; k < rl[(size_t)v]; ++k) {
+            col[rowptr[v] + k] = tmp[(size_t)cnt[(size_t)v] + k].first;
+            val[rowptr[v] + k] = tmp[(size_t)cnt[(size_t)v] + k].second;
+        }
+    return SBLAS_OK;
+}
+
 int sblas_gen_vector(int n, unsigned long long seed, double *v)
 {
     if (n < 0 || !v) return SBLAS_ERR_INVALID;

@@ -312,6 +312,7 @@ struct sblas_csr_s {
     long long plan_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device bytes per algorithm's plan
     int auto_algo = 0;          // SBLAS_SPMV_AUTO's choice (capi.hip pick_algo), 0 = not yet
     double col_adjacency = -1;  // its locality probe
+    double col_maxshare = -1;   // its largest eighth-of-the-columns share of the sampled entries
 };
 
 namespace sblas {

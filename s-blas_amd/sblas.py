@@ -128,6 +128,8 @@ _sig("sblas_gen_synth_rowptr", _i, _i, _i, _i, _p)
 _sig("sblas_gen_synth_rows", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _i, _i, _p, _p)
 _sig("sblas_gen_vector", _i, _i, C.c_ulonglong, _p)
 _sig("sblas_gen_lower_banded", _i, _i, _i, _i, C.c_ulonglong, _p, _p, _p)
+_sig("sblas_gen_stencil3d", _i, _i, _i, _i, _i, C.c_ulonglong, _p, _p, _p)
+_sig("sblas_gen_rmat", _i, _i, _i, C.c_ulonglong, _p, _p, _p, C.c_longlong)
 
 
 def check(st: int, what: str = "") -> None:
@@ -256,6 +258,31 @@ def gen_synth_rows(n: int, rowptr: np.ndarray, r0: int, r1: int, heavy: int = 96
     check(lib.sblas_gen_synth_rows(n, heavy, light, int(prefix), seed, ptr(rowptr), r0, r1,
                                    ptr(col), ptr(val)), "gen_synth_rows")
     return col[:cnt], val[:cnt]
+
+
+def gen_stencil3d(nx: int, ny: int, nz: int, points: int = 27, seed: int = 49):
+    """3-D 7/27-point stencil CSR (int64 rowptr, int32 col, float64 val): the
+    structured SuiteSparse kind (sblas_gen_stencil3d)."""
+    n = nx * ny * nz
+    rp = np.zeros(n + 1, np.int64)
+    check(lib.sblas_gen_stencil3d(nx, ny, nz, points, seed, ptr(rp), None, None), "gen_stencil3d")
+    nnz = int(rp[-1])
+    col = np.zeros(max(nnz, 1), np.int32)
+    val = np.zeros(max(nnz, 1), np.float64)
+    check(lib.sblas_gen_stencil3d(nx, ny, nz, points, seed, ptr(rp), ptr(col), ptr(val)), "gen_stencil3d")
+    return rp, col[:nnz], val[:nnz]
+
+
+def gen_rmat(scale: int, edge_factor: int = 16, seed: int = 50):
+    """R-MAT power-law graph CSR, 2^scale vertices (sblas_gen_rmat)."""
+    n = 1 << scale
+    cap = edge_factor * n
+    rp = np.zeros(n + 1, np.int64)
+    col = np.zeros(cap, np.int32)
+    val = np.zeros(cap, np.float64)
+    check(lib.sblas_gen_rmat(scale, edge_factor, seed, ptr(rp), ptr(col), ptr(val), cap), "gen_rmat")
+    nnz = int(rp[-1])
+    return rp, col[:nnz].copy(), val[:nnz].copy()
 
 
 def gen_lower_banded(n: int, offd: int, band: int, seed: int = 47):

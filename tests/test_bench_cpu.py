@@ -58,3 +58,23 @@ def test_bench_exits_nonzero_when_gpus_exceed_devices():
     assert r.returncode == 2, r.stdout + r.stderr
     assert "refusing to measure fewer GPUs" in r.stderr
     assert r.stdout.strip() == ""
+
+
+@pytest.mark.parametrize("matrix", ["stencil7", "stencil27", "rmat"])
+def test_workload_rows_match_generators(matrix):
+    """bench.py's Workload hands out the generator's rows for any [a, b) (the
+    torch path slices them per rank)."""
+    sys.path.insert(0, os.path.join(ROOT, "s-blas_amd"))
+    import argparse
+    import sblas
+    args = argparse.Namespace(matrix=matrix, grid=6, scale=10, nrows=0, heavy=96, light=9, cols="random")
+    W = bench.Workload(args, sblas)
+    if matrix == "rmat":
+        rp, col, val = sblas.gen_rmat(10, 16, seed=50)
+    else:
+        rp, col, val = sblas.gen_stencil3d(6, 6, 6, int(matrix[7:]), seed=49)
+    assert W.n == len(rp) - 1 and W.nnz == rp[-1] and not W.default
+    for a, b in ((0, W.n), (3, 17), (W.n - 5, W.n)):
+        c, v = W.rows(a, b)
+        assert (c == col[rp[a]:rp[b]]).all() and (v == val[rp[a]:rp[b]]).all()
+    assert matrix[:4] in W.describe("auto").lower() or "r-mat" in W.describe("auto").lower()

@@ -299,3 +299,53 @@ def test_overlap_halves_place_every_row_once(m, g):
     gB = np.concatenate([s[sA:sA + sB] for s in slices])
     y = np.concatenate([place(gA, sA, rows_a), place(gB, sB, m - rows_a)])
     assert np.array_equal(y, np.arange(m))
+
+
+@pytest.mark.parametrize("points", [7, 27])
+def test_stencil3d_generator(sb, points):
+    """sblas_gen_stencil3d: natural-order 3-D stencil, every neighbour inside
+    the grid present exactly once, columns ascending, symmetric pattern,
+    diagonally dominant, deterministic."""
+    nx, ny, nz = 5, 4, 3
+    rp, col, val = sb.gen_stencil3d(nx, ny, nz, points, seed=7)
+    n = nx * ny * nz
+    assert len(rp) == n + 1
+    A = np.zeros((n, n))
+    for r in range(n):
+        c = col[rp[r]:rp[r + 1]]
+        assert np.all(np.diff(c) > 0)
+        A[r, c] = val[rp[r]:rp[r + 1]]
+        i, j, k = r % nx, (r // nx) % ny, r // (nx * ny)
+        want = []
+        for dk in (-1, 0, 1):
+            for dj in (-1, 0, 1):
+                for di in (-1, 0, 1):
+                    if points == 7 and abs(di) + abs(dj) + abs(dk) > 1:
+                        continue
+                    if 0 <= i + di < nx and 0 <= j + dj < ny and 0 <= k + dk < nz:
+                        want.append(r + (dk * ny + dj) * nx + di)
+        assert list(c) == want
+    assert np.array_equal(A != 0, (A != 0).T)
+    off = np.abs(A).sum(axis=1) - np.abs(np.diag(A))
+    assert np.allclose(np.diag(A), 1.0 + off)
+    rp2, col2, val2 = sb.gen_stencil3d(nx, ny, nz, points, seed=7)
+    assert np.array_equal(col, col2) and np.array_equal(val, val2)
+
+
+def test_rmat_generator(sb):
+    """sblas_gen_rmat: 2^scale rows, sorted distinct columns per row, at most
+    edge_factor * 2^scale entries after merging duplicates, a power-law row
+    length spread, deterministic for a seed."""
+    scale, ef = 12, 16
+    rp, col, val = sb.gen_rmat(scale, ef, seed=3)
+    n = 1 << scale
+    assert len(rp) == n + 1 and 0 < rp[-1] <= ef * n
+    assert np.all((col >= 0) & (col < n))
+    for r in range(n):
+        assert np.all(np.diff(col[rp[r]:rp[r + 1]]) > 0)
+    lens = np.diff(rp)
+    assert lens.max() > 20 * lens.mean()          # heavy rows exist
+    assert (lens == 0).sum() > 0                    # and empty ones
+    assert np.all(val > 0)                          # U[0,1) draws, merged by summing
+    rp2, col2, val2 = sb.gen_rmat(scale, ef, seed=3)
+    assert np.array_equal(rp, rp2) and np.array_equal(col, col2) and np.array_equal(val, val2)

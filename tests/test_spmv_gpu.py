@@ -275,7 +275,24 @@ def test_spmv_out_of_core(torch_cuda, sb, orc, chunk, nstreams, ngpu, beta_zero)
     check(orc, rp, col, val, x, alpha, beta, y0, y)
 
 
-@pytest.mark.parametrize("case", ["random_small", "prefix", "banded_runs", "diagonal", "override"])
+@pytest.mark.parametrize("kind", ["stencil7", "stencil27", "rmat"])
+def test_suitesparse_class(torch_cuda, sb, orc, algo, kind):
+    """Every kernel on the SuiteSparse-class generators bench.py --matrix
+    offers: 3-D 7- and 27-point stencils (banded, structured) and an R-MAT
+    power-law graph (rows of 0 to ~1,000 entries, hot columns)."""
+    if kind == "rmat":
+        rp, col, val = sb.gen_rmat(11, 16, seed=5)
+    else:
+        rp, col, val = sb.gen_stencil3d(13, 11, 9, int(kind[7:]), seed=6)
+    n = len(rp) - 1
+    x = orc.gen_vector(n, 43)
+    y0 = orc.gen_vector(n, 45)
+    alpha, beta = orc.alpha_beta()
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, alpha, beta, y0)
+    check(orc, rp, col, val, x, alpha, beta, y0, got)
+
+
+@pytest.mark.parametrize("case", ["random_small", "prefix", "banded_runs", "diagonal", "override", "stencil27"])
 def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
     """SBLAS_SPMV_AUTO (sblas_csr_pick): coalescing columns -> row split;
     scattered columns under 2M nonzeros -> panel; SBLAS_AUTO overrides.  The
@@ -294,6 +311,10 @@ def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
         starts = np.stack([np.arange(n) % 5990, 6000 + np.arange(n) % 5990, 12000 + np.arange(n) % 7990], 1)
         col = (starts[:, :, None] + np.arange(8)[None, None, :]).reshape(-1).astype(np.int32)
         val = rng.standard_normal(int(rp[-1]))
+        want_algo = sb.ROWSPLIT
+    elif case == "stencil27":  # 3-D FEM-block pattern: neighbouring rows share x lines
+        rp, col, val = sb.gen_stencil3d(30, 30, 22, 27, seed=6)
+        n = len(rp) - 1
         want_algo = sb.ROWSPLIT
     elif case == "diagonal":  # one entry per row: locality across rows
         rp = np.arange(n + 1, dtype=np.int64)
