@@ -1378,9 +1378,20 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         for (int k = 0; k < 8; ++k)
             for (size_t j = 0; j < wleft[k].size(); j += 2)
                 q[k].push_back({wleft[k][j], j + 1 < wleft[k].size() ? wleft[k][j + 1] : -1});
+        // leftover light sub-items: two to an item only as far as the grid
+        // needs it; the rest run alone (both teams on one sub-item), so an
+        // item never carries twice a light sub-item's work while workgroups
+        // idle (power-law matrices: most rows light, few heavy sub-items)
+        long long items_now = 0;
+        for (int k = 0; k < 8; ++k) items_now += (long long)q[k].size();
+        const long long left = (long long)(nsub.size() - ni);
+        const long long free_slots = std::max<long long>(0, (long long)resident - items_now);
+        long long npairs = std::max<long long>(0, left - free_slots);  // items = left - npairs <= free
+        if (2 * npairs > left) npairs = left / 2;
         for (int t = 0; ni < nsub.size(); ++t) {
             const int a0 = nsub[ni++];
-            const int a1 = ni < nsub.size() ? nsub[ni++] : -1;
+            const int a1 = (npairs > 0 && ni < nsub.size()) ? nsub[ni++] : -1;
+            if (a1 >= 0) --npairs;
             q[t % 8].push_back({a0, a1});
         }
     }

@@ -15,6 +15,8 @@ No GPU needed.  Usage: python3 xs_plan_model.py [--n 2000000] [--world 1]
 import argparse
 import heapq
 import math
+import os
+import sys
 
 import numpy as np
 
@@ -39,7 +41,9 @@ def config2_rowptr(n, heavy=96, light=9, world=1):
     return rp
 
 
-def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None):
+def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid"):
+    """pairing: leftover light sub-items two to an item only as far as the
+    grid needs ("grid", the planner since round 3) or always ("always")."""
     m, nnz = len(rp) - 1, int(rp[-1])
     nmib = (n * 8 + (1 << 20) - 1) >> 20
     q = max(1, (math.ceil(n / ((1 << 18) - 1)) + 7) // 8, (nmib + 7) // 8)
@@ -135,9 +139,18 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None):
             for j in range(0, len(left[k]), 2):
                 queues[k].append(left[k][j] + (left[k][j + 1] if j + 1 < len(left[k]) else 0))
         t = 0
+        left = len(nsub) - ni
+        free = max(0, CUS - sum(map(len, queues)))
+        npairs = max(0, left - free) if pairing == "grid" else left // 2
+        npairs = min(npairs, left // 2)
         while ni < len(nsub):
-            queues[t % 8].append(nsub[ni] + (nsub[ni + 1] if ni + 1 < len(nsub) else 0))
-            ni += 2
+            if npairs > 0 and ni + 1 < len(nsub):
+                queues[t % 8].append(nsub[ni] + nsub[ni + 1])
+                ni += 2
+                npairs -= 1
+            else:
+                queues[t % 8].append(nsub[ni])
+                ni += 1
             t += 1
     # 32 CUs per XCD claim from their own queue first (greedy list schedule)
     busiest = 0.0
@@ -157,9 +170,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2_000_000)
     ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--rmat", type=int, default=0, help="model an R-MAT graph of this scale instead")
     args = ap.parse_args()
     rp = config2_rowptr(args.n, world=args.world)
-    for mode, rc in (("paired", None), ("solo", None), ("unpaired", None), ("paired", 4096), ("paired", 6144)):
+    if args.rmat:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+        import sblas
+        rp, _, _ = sblas.gen_rmat(args.rmat, 16, seed=50)
+        n = len(rp) - 1
+        for pairing in ("always", "grid"):
+            print(pairing, plan(rp, n, "paired", pairing=pairing))
+        return
+    for mode, rc in (("paired", None), ("solo", None), ("unpaired", None)):
         print(plan(rp, args.n, mode, rows_cap=rc))
 
 
