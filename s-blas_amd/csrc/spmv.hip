@@ -52,7 +52,17 @@ __device__ __forceinline__ void store_y(double *p, double v)
     else *p = v;
 }
 
-template <bool kBeta, bool kSc1 = false>
+// kSeq (default; SBLAS_RS_SEQ=0 selects the earlier form for the row-split
+// launch): the stream block's entries are taken lane-consecutively
+// -- thread t holds entries j0 + t + 256k, so one gather instruction of a
+// wave covers 64 CONSECUTIVE entries and the TA merges lanes whose columns
+// share an x line (a banded / stencil row's runs of neighbouring columns) --
+// with 4-B / 8-B col / val loads, instead of 16-B loads of 4 consecutive
+// entries per lane, whose gather instructions sample every 4th entry.
+// Measured (row split, cold, `profiles/r03/rowsplit_seq/`): 27-point stencil
+// 0.549 -> 0.615 of 8 TB/s, 7-point 0.577 -> 0.625, config 2 prefix columns
+// 0.674 -> 0.708, random 0.208 -> 0.217.
+template <bool kBeta, bool kSc1 = false, bool kSeq = true>
 __device__ __forceinline__ void rowsplit_block(
     const RowBlock blk, const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x, double alpha, double beta,
@@ -66,7 +76,26 @@ __device__ __forceinline__ void rowsplit_block(
         const int r0 = blk.row, r1 = blk.a;
         const int j0 = rowptr[r0], j1 = rowptr[r1];
         const int base = j0 & ~3;
-        const int ngroups = (j1 - base + 3) >> 2;
+        const int ngroups = kSeq ? 0 : (j1 - base + 3) >> 2;
+        if (kSeq && j1 > j0) {  // block-uniform
+            constexpr int K = kRsBlockNnz / kRsThreads;
+            static_assert(K * kRsThreads == kRsBlockNnz, "a stream block is K entries per thread");
+            int c[K];
+            double v[K], xv[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {  // clamped, unconditional (see below)
+                const int e = min(j0 + k * kRsThreads + tid, j1 - 1);
+                c[k] = __builtin_nontemporal_load(col + e);
+                v[k] = __builtin_nontemporal_load(val + e);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) xv[k] = x[c[k]];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int e = j0 + k * kRsThreads + tid;
+                if (e < j1) prod[e - j0] = v[k] * xv[k];
+            }
+        }
         // Two 4-element groups per thread per pass, all loads issued before any
         // use.  Gathers are UNCONDITIONAL: the 16-B over-read window only ever
         // holds neighbouring rows' columns or the zeroed padding, so every index
@@ -149,7 +178,7 @@ __device__ __forceinline__ void rowsplit_block(
     }
 }
 
-template <bool kBeta>
+template <bool kBeta, bool kSeq = true>
 __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
@@ -158,8 +187,8 @@ __global__ __launch_bounds__(kRsThreads) void k_spmv_rowsplit(
 {
     __shared__ double prod[kRsBlockNnz + 8];
     __shared__ double wsum[kRsThreads / 64];
-    rowsplit_block<kBeta>(blocks[blockIdx.x], rowptr, col, val, x, alpha, beta, y, partial, prod,
-                          wsum);
+    rowsplit_block<kBeta, false, kSeq>(blocks[blockIdx.x], rowptr, col, val, x, alpha, beta, y, partial, prod,
+                                       wsum);
 }
 
 template <bool kBeta>
@@ -266,14 +295,20 @@ int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
 {
     if (!A.rs.ready) return SBLAS_ERR_INVALID;
     if (A.rs.nblocks == 0) return SBLAS_OK;
+    static const int seq = [] {
+        const char *e = getenv("SBLAS_RS_SEQ");
+        return e ? atoi(e) : 1;
+    }();
     if (beta != 0.0) {
-        SBLAS_LAUNCH(k_spmv_rowsplit<true>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+        auto kern = seq ? k_spmv_rowsplit<true, true> : k_spmv_rowsplit<true, false>;
+        SBLAS_LAUNCH(kern, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
                            A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
         if (A.rs.nlong)
             SBLAS_LAUNCH(k_spmv_long_finalize<true>, dim3((A.rs.nlong + 63) / 64), dim3(64),
                                0, s, A.rs.long_rows, A.rs.nlong, A.rs.partial, alpha, beta, y);
     } else {
-        SBLAS_LAUNCH(k_spmv_rowsplit<false>, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
+        auto kern = seq ? k_spmv_rowsplit<false, true> : k_spmv_rowsplit<false, false>;
+        SBLAS_LAUNCH(kern, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
                            A.rowptr, A.col, A.val, x, A.rs.blocks, alpha, beta, y, A.rs.partial);
         if (A.rs.nlong)
             SBLAS_LAUNCH(k_spmv_long_finalize<false>, dim3((A.rs.nlong + 63) / 64), dim3(64),
