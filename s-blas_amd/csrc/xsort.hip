@@ -1125,41 +1125,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         if (best_subs < 0 || subs < best_subs) best_subs = subs;
         cap *= 1.02;
     }
-    // SBLAS_XS_TAILFRAC (permille, opt-in): the last light ranges holding
-    // ~that share of the entries are cut into 8 small ranges each and queued
-    // after every regular item as dynamic solo items, so workgroups that
-    // finish early (the XCDs dispatched first, the faster ones) take the
-    // tail instead of idling while the slowest XCD finishes
-    std::vector<char> small_range;
-    if (const char *e = getenv("SBLAS_XS_TAILFRAC"); e && P.pair && P.dyn && atoi(e) > 0) {
-        const long long target = nnz * std::min(500, atoi(e)) / 1000;
-        std::vector<char> cutme(ranges.size(), 0);
-        long long acc = 0;
-        for (size_t i = ranges.size(); i-- > 0 && acc < target;)
-            if (!ranges[i].wide && ranges[i].nrows >= 16) {
-                cutme[i] = 1;
-                acc += rp[ranges[i].row0 + ranges[i].nrows] - rp[ranges[i].row0];
-            }
-        std::vector<XsRange> out;
-        for (size_t i = 0; i < ranges.size(); ++i) {
-            if (!cutme[i]) {
-                out.push_back(ranges[i]);
-                small_range.push_back(0);
-                continue;
-            }
-            const XsRange &R = ranges[i];
-            for (int k = 0; k < 8; ++k) {
-                XsRange S = R;
-                S.row0 = R.row0 + (int)((long long)R.nrows * k / 8);
-                S.nrows = R.row0 + (int)((long long)R.nrows * (k + 1) / 8) - S.row0;
-                if (S.nrows <= 0) continue;
-                out.push_back(S);
-                small_range.push_back(1);
-            }
-        }
-        ranges.swap(out);
-    }
-    small_range.resize(ranges.size(), 0);
     const int I = (int)ranges.size();
     if ((long long)I >= (1LL << 23)) {
         set_error("xsort: %d row ranges (> 2^23)", I);
@@ -1347,7 +1312,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
 
     mark("pass2");
     // sub-items, wide partial slots, then items (pairs) in XCD queues
-    std::vector<int> wide, nsub, ssub;  // ssub: SBLAS_XS_TAILFRAC's small light ranges
+    std::vector<int> wide, nsub;
     std::vector<std::vector<int>> wsub(8);
     long long pbase = 0;
     std::vector<int2> rtasks;  // fused reduce: (range, first row) per kXsThreads rows
@@ -1361,8 +1326,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             for (int r0 = 0; r0 < R.nrows; r0 += kXsThreads) rtasks.push_back(make_int2(i, r0));
             wide.push_back(i);
             for (int k = 0; k < 8; ++k) wsub[k].push_back((i << 8) | (k + 1));
-        } else if (small_range[(size_t)i]) {
-            ssub.push_back(i << 8);
         } else {
             nsub.push_back(i << 8);
         }
@@ -1432,7 +1395,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             q[t % 8].push_back({a0, a1});
         }
     }
-    for (size_t j = 0; j < ssub.size(); ++j) q[j % 8].push_back({ssub[j], -1});  // after every regular item
     P.nranges = I;
     P.nwide = (int)wide.size();
     P.nchunks = nchunks;

@@ -76,24 +76,21 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
     (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
     (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_K24": "0"}),
     (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2"}), (5, {"SBLAS_XS_TAIL": "1"}),
-    (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (1, {"SBLAS_RS_SEQ": "0"}),
-    (5, {"SBLAS_XS_TAILFRAC": "50"})],
+    (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (1, {"SBLAS_RS_SEQ": "0"})],
     ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused",
-         "xsort_k32", "xsort_k24_u2", "xsort_tail", "xsort_tail_allwide", "xsort_solo", "rowsplit_vec4", "xsort_tailfrac"])
+         "xsort_k32", "xsort_k24_u2", "xsort_tail", "xsort_tail_allwide", "xsort_solo", "rowsplit_vec4"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    launches = 25 if (algo == 5 and (not env or env in ({"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"},
-                                                        {"SBLAS_XS_TAILFRAC": "50"}))
+    launches = 25 if (algo == 5 and (not env or env in ({"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}))
                       and not cfg2["prefix"]) else 1
     _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
 
 
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"},
-                                 {"SBLAS_XS_TAILFRAC": "50"}],
-                         ids=["default", "batch", "tail", "solo", "tailfrac"])
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}],
+                         ids=["default", "batch", "tail", "solo"])
 def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world, rank, env):
     """A rank's cyclic slice of config 2 (bench.py's N > 1 share) with the
     persistent column-sorted kernel and its opt-in batch form (SBLAS_XS_BATCH=1,
