@@ -190,7 +190,7 @@ struct SpmmPlan {
     unsigned *tt_key = nullptr;          // per slot: row
     double *tt_val = nullptr;            // per slot: value
     int *tt_loff = nullptr;              // [nlist + 1] group offsets of the lists
-    double fill_thresh = 0.25;
+    double fill_thresh = 0.08;  // MFMA tile when a 16-row block fills >= 8% of its column union
     bool ready = false;
 };
 

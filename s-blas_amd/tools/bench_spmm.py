@@ -120,6 +120,10 @@ def main():
     ap.add_argument("--blocky", type=int, default=0,
                     help="instead of the rail4284 shape: 16-row blocks each dense (~90%%) over "
                          "BLOCKY random columns (an FEM-like matrix where MFMA tiles apply)")
+    ap.add_argument("--stencil", type=int, default=0,
+                    help="instead of the rail4284 shape: a 3-D 27-point stencil on a STENCIL^3 grid "
+                         "(sblas_gen_stencil3d; the SuiteSparse-class banded case)")
+    ap.add_argument("--points", type=int, default=27, choices=[7, 27])
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true",
@@ -149,7 +153,11 @@ def main():
             dist.init_process_group("gloo")
 
     m, k, n = args.mrows, args.kcols, args.ncols
-    if args.blocky:
+    if args.stencil:
+        g = args.stencil
+        rp, col, _ = sblas.gen_stencil3d(g, g, g, args.points, seed=49)
+        m = k = len(rp) - 1
+    elif args.blocky:
         rp, col = blocky(m, k, args.blocky, 44)
         m = len(rp) - 1
     else:
@@ -240,16 +248,18 @@ def main():
             "kernel_ms_max_over_ranks": round(kern_max, 4),
             "kernel_only_gflops": round(2.0 * nnz * n / kern_max / 1e6, 3),
             "higher_is_better": True, "scaling": "strong", "dtype": "f64",
-            "data": "synthetic rail4284-shaped (DESIGN.md)",
+            "data": "synthetic (DESIGN.md)",
             "config": {"workload": "C = -0.7*A*B + 0.8*C", "m": m, "k": k, "nnz": nnz, "ncols": n,
                        "b_layout": "row" if lay == 1 else "col",
-                       "structure": f"blocky{args.blocky}" if args.blocky
-                       else "rail4284-shaped uniform random",
+                       "structure": (f"{args.points}-point 3-D stencil {args.stencil}^3" if args.stencil
+                                     else f"blocky{args.blocky}" if args.blocky
+                                     else "rail4284-shaped uniform random"),
+                       "mfma_blocks": int(op.A.spmm_info()[0]) if hasattr(op.A, "spmm_info") else None,
                        "partition": ("single GPU" if world == 1 else
                                      "whole-row blocks by nnz, B replicated, C all-gathered"
                                      if args.split == "rows" else
                                      "A replicated, B/C column slices, C all-gathered"),
-                       "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.25")},
+                       "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.08")},
             "roofline": {"bound": "hbm", "achieved": round(abytes / kern_max / 1e6, 1), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(abytes / kern_max / 1e6 / 8000.0, 4)},
             "gbps_brow": round(nnz * n * 8 / kern_max / 1e6 / max(world, 1), 1),
@@ -259,7 +269,7 @@ def main():
         }
         if check is not None:
             out["check_vs_oracle"] = check
-        if world == 1 and not args.blocky and lay == 1:
+        if world == 1 and not args.blocky and not args.stencil and lay == 1:
             out["roofline"]["traffic"] = pmc_traffic_spmm()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_spmm(m, n, rp, col, val, Bh, C0h.T)
