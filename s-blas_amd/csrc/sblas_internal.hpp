@@ -152,11 +152,7 @@ struct SpmmPlan {
     int *mblock = nullptr;     // [nmfma] 16-row block index
     int *mchunk = nullptr;     // [nmfma+1] offsets in 4-column chunks
     int *ucol = nullptr;       // [4*chunks] union columns (padded)
-    double *atile = nullptr;   // [chunks*64] A fragments, lane-major (SBLAS_SPMM_MFMA_DENSE=1)
-    unsigned long long *amask = nullptr;  // [chunks] packed form (default): lanes holding a nonzero
-    int *aoff = nullptr;       // [chunks+1] offsets of each chunk's packed values
-    double *avals = nullptr;   // the chunks' nonzeros in lane order
-    bool mfma_dense = false;   // dense 16 x 4 fragments instead of the packed form
+    double *atile = nullptr;   // [chunks*64] A fragments, lane-major
     int nsparse = 0;           // rows handled by the row-wave kernel
     long long sparse_nnz = 0;  // their nonzeros
     int *srows = nullptr;

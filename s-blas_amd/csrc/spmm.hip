@@ -187,78 +187,6 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(
     }
 }
 
-// Packed-A form (default): a chunk's 16 x 4 fragment travels as a 64-bit lane
-// mask and its nonzeros in lane order (a stencil's blocks fill 8-17% of
-// their union, so the dense fragments were 6-12x the CSR bytes of A, the
-// largest stream of the kernel); lane l rebuilds its operand from the mask's
-// popcount below l, holes are exact zeros as before, so the products and
-// their MFMA order are the dense tile's.  Two chunks per step, every load of
-// both issued before the first MFMA.
-template <bool kBeta>
-__global__ __launch_bounds__(256) void k_spmm_mfma_packed(
-    const int *__restrict__ mblock, const int *__restrict__ mchunk, const int *__restrict__ ucol,
-    const unsigned long long *__restrict__ amask, const int *__restrict__ aoff,
-    const double *__restrict__ avals, int nmfma, const double *__restrict__ B, long long ldb,
-    int m, int n, int ngrp, double alpha, double beta, double *__restrict__ C, long long ldc)
-{
-    const int lane = threadIdx.x & 63;
-    const long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w >= (long long)nmfma * ngrp) return;
-    const int q = (int)(w / ngrp), g = (int)(w % ngrp);
-    const int r0 = mblock[q] * 16;
-    const int kq = lane >> 4, jq = lane & 15;
-    const unsigned long long below = lane ? (~0ULL >> (64 - lane)) : 0ULL;
-    v4d acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-    int cj[4];
-    bool live[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        cj[t] = g * 64 + t * 16 + jq;
-        live[t] = cj[t] < n;
-        if (!live[t]) cj[t] = 0;
-    }
-    const int c0 = mchunk[q], c1 = mchunk[q + 1];
-    auto operand = [&](int c) {
-        const unsigned long long mk = amask[c];
-        const bool has = (mk >> lane) & 1ULL;
-        const int idx = aoff[c] + __builtin_popcountll(mk & below);
-        return has ? avals[idx] : 0.0;
-    };
-    for (int c = c0; c < c1; c += 2) {  // wave-uniform
-        const bool two = c + 1 < c1;
-        const int cn = two ? c + 1 : c;
-        const double a0 = operand(c), a1 = operand(cn);
-        const long long br0 = (long long)ucol[c * 4 + kq] * ldb;
-        const long long br1 = (long long)ucol[cn * 4 + kq] * ldb;
-        double b0[4], b1[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            b0[t] = live[t] ? B[br0 + cj[t]] : 0.0;
-            b1[t] = live[t] ? B[br1 + cj[t]] : 0.0;
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[t], acc[t], 0, 0, 0);
-        if (two) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[t], acc[t], 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        if (!live[t]) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = r0 + kq + 4 * r;
-            if (row < m) {
-                double *o = C + (long long)cj[t] * ldc + row;
-                *o = kBeta ? alpha * acc[t][r] + beta * *o : alpha * acc[t][r];
-            }
-        }
-    }
-}
-
 // ---- L2-slice SpMM (few rows, tall B) -------------------------------------
 // With m small (rail4284: 4,284 rows) and B far larger than the chip's 32 MB
 // of L2 (559 MB), every nonzero's 512-B B row comes over the fabric: the
@@ -1371,8 +1299,6 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     }
     std::vector<int> mblock, mchunk{0}, ucol, srows;
     std::vector<double> atile;
-    std::vector<char> aset;  // atile slots holding a nonzero of A (the packed form's mask)
-    P.mfma_dense = getenv("SBLAS_SPMM_MFMA_DENSE") && atoi(getenv("SBLAS_SPMM_MFMA_DENSE")) != 0;
     P.sparse_nnz = 0;
 
     // 16-row blocks: the distinct columns of each (sorted) decide whether the
@@ -1404,14 +1330,12 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
         const int nch = ((int)U.size() + 3) / 4;
         const size_t t0 = atile.size();
         atile.resize(t0 + (size_t)nch * 64, 0.0);
-        aset.resize(t0 + (size_t)nch * 64, 0);
         for (int c = 0; c < nch * 4; ++c) ucol.push_back(c < (int)U.size() ? U[c] : U[0]);
         for (int r = r0; r < r1; ++r)
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 const int k = (int)(std::lower_bound(U.begin(), U.end(), hcol[j]) - U.begin());
                 // lane l of chunk k/4 holds A[l & 15][4*(k/4) + (l >> 4)]
                 atile[t0 + (size_t)(k / 4) * 64 + (size_t)((k % 4) * 16 + (r - r0))] += hval[j];
-                aset[t0 + (size_t)(k / 4) * 64 + (size_t)((k % 4) * 16 + (r - r0))] = 1;
             }
         mblock.push_back(b);
         mchunk.push_back(mchunk.back() + nch);
@@ -1427,25 +1351,7 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     SBLAS_TRY(up(&P.mblock, mblock));
     SBLAS_TRY(up(&P.mchunk, mchunk));
     SBLAS_TRY(up(&P.ucol, ucol));
-    if (P.mfma_dense) {
-        SBLAS_TRY(up(&P.atile, atile));
-    } else {
-        const size_t nchunk = atile.size() / 64;
-        std::vector<unsigned long long> amask(nchunk, 0);
-        std::vector<int> aoff(nchunk + 1, 0);
-        std::vector<double> avals;
-        for (size_t c = 0; c < nchunk; ++c) {
-            for (int l = 0; l < 64; ++l)
-                if (aset[c * 64 + (size_t)l]) {
-                    amask[c] |= 1ULL << l;
-                    avals.push_back(atile[c * 64 + (size_t)l]);
-                }
-            aoff[c + 1] = (int)avals.size();
-        }
-        SBLAS_TRY(up(&P.amask, amask));
-        SBLAS_TRY(up(&P.aoff, aoff));
-        SBLAS_TRY(up(&P.avals, avals));
-    }
+    SBLAS_TRY(up(&P.atile, atile));
     SBLAS_TRY(up(&P.srows, srows));
     // L2-slice form: few rows (every XCD holds all m partial rows), B much
     // taller than the L2s (k >= 2^17: >= 64 MiB at n = 64), no MFMA blocks.
@@ -1488,9 +1394,6 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.mchunk);
     (void)hipFree(P.ucol);
     (void)hipFree(P.atile);
-    (void)hipFree(P.amask);
-    (void)hipFree(P.aoff);
-    (void)hipFree(P.avals);
     (void)hipFree(P.srows);
     (void)hipFree(P.l2_rp);
     (void)hipFree(P.l2_col);
@@ -1690,20 +1593,14 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     if (P.ready && P.nmfma > 0) {
         const long long waves = (long long)P.nmfma * nslab;
         const unsigned nb = (unsigned)((waves + 3) / 4);
-        if (P.mfma_dense) {
-            if (beta != 0.0)
-                hipLaunchKernelGGL(k_spmm_mfma<true>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
-                                   P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
-                                   (long long)ldc);
-            else
-                hipLaunchKernelGGL(k_spmm_mfma<false>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
-                                   P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
-                                   (long long)ldc);
-        } else {
-            auto kern = beta != 0.0 ? k_spmm_mfma_packed<true> : k_spmm_mfma_packed<false>;
-            hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol, P.amask, P.aoff,
-                               P.avals, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C, (long long)ldc);
-        }
+        if (beta != 0.0)
+            hipLaunchKernelGGL(k_spmm_mfma<true>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
+                               P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
+                               (long long)ldc);
+        else
+            hipLaunchKernelGGL(k_spmm_mfma<false>, dim3(nb), dim3(256), 0, s, P.mblock, P.mchunk, P.ucol,
+                               P.atile, P.nmfma, Brow, ldr, A.m, n, nslab, alpha, beta, C,
+                               (long long)ldc);
     }
     SBLAS_HIP(hipGetLastError());
     return SBLAS_OK;

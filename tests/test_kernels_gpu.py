@@ -771,17 +771,12 @@ def block_dense_csr(rng, nblk, width, k, sparse_tail=0):
     return rp, col, rng.standard_normal(int(rp[-1]))
 
 
-@pytest.mark.parametrize("form", ["packed", "dense"])
 @pytest.mark.parametrize("fill", ["default", "0", "2"])
 @pytest.mark.parametrize("ncols", [64, 40, 130])
-def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols, form):
-    """MFMA B-panel tiles (packed A fragments by default, SBLAS_SPMM_MFMA_DENSE=1
-    the dense ones) against the oracle."""
+def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols):
     torch = torch_cuda
     if fill != "default":
         monkeypatch.setenv("SBLAS_SPMM_MFMA_FILL", fill)
-    if form == "dense":
-        monkeypatch.setenv("SBLAS_SPMM_MFMA_DENSE", "1")
     rng = np.random.default_rng(ncols)
     k = 3000
     rp, col, val = block_dense_csr(rng, 12, 37, k, sparse_tail=21)  # m = 213: partial last block
