@@ -164,14 +164,29 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(
         live[t] = cj[t] < n;
         if (!live[t]) cj[t] = 0;
     }
-    for (int c = mchunk[q]; c < mchunk[q + 1]; ++c) {
-        const double a = atile[(long long)c * 64 + lane];
-        const long long brow = (long long)ucol[c * 4 + kq] * ldb;
-        double b[4];
+    // kU chunks per step, every load of the step issued before its first MFMA
+    // (the union-column -> B-row loads are a dependent pair per chunk)
+    constexpr int kU = 2;
+    const int c0 = mchunk[q], c1 = mchunk[q + 1];
+    for (int c = c0; c < c1; c += kU) {  // wave-uniform
+        double a[kU], b[kU][4];
+        long long brow[kU];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) b[t] = live[t] ? B[brow + cj[t]] : 0.0;
+        for (int u = 0; u < kU; ++u) {
+            const int cu = min(c + u, c1 - 1);
+            a[u] = c + u < c1 ? atile[(long long)cu * 64 + lane] : 0.0;
+            brow[u] = (long long)ucol[cu * 4 + kq] * ldb;
+        }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[t], acc[t], 0, 0, 0);
+        for (int u = 0; u < kU; ++u)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) b[u][t] = live[t] ? B[brow[u] + cj[t]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (c + u >= c1) break;  // wave-uniform: no MFMA for a padding step
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][t], acc[t], 0, 0, 0);
+        }
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
