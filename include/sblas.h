@@ -189,9 +189,14 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz,
  * flags (deterministic sums), 2 = level-set (rows grouped by level,
  * findlevel.h:71-147; one synchronisation per level; built on the first
  * algo-2 solve; x bit-identical to algo 1), 3 = the pull executor with its
- * tickets in level order (same analysis; x bit-identical to algo 1). */
+ * tickets in level order (same analysis; x bit-identical to algo 1),
+ * 4 = AUTO: the pull executor in level order when at least a quarter of the
+ * rows depend on a row of their own 64-row wave (stencil / FEM triangles),
+ * else in natural order (decided once per handle by a device probe). */
 int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x,
                      void *stream);
+/* algo 4's choice for this handle (1 or 3), probing on first use. */
+int sblas_trsv_pick(sblas_trsv T, void *stream, int *algo);
 int sblas_trsv_levels(sblas_trsv T, int *nlevel);
 int sblas_trsv_destroy(sblas_trsv T);
 /* SpTRSM, rhs right-hand sides (sptrsm_syncfree_cuda_executor,

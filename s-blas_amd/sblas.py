@@ -87,6 +87,7 @@ _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
 _sig("sblas_csr_transpose", _i, _p, _p, _p, _p, _p)
 _sig("sblas_trsv_create", _i, _p, _i, _i, _i, _p, _p, _p, _i, _p)
 _sig("sblas_trsv_solve", _i, _p, _i, _p, _p, _p)
+_sig("sblas_trsv_pick", _i, _p, _p, _p)
 _sig("sblas_trsv_levels", _i, _p, _p)
 _sig("sblas_trsv_destroy", _i, _p)
 _sig("sblas_trsv_mgpu_solve", _i, _p, _p, _p, _i, _i, _i, _p, _p, _i, _p)
@@ -598,6 +599,12 @@ class DeviceTRSV:
 
     def solve(self, algo: int, b_ptr: int, x_ptr: int, stream=None) -> None:
         check(lib.sblas_trsv_solve(self.h, algo, b_ptr, x_ptr, stream), "trsv_solve")
+
+    def pick(self, stream=None) -> int:
+        """algo 4 (AUTO)'s ticket order for this handle: 1 natural, 3 level order."""
+        a = C.c_int(0)
+        check(lib.sblas_trsv_pick(self.h, stream, C.byref(a)), "trsv_pick")
+        return a.value
 
     def solve_rhs(self, rhs: int, b_ptr: int, x_ptr: int, stream=None) -> None:
         """SpTRSM: b, x device n x rhs row-major."""

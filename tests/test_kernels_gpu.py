@@ -362,6 +362,47 @@ def test_sptrsv_kat(torch_cuda, sb, orc, name, sub, algo):
     T.close()
 
 
+@pytest.mark.parametrize("kind", ["stencil27", "stencil7", "banded"])
+def test_sptrsv_auto_order(torch_cuda, sb, orc, kind):
+    """algo 4 (AUTO): level-ordered tickets for a stencil's lower triangle
+    (row i depends on row i - 1, a chain through every wave), natural order
+    for a banded random triangle; x bit-identical to algo 1 and within the
+    bound of the exact solution."""
+    torch = torch_cuda
+    if kind == "banded":
+        cp, ri, v = sb.gen_lower_banded(30000, 4, 5000, 11)
+        n = len(cp) - 1
+        want = 1
+    else:
+        g = 24
+        srp, scol, sval = sb.gen_stencil3d(g, g, g, int(kind[7:]), seed=49)
+        n = len(srp) - 1
+        srow = np.repeat(np.arange(n), np.diff(srp))
+        keep = scol >= srow
+        cp = np.zeros(n + 1, np.int32)
+        cp[1:] = np.cumsum(np.bincount(srow[keep], minlength=n))
+        ri = np.ascontiguousarray(scol[keep]).astype(np.int32)
+        v = np.ascontiguousarray(sval[keep])
+        want = 3
+    xref = np.floor(sb.gen_vector(n, 48) * 10.0) + 1.0
+    cols = np.repeat(np.arange(n), np.diff(cp))
+    b = np.bincount(ri, weights=v * xref[cols], minlength=n)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, v, b)]
+    T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 0)
+    try:
+        assert T.pick() == want
+        xs = []
+        for algo in (4, 1):
+            xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+            T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+            torch.cuda.synchronize()
+            xs.append(xd.cpu().numpy())
+        assert np.array_equal(xs[0], xs[1])
+        assert np.abs(xs[0] - xref).sum() / np.abs(xref).sum() < 1e-12
+    finally:
+        T.close()
+
+
 @pytest.mark.parametrize("sleep", ["0", "16", "-5"])
 @pytest.mark.parametrize("algo", [1, 3])
 def test_sptrsv_pull_backoff(torch_cuda, sb, monkeypatch, algo, sleep):
