@@ -204,7 +204,8 @@ int sblas_trsv_destroy(sblas_trsv T);
  * row-major.  Pull executor; rhs == 1 is sblas_trsv_solve(T, 1, ...). */
 int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream);
 /* SpTRSM with the executor chosen: algo 1 = the pull executor above (opt
- * ignored); algo 0 = the reference's push dataflow (CSC scatter of left sums
+ * ignored); algo 3 = the pull executor with tickets in level order, 4 = 1 or
+ * 3 as sblas_trsv_pick chooses (opt ignored; 2 is invalid); algo 0 = the reference's push dataflow (CSC scatter of left sums
  * with fp64 atomics, sptrsv_syncfree_cuda.h:170-282) with its lane mapping
  * opt: 1 OPT_WARP_NNZ (lanes over a column's entries), 2 OPT_WARP_RHS (lanes
  * over the right-hand sides), 3 OPT_WARP_AUTO (per column: rhs mapping when

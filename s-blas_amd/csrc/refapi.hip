@@ -334,13 +334,13 @@ static int sptrsv_one_device(const int *cscColPtr, const int *cscRowIdx, const d
     // dataflow with that lane mapping (rhs == 1, opt 1: k_trsv_push); any
     // other opt, OPT_WARP_AUTO included (the reference main's choice), picks
     // the fastest executor: the CSR pull executor, its ticket order chosen by
-    // sblas_trsv_solve algo 4 (SpTRSM pull for rhs > 1)
+    // sblas_trsv_solve algo 4 (SpTRSM pull in the same order for rhs > 1)
     const bool push = opt == 1 || opt == 2;
     auto solve = [&]() {
         const double *bb = (const double *)db.p;
         double *xx = (double *)dx.p;
         if (rhs == 1 && opt != 2) return sblas_trsv_solve(T, push ? 0 : 4, bb, xx, nullptr);
-        return sblas_trsv_solve_rhs_opt(T, push ? 0 : 1, opt, rhs, bb, xx, nullptr);
+        return sblas_trsv_solve_rhs_opt(T, push ? 0 : 4, opt, rhs, bb, xx, nullptr);
     };
     int st = solve();  // warm-up
     const double t0 = sblas_get_time();

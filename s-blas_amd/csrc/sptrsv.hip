@@ -437,6 +437,7 @@ struct TrsmArgs {
     unsigned long long *xown;             // this block's x (polled)
     unsigned long long *const *xs;        // [g] peers' x (only q > d used); null if g == 1
     int g, d, o0, nloc, n, rhs, backward, by_row;
+    const int *lrow;                      // level order (algo 3): ticket t is row lrow[t], CSR row t; else null
 };
 
 template <int RP>
@@ -458,8 +459,9 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
         const int t = t0 + slot;
         const bool live = t < P.nloc;
         const int o = P.o0 + (live ? t : 0);
-        const int i = P.backward ? P.n - 1 - o : o;
-        const int ri = P.by_row ? i : (live ? t : 0);
+        const int i = P.lrow ? (live ? P.lrow[t] : 0) : (P.backward ? P.n - 1 - o : o);
+        const int ri = P.lrow ? (live ? t : 0) : (P.by_row ? i : (live ? t : 0));
+        const int bi = P.lrow ? i : ri;  // b's row
         int j0 = 0, jend = 0;
         double diag = 1.0;
         if (live) {
@@ -494,7 +496,7 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
                     }
                 }
                 if (pending && j == jend) {
-                    const double xi = (P.b[(size_t)ri * P.rhs + k] - sum) / diag;
+                    const double xi = (P.b[(size_t)bi * P.rhs + k] - sum) / diag;
                     const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
                     const size_t at = (size_t)i * P.rhs + k;
                     __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1038,17 +1040,16 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     return SBLAS_OK;
 }
 
-int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream)
+// SpTRSM pull: tickets in natural order, or in level order (level = true:
+// the rows of a ticket independent, as algo 3 of sblas_trsv_solve)
+static int trsm_pull(sblas_trsv_s *T, bool level, int rhs, const double *d_b, double *d_x, hipStream_t s)
 {
-    if (!T || !d_b || !d_x || rhs <= 0) return SBLAS_ERR_INVALID;
-    if (rhs == 1) return sblas_trsv_solve(T, 1, d_b, d_x, stream);
-    if (T->n == 0) return SBLAS_OK;
-    DeviceGuard g(T->device);
-    hipStream_t s = (hipStream_t)stream;
+    if (level) SBLAS_TRY(build_levelset(T, s));
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     fill_pending((unsigned long long *)d_x, (long long)T->n * rhs, s);
-    TrsmArgs P{T->rrowptr, T->rcol, T->rval, d_b, (unsigned long long *)d_x, nullptr,
-               1, 0, 0, T->n, T->n, rhs, T->substitution, 1};
+    TrsmArgs P{level ? T->lrp : T->rrowptr, level ? T->lcol : T->rcol, level ? T->lval : T->rval, d_b,
+               (unsigned long long *)d_x, nullptr, 1, 0, 0, T->n, T->n, rhs, T->substitution, 1,
+               level ? T->lrow : nullptr};
     launch_trsm(P, T->ctl, grid_for(T->device), s);
     SBLAS_HIP(hipGetLastError());
     unsigned h[kCtlBytes / 4] = {0};
@@ -1061,15 +1062,31 @@ int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, 
     return SBLAS_OK;
 }
 
+int sblas_trsv_solve_rhs(sblas_trsv T, int rhs, const double *d_b, double *d_x, void *stream)
+{
+    if (!T || !d_b || !d_x || rhs <= 0) return SBLAS_ERR_INVALID;
+    if (rhs == 1) return sblas_trsv_solve(T, 1, d_b, d_x, stream);
+    if (T->n == 0) return SBLAS_OK;
+    DeviceGuard g(T->device);
+    return trsm_pull(T, false, rhs, d_b, d_x, (hipStream_t)stream);
+}
+
 int sblas_trsv_solve_rhs_opt(sblas_trsv T, int algo, int opt, int rhs, const double *d_b,
                              double *d_x, void *stream)
 {
-    if (!T || !d_b || !d_x || rhs <= 0 || algo < 0 || algo > 1) return SBLAS_ERR_INVALID;
+    if (!T || !d_b || !d_x || rhs <= 0 || algo < 0 || algo > 4 || algo == 2) return SBLAS_ERR_INVALID;
     if (algo == 1) return sblas_trsv_solve_rhs(T, rhs, d_b, d_x, stream);
-    if (opt < kOptNnz || opt > kOptAuto) return SBLAS_ERR_INVALID;
+    if (algo != 0 && rhs == 1) return sblas_trsv_solve(T, algo, d_b, d_x, stream);
+    if (algo == 0 && (opt < kOptNnz || opt > kOptAuto)) return SBLAS_ERR_INVALID;
     if (T->n == 0) return SBLAS_OK;
     DeviceGuard g(T->device);
     hipStream_t s = (hipStream_t)stream;
+    if (algo == 4) {
+        const int a = trsv_pick(T, s);
+        if (a < 0) return -a;
+        algo = a;
+    }
+    if (algo != 0) return trsm_pull(T, algo == 3, rhs, d_b, d_x, s);
     const size_t need = (size_t)T->n * rhs;
     if (need > T->left_rhs_cap) {
         if (T->left_rhs) SBLAS_HIP(hipFree(T->left_rhs));
@@ -1368,7 +1385,7 @@ int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solv
             TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
             hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, H->stream_of(d), P, q.ctl);
         } else if (nloc > 0) {
-            TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0};
+            TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0, nullptr};
             launch_trsm(P, q.ctl, grid, H->stream_of(d));
         }
         MG(hipGetLastError());

@@ -612,7 +612,7 @@ class DeviceTRSV:
 
     def solve_rhs_opt(self, algo: int, opt: int, rhs: int, b_ptr: int, x_ptr: int, stream=None) -> None:
         """algo 0: reference push dataflow with lane mapping opt (1 nnz, 2 rhs, 3 auto);
-        algo 1: pull executor."""
+        algo 1: pull executor; 3: pull, tickets in level order; 4: 1 or 3 as pick() chooses."""
         check(lib.sblas_trsv_solve_rhs_opt(self.h, algo, opt, rhs, b_ptr, x_ptr, stream),
               "trsv_solve_rhs_opt")
 

@@ -106,9 +106,10 @@ def main():
         dX = torch.from_numpy(X).to(dev)
         dB = torch.from_numpy(B).to(dev)
         dXs = torch.zeros_like(dB)
-        # pull executor, then the reference's push dataflow with each lane
+        # pull executor (natural, level-ordered, AUTO tickets), then the reference's push dataflow with each lane
         # mapping (opt 1 = OPT_WARP_NNZ, 2 = OPT_WARP_RHS, 3 = OPT_WARP_AUTO)
-        for name, algo, opt in ((f"trsm_pull_rhs{r}", 1, 0), (f"trsm_push_nnz_rhs{r}", 0, 1),
+        for name, algo, opt in ((f"trsm_pull_rhs{r}", 1, 0), (f"trsm_pull_level_rhs{r}", 3, 0),
+                                (f"trsm_pull_auto_rhs{r}", 4, 0), (f"trsm_push_nnz_rhs{r}", 0, 1),
                                 (f"trsm_push_rhs_rhs{r}", 0, 2), (f"trsm_push_auto_rhs{r}", 0, 3)):
             if algo == 0 and args.no_push_rhs:
                 continue

@@ -399,6 +399,22 @@ def test_sptrsv_auto_order(torch_cuda, sb, orc, kind):
             xs.append(xd.cpu().numpy())
         assert np.array_equal(xs[0], xs[1])
         assert np.abs(xs[0] - xref).sum() / np.abs(xref).sum() < 1e-12
+        # SpTRSM: algo 3 (level-ordered tickets) and 4 bit-identical to the
+        # natural-order pull, every right-hand side within the bound
+        rhs = 5
+        xr = np.stack([xref * (k + 1) for k in range(rhs)], axis=1)
+        bm = np.stack([b * (k + 1) for k in range(rhs)], axis=1)
+        db = torch.from_numpy(np.ascontiguousarray(bm)).cuda()
+        xm = []
+        for algo in (1, 3, 4):
+            xd = torch.zeros(n * rhs, dtype=torch.float64, device="cuda")
+            T.solve_rhs_opt(algo, 3, rhs, db.data_ptr(), xd.data_ptr())
+            torch.cuda.synchronize()
+            xm.append(xd.cpu().numpy().reshape(n, rhs))
+        assert np.array_equal(xm[0], xm[1]) and np.array_equal(xm[0], xm[2])
+        assert np.abs(xm[0] - xr).sum() / np.abs(xr).sum() < 1e-12
+        with pytest.raises(RuntimeError):
+            T.solve_rhs_opt(2, 3, rhs, db.data_ptr(), xd.data_ptr())
     finally:
         T.close()
 
