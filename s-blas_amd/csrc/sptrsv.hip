@@ -440,9 +440,18 @@ struct TrsmArgs {
     const int *lrow;                      // level order (algo 3): ticket t is row lrow[t], CSR row t; else null
 };
 
-template <int RP>
+// RP lanes per row, each lane V consecutive right-hand sides (a pass covers
+// RP x V of them), R = 64 / RP rows per wave step: V > 1 puts V independent
+// polls in flight per lane and R x V rows on one ticket claim -- one claim
+// per row at rhs 64 (V = 1) capped the solve at the single counter's ~85 M
+// claims/s.  kSys: x polled at system scope (peer devices
+// publish into it, g > 1); one device polls at agent scope (L2).  After a
+// ready dependency the next kBatch - 1 are loaded together, as in
+// k_trsv_pull.  Per column the same sums in the same order for every (RP, V).
+template <int RP, int V, bool kSys>
 __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *ctl)
 {
+    constexpr int kBatch = V >= 4 ? 2 : 8 / V;
     constexpr int R = 64 / RP;
     const int lane = threadIdx.x & 63;
     const int slot = lane / RP, kl = lane % RP;
@@ -476,32 +485,85 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
                 jend = e - 1;
             }
         }
-        for (int kc = 0; kc < P.rhs; kc += RP) {
-            const int k = kc + kl;
-            bool pending = live && k < P.rhs;
+        for (int kc = 0; kc < P.rhs; kc += RP * V) {
+            const int k0 = kc + kl * V;
+            const int nv = live ? max(0, min(V, P.rhs - k0)) : 0;  // this lane's columns
+            bool pending = nv > 0;
             int j = j0;
-            double sum = 0.0;
+            double sum[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) sum[v] = 0.0;
             unsigned spins = 0;
             int cj = (pending && j < jend) ? P.col[j] : 0;
             double vj = (pending && j < jend) ? P.val[j] : 0.0;
+            // x row c, this lane's columns (out-of-range columns read as 0: ready)
+            auto ldrow = [&](int c, unsigned long long(&xv)[V]) {
+                const unsigned long long *p = xl + (size_t)c * P.rhs + k0;
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    xv[v] = v < nv ? (kSys ? ld_sys_u64(p + v) : ld_sc1_u64(p + v)) : 0ull;
+            };
+            auto ready = [&](const unsigned long long(&xv)[V]) {
+                bool r = true;
+#pragma unroll
+                for (int v = 0; v < V; ++v) r &= xv[v] != kXPending;
+                return r;
+            };
+            auto acc = [&](double a, const unsigned long long(&xv)[V]) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) sum[v] += a * __longlong_as_double((long long)xv[v]);
+            };
             while (__any(pending)) {
                 if (pending && j < jend) {
-                    const unsigned long long xv = ld_sys_u64(xl + (size_t)cj * P.rhs + k);
-                    if (xv != kXPending) {
-                        sum += vj * __longlong_as_double((long long)xv);
-                        if (++j < jend) {
-                            cj = P.col[j];
-                            vj = P.val[j];
+                    unsigned long long xv[V];
+                    ldrow(cj, xv);
+                    if (ready(xv)) {
+                        acc(vj, xv);
+                        if (++j < jend) {  // ready: batch the next dependencies
+                            int cc[kBatch - 1];
+                            double vv[kBatch - 1];
+                            unsigned long long xb[kBatch - 1][V];
+#pragma unroll
+                            for (int u = 0; u < kBatch - 1; ++u) {  // clamped, unconditional
+                                const int jj = min(j + u, jend - 1);
+                                cc[u] = P.col[jj];
+                                vv[u] = P.val[jj];
+                            }
+#pragma unroll
+                            for (int u = 0; u < kBatch - 1; ++u) ldrow(cc[u], xb[u]);
+                            bool open = true;
+#pragma unroll
+                            for (int u = 0; u < kBatch - 1; ++u) {
+                                if (open && j < jend) {
+                                    if (!ready(xb[u])) {
+                                        open = false;
+                                    } else {
+                                        acc(vv[u], xb[u]);
+                                        ++j;
+                                    }
+                                }
+                            }
+                            if (j < jend) {
+                                cj = P.col[j];
+                                vj = P.val[j];
+                            }
                         }
                     }
                 }
                 if (pending && j == jend) {
-                    const double xi = (P.b[(size_t)bi * P.rhs + k] - sum) / diag;
-                    const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
-                    const size_t at = (size_t)i * P.rhs + k;
-                    __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    for (int q = P.d + 1; q < P.g; ++q)
-                        __hip_atomic_store(P.xs[q] + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        if (v >= nv) break;
+                        const double xi = (P.b[(size_t)bi * P.rhs + k0 + v] - sum[v]) / diag;
+                        const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
+                        const size_t at = (size_t)i * P.rhs + k0 + v;
+                        if (kSys)
+                            __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        else
+                            __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        for (int q = P.d + 1; q < P.g; ++q)
+                            __hip_atomic_store(P.xs[q] + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                     pending = false;
                 }
                 if (__any(pending)) {
@@ -519,24 +581,60 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
     }
 }
 
-static int trsm_lanes(int rhs)
+// Right-hand sides per lane for pass width c (rhs rounded up to a power of
+// two, <= 64).  Measured (r03_trsm_v2, ms; config-5 stand-in natural order /
+// 27-point 100^3 stencil level order):
+//   rhs   V=1          V=2          V=4          V=8
+//    4    4.23 / 2.99  3.21 / 3.52  4.96 / 8.30  4.94 / 8.24
+//    8    8.21 / 3.15  4.30 / 3.30  4.61 / 5.76  8.31 / 19.3
+//   16   16.2  / 3.83  8.25 / 3.48  6.71 / 5.15  7.89 / 13.4
+//   32   32.2  / 6.28  16.3 / 3.88  10.9 / 5.30  11.7 / 12.6
+//   64   64.4  / 11.7  32.7 / 6.41  17.9 / 5.33  18.9 / 13.5
+// Natural order is bound by the ticket counter (~85 M claims/s, one claim
+// per 64 / RP rows): wider lanes, fewer claims.  In level order a wave's rows
+// are independent rows of one level and longer per-lane rows lengthen every
+// level.  SBLAS_TRSM_V overrides.
+static int trsm_cols_per_lane(int c, bool level)
 {
-    int rp = 1;
-    while (rp < rhs && rp < 64) rp *= 2;
-    return rp;
+    if (const char *e = getenv("SBLAS_TRSM_V")) {
+        const int a = atoi(e);
+        return a >= 8 ? 8 : a >= 4 ? 4 : a >= 2 ? 2 : 1;
+    }
+    if (level) return c <= 8 ? 1 : c <= 32 ? 2 : 4;
+    return c <= 8 ? 2 : 4;
+}
+
+template <int V, bool kSys>
+static void launch_trsm_v(int rp, const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t s)
+{
+    switch (rp) {
+    case 1: hipLaunchKernelGGL((k_trsm_pull<1, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 2: hipLaunchKernelGGL((k_trsm_pull<2, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 4: hipLaunchKernelGGL((k_trsm_pull<4, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 8: hipLaunchKernelGGL((k_trsm_pull<8, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 16: hipLaunchKernelGGL((k_trsm_pull<16, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    case 32: hipLaunchKernelGGL((k_trsm_pull<32, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    default: hipLaunchKernelGGL((k_trsm_pull<64, V, kSys>), dim3(grid), dim3(256), 0, s, P, ctl); break;
+    }
+}
+
+template <bool kSys>
+static void launch_trsm_t(const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t s)
+{
+    int c = 1;  // pass width: right-hand sides rounded up to a power of two, <= 64
+    while (c < P.rhs && c < 64) c *= 2;
+    const int v = std::min(trsm_cols_per_lane(c, P.lrow != nullptr), c);
+    const int rp = c / v;
+    if (v == 8) launch_trsm_v<8, kSys>(rp, P, ctl, grid, s);
+    else if (v == 4) launch_trsm_v<4, kSys>(rp, P, ctl, grid, s);
+    else if (v == 2) launch_trsm_v<2, kSys>(rp, P, ctl, grid, s);
+    else launch_trsm_v<1, kSys>(rp, P, ctl, grid, s);
 }
 
 static void launch_trsm(const TrsmArgs &P, unsigned *ctl, int grid, hipStream_t s)
 {
-    switch (trsm_lanes(P.rhs)) {
-    case 1: hipLaunchKernelGGL(k_trsm_pull<1>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    case 2: hipLaunchKernelGGL(k_trsm_pull<2>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    case 4: hipLaunchKernelGGL(k_trsm_pull<4>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    case 8: hipLaunchKernelGGL(k_trsm_pull<8>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    case 16: hipLaunchKernelGGL(k_trsm_pull<16>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    case 32: hipLaunchKernelGGL(k_trsm_pull<32>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    default: hipLaunchKernelGGL(k_trsm_pull<64>, dim3(grid), dim3(256), 0, s, P, ctl); break;
-    }
+    if (P.g > 1) launch_trsm_t<true>(P, ctl, grid, s);
+    else launch_trsm_t<false>(P, ctl, grid, s);
 }
 
 // ---- SpTRSM push: the reference's dataflow with its lane mappings ---------
@@ -1050,7 +1148,9 @@ static int trsm_pull(sblas_trsv_s *T, bool level, int rhs, const double *d_b, do
     TrsmArgs P{level ? T->lrp : T->rrowptr, level ? T->lcol : T->rcol, level ? T->lval : T->rval, d_b,
                (unsigned long long *)d_x, nullptr, 1, 0, 0, T->n, T->n, rhs, T->substitution, 1,
                level ? T->lrow : nullptr};
-    launch_trsm(P, T->ctl, grid_for(T->device), s);
+    int grid = grid_for(T->device);
+    if (const char *e = getenv("SBLAS_TRSM_WG_PER_CU")) grid = grid * std::max(1, std::min(8, atoi(e)));
+    launch_trsm(P, T->ctl, grid, s);
     SBLAS_HIP(hipGetLastError());
     unsigned h[kCtlBytes / 4] = {0};
     SBLAS_HIP(hipMemcpyAsync(h, T->ctl, kCtlBytes, hipMemcpyDeviceToHost, s));
@@ -1385,7 +1485,8 @@ int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solv
             TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
             hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, H->stream_of(d), P, q.ctl);
         } else if (nloc > 0) {
-            TrsmArgs P{q.rowptr, q.col, q.val, q.b, q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0, nullptr};
+            TrsmArgs P{q.rowptr, q.col, q.val, q.b,    q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0,
+                       nullptr};
             launch_trsm(P, q.ctl, grid, H->stream_of(d));
         }
         MG(hipGetLastError());

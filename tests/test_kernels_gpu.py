@@ -719,6 +719,37 @@ def test_sptrsm_kat(torch_cuda, sb, name, sub, rhs):
         assert np.array_equal(x, X)
 
 
+@pytest.mark.parametrize("v", ["1", "2", "4", "8"])
+def test_sptrsm_cols_per_lane(torch_cuda, sb, monkeypatch, v):
+    """SpTRSM pull with V right-hand sides per lane (SBLAS_TRSM_V; the
+    default picks V from rhs and the ticket order): exact on the integer KAT
+    systems for ragged rhs (columns past rhs inside a lane's group), natural
+    and level order, one device and the multi-device split."""
+    torch = torch_cuda
+    monkeypatch.setenv("SBLAS_TRSM_V", v)
+    for name, sub in (("qh768", "fwd"), ("ash85", "bwd")):
+        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
+        cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
+        n = len(cp) - 1
+        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv)]
+        T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                          0 if sub == "fwd" else 1)
+        try:
+            for rhs in (2, 5, 13, 64, 67):
+                X = np.random.default_rng(rhs).integers(1, 11, (n, rhs)).astype(np.float64)
+                db = torch.from_numpy(csc_matmat(cp, ri, cv, X)).cuda()
+                for algo in (1, 3):
+                    xd = torch.full((n, rhs), -1.0, dtype=torch.float64, device="cuda")
+                    T.solve_rhs_opt(algo, 0, rhs, db.data_ptr(), xd.data_ptr())
+                    torch.cuda.synchronize()
+                    assert np.array_equal(xd.cpu().numpy(), X), (name, rhs, algo)
+        finally:
+            T.close()
+        X = np.random.default_rng(7).integers(1, 11, (n, 13)).astype(np.float64)
+        x, _ = sb.trsv_mgpu_solve(cp, ri, cv, n, csc_matmat(cp, ri, cv, X), 2, 0 if sub == "fwd" else 1, 13)
+        assert np.array_equal(x, X)
+
+
 @pytest.mark.parametrize("opt", [1, 2, 3], ids=["warp_nnz", "warp_rhs", "warp_auto"])
 @pytest.mark.parametrize("rhs", [1, 3, 17, 64, 100])
 def test_sptrsm_push_lane_mappings(torch_cuda, sb, opt, rhs):
