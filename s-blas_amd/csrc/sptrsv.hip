@@ -440,7 +440,7 @@ struct TrsmArgs {
     const int *lrow;                      // level order (algo 3): ticket t is row lrow[t], CSR row t; else null
 };
 
-// RP lanes per row, each lane V consecutive right-hand sides (a pass covers
+// RP lanes per row, each lane V right-hand sides RP apart (a pass covers
 // RP x V of them), R = 64 / RP rows per wave step: V > 1 puts V independent
 // polls in flight per lane and R x V rows on one ticket claim -- one claim
 // per row at rhs 64 (V = 1) capped the solve at the single counter's ~85 M
@@ -486,8 +486,11 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
             }
         }
         for (int kc = 0; kc < P.rhs; kc += RP * V) {
-            const int k0 = kc + kl * V;
-            const int nv = live ? max(0, min(V, P.rhs - k0)) : 0;  // this lane's columns
+            // this lane's columns k0 + v*RP, v < nv: each load instruction reads RP
+            // consecutive columns of a row (one line at RP = 16), not RP strided groups
+            const int k0 = kc + kl;
+            const int rem = P.rhs - k0;
+            const int nv = (live && rem > 0) ? min(V, (rem + RP - 1) / RP) : 0;
             bool pending = nv > 0;
             int j = j0;
             double sum[V];
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
                 const unsigned long long *p = xl + (size_t)c * P.rhs + k0;
 #pragma unroll
                 for (int v = 0; v < V; ++v)
-                    xv[v] = v < nv ? (kSys ? ld_sys_u64(p + v) : ld_sc1_u64(p + v)) : 0ull;
+                    xv[v] = v < nv ? (kSys ? ld_sys_u64(p + v * RP) : ld_sc1_u64(p + v * RP)) : 0ull;
             };
             auto ready = [&](const unsigned long long(&xv)[V]) {
                 bool r = true;
@@ -554,9 +557,9 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
 #pragma unroll
                     for (int v = 0; v < V; ++v) {
                         if (v >= nv) break;
-                        const double xi = (P.b[(size_t)bi * P.rhs + k0 + v] - sum[v]) / diag;
+                        const double xi = (P.b[(size_t)bi * P.rhs + k0 + v * RP] - sum[v]) / diag;
                         const unsigned long long bits = (unsigned long long)__double_as_longlong(xi);
-                        const size_t at = (size_t)i * P.rhs + k0 + v;
+                        const size_t at = (size_t)i * P.rhs + k0 + v * RP;
                         if (kSys)
                             __hip_atomic_store(P.xown + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         else
@@ -582,18 +585,18 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
 }
 
 // Right-hand sides per lane for pass width c (rhs rounded up to a power of
-// two, <= 64).  Measured (r03_trsm_v2, ms; config-5 stand-in natural order /
+// two, <= 64).  Measured (r03_trsm_v3, ms; config-5 stand-in natural order /
 // 27-point 100^3 stencil level order):
 //   rhs   V=1          V=2          V=4          V=8
-//    4    4.23 / 2.99  3.21 / 3.52  4.96 / 8.30  4.94 / 8.24
-//    8    8.21 / 3.15  4.30 / 3.30  4.61 / 5.76  8.31 / 19.3
-//   16   16.2  / 3.83  8.25 / 3.48  6.71 / 5.15  7.89 / 13.4
-//   32   32.2  / 6.28  16.3 / 3.88  10.9 / 5.30  11.7 / 12.6
-//   64   64.4  / 11.7  32.7 / 6.41  17.9 / 5.33  18.9 / 13.5
+//    4    4.22 / 3.01  3.21 / 3.50  4.95 / 8.19  4.95 / 8.19
+//    8    8.21 / 3.14  4.29 / 3.30  4.61 / 5.68  8.29 / 19.2
+//   16   16.2  / 3.81  8.25 / 3.51  6.48 / 5.10  7.58 / 13.2
+//   32   32.2  / 6.32  16.3 / 3.85  10.2 / 5.01  10.2 / 8.54
+//   64   64.3  / 11.8  32.6 / 6.38  17.2 / 4.94  16.0 / 7.94
 // Natural order is bound by the ticket counter (~85 M claims/s, one claim
-// per 64 / RP rows): wider lanes, fewer claims.  In level order a wave's rows
-// are independent rows of one level and longer per-lane rows lengthen every
-// level.  SBLAS_TRSM_V overrides.
+// per 64 / RP rows) up to V = 4: wider lanes, fewer claims.  In level order a
+// wave's rows are independent rows of one level and longer per-lane rows
+// lengthen every level.  SBLAS_TRSM_V overrides.
 static int trsm_cols_per_lane(int c, bool level)
 {
     if (const char *e = getenv("SBLAS_TRSM_V")) {
@@ -601,7 +604,7 @@ static int trsm_cols_per_lane(int c, bool level)
         return a >= 8 ? 8 : a >= 4 ? 4 : a >= 2 ? 2 : 1;
     }
     if (level) return c <= 8 ? 1 : c <= 32 ? 2 : 4;
-    return c <= 8 ? 2 : 4;
+    return c <= 8 ? 2 : c <= 32 ? 4 : 8;
 }
 
 template <int V, bool kSys>
