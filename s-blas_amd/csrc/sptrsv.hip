@@ -1151,8 +1151,14 @@ static int trsm_pull(sblas_trsv_s *T, bool level, int rhs, const double *d_b, do
     TrsmArgs P{level ? T->lrp : T->rrowptr, level ? T->lcol : T->rcol, level ? T->lval : T->rval, d_b,
                (unsigned long long *)d_x, nullptr, 1, 0, 0, T->n, T->n, rhs, T->substitution, 1,
                level ? T->lrow : nullptr};
-    int grid = grid_for(T->device);
-    if (const char *e = getenv("SBLAS_TRSM_WG_PER_CU")) grid = grid * std::max(1, std::min(8, atoi(e)));
+    // workgroups per CU (x grid_for's): natural order at rhs >= 16 gains from
+    // more rows in flight (config 5: rhs 16 / 32 / 64 at 1 -> 2 -> 4 per CU:
+    // 6.50 / 10.2 / 16.1 -> 4.63 / 8.55 / 10.4 -> 4.86 / 8.53 / 9.26 ms); level
+    // order loses (27-point stencil rhs 64: 4.93 / 5.12 / 5.32 ms;
+    // profiles/r03/sptrsm/trsm_grid2/).  SBLAS_TRSM_WG_PER_CU overrides.
+    int mult = level || rhs < 16 ? 1 : rhs <= 32 ? 2 : 4;
+    if (const char *e = getenv("SBLAS_TRSM_WG_PER_CU")) mult = std::max(1, std::min(8, atoi(e)));
+    const int grid = grid_for(T->device) * mult;
     launch_trsm(P, T->ctl, grid, s);
     SBLAS_HIP(hipGetLastError());
     unsigned h[kCtlBytes / 4] = {0};

@@ -2,7 +2,7 @@
 # triangles and the config-5 stand-in at rhs 4..64
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r03_trsm_vdef2
+O=gpurun_out/r03_trsm_vdef3
 mkdir -p $O
 T="timeout -k 10"
 $T 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -k "trsv or trsm or sptrsv or config5" \
