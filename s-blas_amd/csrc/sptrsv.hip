@@ -438,6 +438,7 @@ struct TrsmArgs {
     unsigned long long *const *xs;        // [g] peers' x (only q > d used); null if g == 1
     int g, d, o0, nloc, n, rhs, backward, by_row;
     const int *lrow;                      // level order (algo 3): ticket t is row lrow[t], CSR row t; else null
+    int slp;                              // poll back-off (k_trsv_pull's SBLAS_TRSV_SLEEP units)
 };
 
 // RP lanes per row, each lane V right-hand sides RP apart (a pass covers
@@ -456,6 +457,9 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
     const int lane = threadIdx.x & 63;
     const int slot = lane / RP, kl = lane % RP;
     const unsigned long long *xl = P.xown;
+    // poll back-off as k_trsv_pull's (slp >= 0 fixed, < 0 adaptive)
+    const int slp_cap = P.slp < 0 ? 1 << min(-P.slp, 10) : P.slp;
+    const unsigned spin_lim = kSpinLimit / (unsigned)(P.slp < 0 ? 8 : max(slp_cap, 1));
     stamp_start(ctl);
     for (;;) {
         int t0 = 0;
@@ -497,6 +501,7 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
 #pragma unroll
             for (int v = 0; v < V; ++v) sum[v] = 0.0;
             unsigned spins = 0;
+            int cur = 1;  // adaptive back-off, wave-uniform
             int cj = (pending && j < jend) ? P.col[j] : 0;
             double vj = (pending && j < jend) ? P.val[j] : 0.0;
             // x row c, this lane's columns (out-of-range columns read as 0: ready)
@@ -517,10 +522,12 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
                 for (int v = 0; v < V; ++v) sum[v] += a * __longlong_as_double((long long)xv[v]);
             };
             while (__any(pending)) {
+                bool adv = false;
                 if (pending && j < jend) {
                     unsigned long long xv[V];
                     ldrow(cj, xv);
                     if (ready(xv)) {
+                        adv = true;
                         acc(vj, xv);
                         if (++j < jend) {  // ready: batch the next dependencies
                             int cc[kBatch - 1];
@@ -568,11 +575,17 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
                             __hip_atomic_store(P.xs[q] + at, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                     pending = false;
+                    adv = true;
                 }
                 if (__any(pending)) {
-                    __builtin_amdgcn_s_sleep(1);
+                    if (P.slp < 0) {
+                        cur = __any(adv) ? 1 : min(2 * cur, slp_cap);
+                        trsv_backoff(cur);
+                    } else {
+                        trsv_backoff(slp_cap);
+                    }
                     if ((++spins & 1023u) == 0) {
-                        if (spins > kSpinLimit) {
+                        if (spins > spin_lim) {
                             if (lane == 0) atomicOr(&ctl[kAbort], 1u);
                             return;
                         }
@@ -1112,9 +1125,11 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     if (algo == 3) SBLAS_TRY(build_levelset(T, s));
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     const int grid = grid_for(T->device);
-    // poll back-off of the pull executors (k_trsv_pull header); 1 = one
-    // s_sleep(1) per poll, the measured default
-    int slp = 1;
+    // poll back-off of the pull executors (k_trsv_pull header): natural order
+    // one s_sleep(1) per poll; level order the adaptive back-off up to 64
+    // units (-6: 27-point 100^3 2.25 -> 2.03 ms, 7-point 0.97 -> 0.88 ms; -8
+    // and deeper lose; profiles/r03/sptrsv_sleep/)
+    int slp = algo == 3 ? -6 : 1;
     if (const char *e = getenv("SBLAS_TRSV_SLEEP")) slp = std::max(-10, std::min(64, atoi(e)));
     if (algo == 3) {  // sync-free pull, tickets in level order
         fill_pending((unsigned long long *)d_x, T->n, s);
@@ -1150,7 +1165,8 @@ static int trsm_pull(sblas_trsv_s *T, bool level, int rhs, const double *d_b, do
     fill_pending((unsigned long long *)d_x, (long long)T->n * rhs, s);
     TrsmArgs P{level ? T->lrp : T->rrowptr, level ? T->lcol : T->rcol, level ? T->lval : T->rval, d_b,
                (unsigned long long *)d_x, nullptr, 1, 0, 0, T->n, T->n, rhs, T->substitution, 1,
-               level ? T->lrow : nullptr};
+               level ? T->lrow : nullptr, level ? -6 : 1};
+    if (const char *e = getenv("SBLAS_TRSV_SLEEP")) P.slp = std::max(-10, std::min(64, atoi(e)));
     // workgroups per CU (x grid_for's): natural order at rhs >= 16 gains from
     // more rows in flight (config 5: rhs 16 / 32 / 64 at 1 -> 2 -> 4 per CU:
     // 6.50 / 10.2 / 16.1 -> 4.63 / 8.55 / 10.4 -> 4.86 / 8.53 / 9.26 ms); level
@@ -1495,7 +1511,7 @@ int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solv
             hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, H->stream_of(d), P, q.ctl);
         } else if (nloc > 0) {
             TrsmArgs P{q.rowptr, q.col, q.val, q.b,    q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0,
-                       nullptr};
+                       nullptr, 1};
             launch_trsm(P, q.ctl, grid, H->stream_of(d));
         }
         MG(hipGetLastError());
