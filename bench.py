@@ -119,9 +119,10 @@ class Workload:
                 f"y=alpha*A*x+beta*y, {algo} kernel")
 
 
-def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
-    """Oracle restatement (oracle/liboracle.so) timed on this host's cores.
-    Only this leg of bench.py touches oracle/ (DESIGN.md)."""
+def _time_cpu(rowptr, col, val, x, m, nnz, budget_s, threads, runs=3):
+    """Times the oracle port (oracle/liboracle.so) `runs` times each, multi-
+    threaded and single-core, and returns the medians.  Called only in the
+    --cpu-baseline-only child (cpu_baseline below)."""
     import ctypes as C
     lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     f = lib.orc_csr_spmv_omp
@@ -132,12 +133,11 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
     g.restype = None
     g.argtypes = f.argtypes[:-1]
     y = np.zeros(m)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     args = (m, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data, x.ctypes.data, ALPHA, BETA,
             y.ctypes.data)
 
     def timeit(fn, extra, share):
-        fn(*args, *extra)  # warm-up
+        fn(*args, *extra)  # warm-up (page-in, thread pool)
         reps, t0 = 0, time.perf_counter()
         while True:
             fn(*args, *extra)
@@ -146,6 +146,28 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
             if el > share or reps >= 200:
                 return reps, el / reps
 
+    mt = [timeit(f, (threads,), budget_s * 0.5 / runs) for _ in range(runs)]
+    st = [timeit(g, (), budget_s * 0.5 / runs) for _ in range(runs)]
+    return mt, st
+
+
+def cpu_baseline_child(args) -> int:
+    """`bench.py --cpu-baseline-only`: regenerate the workload on the host (the
+    generators are deterministic) and time the oracle port; prints one JSON
+    object.  Runs in its own process so that the OpenMP runtime starts with
+    the pinning environment cpu_baseline() sets (OMP_PROC_BIND is read once,
+    when libgomp initialises -- in the bench process torch/libsblas have
+    already done that)."""
+    import sblas
+    W = Workload(args, sblas)
+    col, val = W.rows(0, W.n)
+    x = sblas.gen_vector(W.n, 43)
+    rp = np.ascontiguousarray(W.rowptr, np.int64)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    mt, st = _time_cpu(rp, np.ascontiguousarray(col, np.int32), np.ascontiguousarray(val, np.float64),
+                       x, W.n, W.nnz, args.cpu_budget, threads)
+    t_mt = float(np.median([t for _, t in mt]))
+    t_st = float(np.median([t for _, t in st]))
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as fh:
@@ -155,16 +177,46 @@ def cpu_baseline(rowptr, col, val, x, m, nnz, budget_s=12.0):
                     break
     except OSError:
         pass
-    r_mt, t_mt = timeit(f, (threads,), budget_s * 0.5)
-    r_st, t_st = timeit(g, (), budget_s * 0.5)
-    return {
-        "value": round(2.0 * nnz / t_mt / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
+    allowed = os.environ.get("SBLAS_BENCH_AFFINITY", "?")  # the parent's mask (libgomp pins ours)
+    gf = lambda t: 2.0 * W.nnz / t / 1e9  # noqa: E731
+    print(json.dumps({
+        "value": round(gf(t_mt), 3), "unit": "GFLOP/s", "cores": threads,
         "kind": "port", "cpu_model": model,
-        "sample": (f"full matrix of the workload, orc_csr_spmv_omp (OpenMP, schedule dynamic) x{r_mt} "
-                   f"reps, {t_mt * 1e3:.1f} ms/SpMV; single-core scalar port orc_csr_spmv "
-                   f"x{r_st}: {t_st * 1e3:.1f} ms/SpMV = {2.0 * nnz / t_st / 1e9:.3f} GFLOP/s"),
-        "single_core_value": round(2.0 * nnz / t_st / 1e9, 3),
-    }
+        "sample": (f"full matrix of the workload, orc_csr_spmv_omp (OpenMP, schedule dynamic, "
+                   f"{threads} threads, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} "
+                   f"OMP_PLACES={os.environ.get('OMP_PLACES')}, {allowed} CPUs in the affinity mask): "
+                   f"median of {len(mt)} runs of {'/'.join(str(r) for r, _ in mt)} reps = "
+                   f"{t_mt * 1e3:.2f} ms/SpMV (runs: {', '.join(f'{gf(t):.1f}' for _, t in mt)} GFLOP/s); "
+                   f"single-core scalar port orc_csr_spmv, median of {len(st)} runs: "
+                   f"{t_st * 1e3:.1f} ms/SpMV = {gf(t_st):.3f} GFLOP/s"),
+        "runs_gflops": [round(gf(t), 3) for _, t in mt],
+        "single_core_value": round(gf(t_st), 3),
+    }), flush=True)
+    return 0
+
+
+def cpu_baseline(args):
+    """The oracle restatement (oracle/liboracle.so) timed on this host's cores,
+    in a child process (cpu_baseline_child) with the threads pinned
+    (OMP_PROC_BIND=close, OMP_PLACES=cores); the median of 3 runs.  Only this
+    leg of bench.py (and the post-timing --check) touches oracle/."""
+    import subprocess
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    try:
+        env["SBLAS_BENCH_AFFINITY"] = str(len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--matrix", args.matrix,
+           "--nrows", str(args.nrows), "--heavy", str(args.heavy), "--light", str(args.light),
+           "--cols", args.cols, "--grid", str(args.grid), "--scale", str(args.scale),
+           "--cpu-budget", str(args.cpu_budget)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": f"cpu baseline child exited {r.returncode}: {r.stderr[-400:]}"}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def choose_driver(gpus: int, env, ndev: int, requested: str = "auto", loopback: bool = False) -> str:
@@ -206,6 +258,171 @@ def pmc_traffic(algo_name: str):
             return float(json.load(fh)["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+CONFIG3 = ("BASELINE configs[2]: the same matrix, CSR5 segmented-sum kernel, rows split by nnz "
+           "(spMV_mgpu_v1, dspmv_mgpu_v1.cu:60-94), y reduced with an all-reduce of the zero-padded "
+           "y (dspmv_mgpu_v1.cu:235-248's merge as one collective)")
+
+
+def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, check, how, exchange=None,
+                   **extra):
+    """The `config3` object every bench line carries:
+    kernel-only, exchange-only and total, max over devices."""
+    achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9 if dev_kern[0] > 0 else 0.0
+    agg = sum(dev_bytes) / (kern_max * 1e-3) / 1e9 if kern_max > 0 else 0.0
+    out = {
+        "what": CONFIG3,
+        "n_gpus": N, "algo": "csr5", "partition": "nnz-balanced (spMV_mgpu_v1)",
+        "exchange": exchange or ("allreduce" if N > 1 else "none (one device)"),
+        "kernel_ms_max": round(kern_max, 5),
+        "exchange_ms_max": round(xch_max, 5),
+        "step_ms": round(step_ms, 5),
+        "gflops": round(2.0 * nnz / (step_ms * 1e-3) / 1e9, 3),
+        "kernel_only_gflops": round(2.0 * nnz / (kern_max * 1e-3) / 1e9, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved0, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved0 / HBM_PEAK_GBS, 4),
+                     "aggregate_GBps": round(agg, 1), "aggregate_frac": round(agg / (HBM_PEAK_GBS * N), 4)},
+        "kernel_ms_per_device": [round(k, 5) for k in dev_kern],
+        "algorithmic_bytes_per_device": [int(b) for b in dev_bytes],
+        "timing": how,
+        "check": check,
+    }
+    out.update(extra)
+    return out
+
+
+def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us):
+    """configs[2] through the C-ABI context: the matrix re-uploaded as CSR5
+    slices of the nnz split with the SBLAS_CTX_ALLREDUCE exchange, timed with
+    the default leg's cold protocol (scrub, device-side hold, aligning
+    all-reduce, per-device spans), then one fresh step checked against the
+    oracle (--check) with every device's y bit-identical."""
+    N = ctx.ngpu
+    ctx.upload(n, n, rowptr, col, val, sblas.CSR5, 1, sblas.CTX_ALLREDUCE)
+    ctx.set_x(x_h)
+    ctx.set_y(np.zeros(n))
+    info = [ctx.slice_info(d) for d in range(N)]
+    dev_bytes = [b if BETA != 0.0 else b - 8 * r for r, _, b in info]
+    for _ in range(max(1, args.warmup)):
+        ctx.spmv_ex(ALPHA, BETA)
+    rows = []
+    for _ in range(args.steps):
+        evict()
+        rows.append(ctx.spmv_ex(ALPHA, BETA, delay_us=delay_us, wait=True))
+    st = np.array(rows)
+    check = None
+    if args.check:
+        y0 = np.zeros(n)
+        ctx.set_y(y0)
+        ctx.spmv_ex(ALPHA, BETA)
+        ys = [ctx.get_y(d) for d in range(N)]
+        check = _oracle_check(rowptr, col, val, x_h, y0, ys)
+    return config3_object(
+        N, float(np.mean(st[:, 0])), float(np.mean(st[:, 1])), float(np.mean(st[:, 2])), int(rowptr[-1]),
+        dev_bytes, [float(np.mean(st[:, 3 + 3 * d])) for d in range(N)], check,
+        "cold steps (1 GiB read sweep before each), sblas_ctx_spmv_ex per-device spans, max over devices",
+        exchange="allreduce", nnz_per_device=[int(z) for _, z, _ in info])
+
+
+def _oracle_check(rowptr, col, val, x_h, y0, ys):
+    """Post-timing verification (oracle = checker only): ys[0] within the
+    per-row fp64 bound of the sequential row sum, every other y bit-identical."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc  # oracle: checker only
+    want = orc.csr_spmv(rowptr, col, val, x_h, ALPHA, BETA, y0)
+    bound = orc.spmv_bound(rowptr, col, val, x_h, ALPHA, BETA, y0)
+    return bool(np.all(np.abs(ys[0] - want) <= bound)) and all(np.array_equal(ys[0], y) for y in ys[1:])
+
+
+def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream, evict,
+                  sync_barrier):
+    """configs[2] under the launcher (one process per GPU): the nnz split's
+    slice as a CSR5 handle (sblas_dist.DistSpMV, exchange "allreduce" =
+    torch.distributed.all_reduce = ncclAllReduce of the zero-padded y), timed
+    cold like the default leg: per step a 1 GiB sweep, barrier, device-side
+    hold, HIP events on the launch stream around kernel and exchange, max
+    over ranks.  At world 1 the span is sblas_spmv_timed's (no exchange)."""
+    n, rowptr = W.n, W.rowptr
+    plan = sblas_dist.make_plan(rowptr, n, world)
+    r0, r1, i0, i1, _ = plan.local(rank)
+    col_rows, val_rows = W.rows(r0, r1)
+    off = i0 - int(rowptr[r0])
+    col = np.ascontiguousarray(col_rows[off:off + (i1 - i0)])
+    val = np.ascontiguousarray(val_rows[off:off + (i1 - i0)])
+    op = sblas_dist.DistSpMV(plan, rank, dev_idx, rowptr, col, val, sblas.CSR5, torch, dist, "allreduce")
+    sp = stream.cuda_stream
+    local_bytes = op.A.algorithmic_bytes(BETA != 0.0)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        op.kernel(ALPHA, x, BETA, sp)
+        if ev is not None:
+            ev[1].record(stream)
+        op.exchange(sp)
+        if ev is not None:
+            ev[2].record(stream)
+
+    kern, xch, span = [], [], []
+    with torch.cuda.stream(stream):
+        for _ in range(max(1, args.warmup)):
+            step()
+        for _ in range(args.steps):
+            evict()
+            sync_barrier()
+            if world == 1:
+                ms = op.A.spmv_timed(op.algo, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp)
+                kern.append(ms)
+                xch.append(0.0)
+                span.append(ms)
+            else:
+                ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+                torch.cuda._sleep(500_000)
+                step(ev)
+                sync_barrier()
+                kern.append(ev[0].elapsed_time(ev[1]))
+                xch.append(ev[1].elapsed_time(ev[2]))
+                span.append(ev[0].elapsed_time(ev[2]))
+        sync_barrier()
+    dev = torch.device("cuda", dev_idx)
+    use_dev = dist is None or dist.get_backend() == "nccl"
+    mine = torch.tensor([np.mean(kern), np.mean(xch), np.mean(span)], dtype=torch.float64,
+                        device=dev if use_dev else "cpu")
+    per = [mine.clone() for _ in range(world)]
+    byts = torch.tensor([float(local_bytes)], dtype=torch.float64, device=mine.device)
+    allb = [byts.clone() for _ in range(world)]
+    if dist is not None:
+        dist.all_gather(per, mine)
+        dist.all_gather(allb, byts)
+    per = [p.cpu().numpy() for p in per]
+    check = None
+    if args.check:
+        with torch.cuda.stream(stream):
+            op.load_y(torch.zeros(plan.m, dtype=torch.float64, device=dev))
+            step()
+        torch.cuda.synchronize()
+        y = op.result().clone()
+        same = True
+        if dist is not None:  # every rank's y bit-identical: elementwise max == min == own
+            yy = y if use_dev else y.cpu()
+            hi, lo = yy.clone(), yy.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            same = bool(torch.equal(hi, yy) and torch.equal(lo, yy))
+        if rank == 0:
+            col_all, val_all = W.rows(0, n)
+            check = _oracle_check(rowptr, col_all, val_all, x_h, np.zeros(plan.m), [y.cpu().numpy()]) and same
+        elif not same:
+            check = False
+    op.close()
+    return config3_object(
+        world, max(p[0] for p in per), max(p[1] for p in per), max(p[2] for p in per), W.nnz,
+        [float(b.item()) for b in allb], [float(p[0]) for p in per], check,
+        ("cold steps: sblas_spmv_timed device span (one GPU, no exchange)" if world == 1 else
+         "cold steps: HIP events on the launch stream around kernel and exchange after a device-side "
+         "hold, max over ranks"),
+        nnz_per_device=[int(plan.end_idx[d] - plan.start_idx[d] + 1) for d in range(world)])
 
 
 def run_ctx(args) -> int:
@@ -302,7 +519,6 @@ def run_ctx(args) -> int:
     else:
         warm_el, warm_last = warm()
         st = cold()
-    del scrubs
     # st[:, 0..2] = max over devices of kernel / exchange / step (ms); then
     # per device d: st[:, 3+3d .. 5+3d]
     step_ms = float(np.mean(st[:, 2]))
@@ -315,12 +531,11 @@ def run_ctx(args) -> int:
         ctx.set_y(y0)
         ctx.spmv_ex(ALPHA, BETA)
         ys = [ctx.get_y(d) for d in range(N)]
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import orc  # oracle: checker only
-        want = orc.csr_spmv(rowptr, col, val, x_h, ALPHA, BETA, y0)
-        bound = orc.spmv_bound(rowptr, col, val, x_h, ALPHA, BETA, y0)
-        check = bool(np.all(np.abs(ys[0] - want) <= bound)) and \
-            all(np.array_equal(ys[0], y) for y in ys[1:])
+        check = _oracle_check(rowptr, col, val, x_h, y0, ys)
+    config3 = None
+    if not args.no_config3:
+        config3 = ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us)
+    del scrubs
     total_flops = 2.0 * nnz
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
     agg = sum(dev_bytes) / (kern_max * 1e-3) / 1e9
@@ -384,11 +599,13 @@ def run_ctx(args) -> int:
         out["ms_per_step"] = round(warm_el / args.steps * 1e3, 5)
     if check is not None:
         out["check_vs_oracle"] = check
+    if config3 is not None:
+        out["config3"] = config3
     if args.ctx_loopback:
         out["note"] = (f"loopback rehearsal: {N} context ranks on {ndev} GPU(s), collectives as "
                        "stream-ordered device copies (no RCCL); not a measurement")
     if N == 1 and not args.no_cpu_baseline and not args.ctx_loopback:
-        out["cpu_baseline"] = cpu_baseline(rowptr, col, val, x_h, n, nnz, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(out), flush=True)
     ctx.close()
     return 0
@@ -454,7 +671,13 @@ def main() -> int:
                     help="auto: torch.distributed ranks under a launcher, else one process over "
                          "sblas_ctx for --gpus > 1 (the persistent single-GPU path at N = 1); "
                          "ctx: force the C-ABI context (also at N = 1)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip the BASELINE configs[2] leg (CSR5, nnz split, all-reduce of y) that every "
+                         "line carries under `config3`")
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_baseline_only:  # child of cpu_baseline(): host only, no torch, no GPU
+        return cpu_baseline_child(args)
 
     import torch
 
@@ -654,6 +877,10 @@ def main() -> int:
                            "gflops": round(2.0 * nnz / (rk * 1e-3) / 1e9, 3),
                            "roofline_frac": round(local_bytes / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "cache": "cold"}
+    config3 = None
+    if not args.no_config3:
+        config3 = torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream,
+                                evict, sync_barrier)
     del scrub
     copy_peak = None
     if world == 1:
@@ -786,9 +1013,10 @@ def main() -> int:
             out["check_vs_oracle"] = check
         if rowsplit_beside is not None:
             out["rowsplit_beside"] = rowsplit_beside
+        if config3 is not None:
+            out["config3"] = config3
         if world == 1 and not args.no_cpu_baseline:
-            rp_all = rowptr
-            out["cpu_baseline"] = cpu_baseline(rp_all, col, val, x_h, plan.m, nnz, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     op.close()
     if dist is not None:

@@ -153,11 +153,19 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
  * analyse / spmv / spmv_timed with SBLAS_SPMV_AUTO resolve through it).  A
  * device probe measures column locality: over up to 65,536 sampled rows, the
  * share of entries whose column is within 16 columns (one 128-B line of x)
- * of the previous entry's (the previous row's last, for a row's first).  >= 1/2 (e.g. the reference generator's
- * contiguous columns, banded or blocked rows): ROWSPLIT, whose gathers then
- * coalesce; otherwise XSORT when the handle holds >= 2M nonzeros and
- * n*8 <= 120 MiB (its column groups), else PANEL.  If the XSORT analysis is
- * unsupported for the matrix, sblas_csr_analyse falls back to PANEL and the
+ * of the previous entry's (the previous row's last, for a row's first), and
+ * how widely the columns spread.  The checks run in this order:
+ *   1. XSORT when the handle holds >= 2M nonzeros, n*8 <= 120 MiB (its
+ *      column groups) and the columns are spread (any adjacency: banded and
+ *      stencil matrices included);
+ *   2. else ROWSPLIT when the adjacency is >= 1/2 (e.g. the reference
+ *      generator's contiguous columns, banded or blocked rows) or the columns
+ *      are crowded into a narrow range, whose gathers then coalesce;
+ *   3. else PANEL.
+ * XSORT accumulates in LDS with fp64 atomics: its y is within the fp64 bound
+ * but NOT bitwise repeatable run to run, so AUTO may pick a non-deterministic
+ * kernel (ROWSPLIT, CSR5 and PANEL are deterministic).  If the XSORT analysis
+ * is unsupported for the matrix, sblas_csr_analyse falls back to PANEL and the
  * choice becomes PANEL.  SBLAS_AUTO=<1..5> overrides the choice. */
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
 /* Device bytes held by the analysis of `algo` (free memory before - after
@@ -167,7 +175,11 @@ long long sblas_csr_plan_bytes(sblas_csr A, int algo);
 long long sblas_spmv_algorithmic_bytes(sblas_csr A, int beta_nonzero);
 
 /* SpMM on a device handle: C(m x n, ldc) = alpha*A*B(k x n, ldb) + beta*C.
- * b_layout 0 = column-major B (ld=ldb >= k), 1 = row-major B (ld >= n). */
+ * b_layout 0 = column-major B (ld=ldb >= k), 1 = row-major B (ld >= n).
+ * Concurrency: the handle owns the SpMM scratch (the row-major B panel and
+ * the split-row partials), so ONE sblas_spmm per handle may be in flight:
+ * issue a handle's calls on one stream, or synchronise between calls on
+ * different streams or threads.  Distinct handles are independent. */
 int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb,
                int b_layout, double beta, double *d_C, int ldc, void *stream);
 
@@ -325,6 +337,19 @@ int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr
 int sblas_ctx_matrix_upload_ex(sblas_ctx ctx, int m, int n, const long long *rowptr,
                                const int *col, const double *val, int algo, int partition,
                                int exchange);
+/* Cyclic partition + all-gather with the exchange overlapped (replaces the
+ * per-task copy/compute overlap of spMV_mgpu_v2, dspmv_mgpu_v2.cu:128-170):
+ * each device's local chunks are cut into `parts` consecutive groups (at most
+ * one per chunk; parts = 1 is sblas_ctx_matrix_upload(..., 0)), each group
+ * its own handle running the whole slice's algorithm (AUTO resolved on the
+ * whole slice).  A step runs part p's kernel on the device's main stream and
+ * part p's all-gather + placement on a second (comm) stream while part
+ * p + 1's kernel runs; the main stream then joins.  Stats: kernel = start ..
+ * last part kernel, exchange = the tail after it, step = start .. join. */
+int sblas_ctx_matrix_upload_parts(sblas_ctx ctx, int m, int n, const long long *rowptr,
+                                  const int *col, const double *val, int algo, int parts);
+/* The parts the loaded matrix runs in (1: not overlapped; 0: nothing loaded). */
+int sblas_ctx_parts(sblas_ctx ctx, int *parts);
 /* Device d's share: rows, entries, and the algorithmic bytes of its SpMV
  * launch with beta != 0 (sblas_spmv_algorithmic_bytes).  Any may be NULL. */
 int sblas_ctx_slice_info(sblas_ctx ctx, int d, long long *rows, long long *nnz,

@@ -51,6 +51,19 @@ struct sblas_ctx_s {
     bool loopback = false;
     std::vector<hipEvent_t> evx, evy;  // [g] cross-stream sync events
     std::vector<const double **> yptr; // allreduce: per device, the g send buffers
+    // overlapped exchange (cyclic partition + all-gather, parts > 1): each
+    // device's local chunks cut into `parts` consecutive groups, each its own
+    // handle; part p's all-gather + placement run on the device's comm stream
+    // while the kernel of part p + 1 runs on the main stream
+    // (dspmv_mgpu_v2.cu:128-170's per-task copies overlapping compute)
+    int parts = 1;
+    std::vector<long long> plo;        // [parts + 1] local chunk bounds of the parts
+    std::vector<sblas_csr> P;          // [g * parts] part handles (device-major)
+    std::vector<hipStream_t> cst;      // [g] comm streams
+    std::vector<hipEvent_t> evp;       // [g * parts] part kernel done (main stream)
+    std::vector<hipEvent_t> evc;       // [g] comm stream done (joins the main stream)
+    std::vector<int> palgo;            // [g] the algorithm the part handles run (AUTO resolved)
+    int parts_req = 1;                 // requested by sblas_ctx_matrix_upload_parts
 };
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
@@ -205,8 +218,79 @@ int xchg_spmv(sblas_ctx_s &C)
     return lb_barrier(C, C.evy);  // every slice read before any is re-primed
 }
 
+// overlapped form, part p: rows of global chunks [plo[p]*g, plo[p+1]*g)
+struct PartGeom {
+    long long stride;  // rows of one device's (padded) part slice
+    long long lrow0;   // first local row of the part on every device
+    long long grow0;   // first global row of the part
+    long long rows;    // global rows of the part
+};
+
+PartGeom part_geom(const sblas_ctx_s &C, int p)
+{
+    const long long R = C.chunk_rows, g = C.g;
+    PartGeom q;
+    q.stride = (C.plo[p + 1] - C.plo[p]) * R;
+    q.lrow0 = C.plo[p] * R;
+    q.grow0 = std::min<long long>(C.m, C.plo[p] * g * R);
+    q.rows = std::min<long long>(C.m, C.plo[p + 1] * g * R) - q.grow0;
+    return q;
+}
+
+// part p's exchange on the comm streams (each first waits for every
+// device's part-p kernel when in loopback, for its own under RCCL): one
+// all-gather of the part slices, then their placement into yfull
+int xchg_part(sblas_ctx_s &C, int p)
+{
+    const int g = C.g;
+    const PartGeom q = part_geom(C, p);
+    if (!C.loopback) {
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C.dev[d]);
+            SBLAS_HIP(hipStreamWaitEvent(C.cst[d], C.evp[(size_t)d * C.parts + p], 0));
+        }
+        if (q.stride > 0) {
+            SBLAS_NCCL(ncclGroupStart());
+            for (int d = 0; d < g; ++d) {
+                DeviceGuard gd(C.dev[d]);
+                SBLAS_NCCL_G(ncclAllGather(C.ylocal[d] + q.lrow0, C.gathered[d] + (size_t)g * q.lrow0,
+                                           (size_t)q.stride, ncclDouble, C.comm[d], C.cst[d]));
+            }
+            SBLAS_NCCL(ncclGroupEnd());
+        }
+    } else {
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C.dev[d]);
+            for (int e = 0; e < g; ++e) SBLAS_HIP(hipStreamWaitEvent(C.cst[d], C.evp[(size_t)e * C.parts + p], 0));
+            for (int r = 0; r < g && q.stride > 0; ++r)
+                SBLAS_HIP(hipMemcpyAsync(C.gathered[d] + (size_t)g * q.lrow0 + (size_t)r * q.stride,
+                                         C.ylocal[r] + q.lrow0, sizeof(double) * q.stride,
+                                         hipMemcpyDeviceToDevice, C.cst[d]));
+        }
+    }
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        if (q.rows > 0)
+            SBLAS_TRY(sblas_assemble_cyclic(C.gathered[d] + (size_t)g * q.lrow0, g, q.stride, C.chunk_rows, q.rows,
+                                            C.yfull[d] + q.grow0, C.cst[d]));
+    }
+    return SBLAS_OK;
+}
+
+void free_parts(sblas_ctx_s &C)
+{
+    for (size_t i = 0; i < C.P.size(); ++i) {
+        DeviceGuard g(C.dev[i / std::max(1, C.parts)]);
+        sblas_csr_destroy(C.P[i]);
+    }
+    C.P.clear();
+    C.plo.clear();
+    C.parts = 1;
+}
+
 void free_matrix(sblas_ctx_s &C)
 {
+    free_parts(C);
     for (int d = 0; d < (int)C.A.size(); ++d) {
         DeviceGuard g(C.dev[d]);
         sblas_csr_destroy(C.A[d]);
@@ -233,6 +317,58 @@ void free_matrix(sblas_ctx_s &C)
     C.last.clear();
     C.pending = false;
     C.loaded = false;
+}
+
+// comm streams and part events, created on the first overlapped upload
+int ensure_overlap_streams(sblas_ctx_s &C)
+{
+    const int g = C.g;
+    if (C.cst.empty()) {
+        C.cst.assign(g, nullptr);
+        C.evc.assign(g, nullptr);
+    }
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        if (!C.cst[d]) SBLAS_HIP(hipStreamCreateWithFlags(&C.cst[d], hipStreamNonBlocking));
+        if (!C.evc[d]) SBLAS_HIP(hipEventCreateWithFlags(&C.evc[d], hipEventDisableTiming));
+    }
+    const size_t need = (size_t)g * C.parts;
+    if (C.evp.size() < need) {
+        // device-major: event i belongs to device i / (evp.size() / g)
+        std::vector<hipEvent_t> old = C.evp;
+        const size_t per_old = old.empty() ? 0 : old.size() / g;
+        for (size_t i = 0; i < old.size(); ++i) {
+            DeviceGuard gd(C.dev[i / per_old]);
+            (void)hipEventDestroy(old[i]);
+        }
+        C.evp.assign(need, nullptr);
+        for (size_t i = 0; i < need; ++i) {
+            DeviceGuard gd(C.dev[i / C.parts]);
+            SBLAS_HIP(hipEventCreateWithFlags(&C.evp[i], hipEventDisableTiming));
+        }
+    }
+    return SBLAS_OK;
+}
+
+// device d's part handles: part p = its local rows of local chunks
+// [plo[p], plo[p+1]), all run with the whole slice's algorithm (AUTO
+// resolved once on the whole slice, so every part runs the same kernel)
+int upload_parts(sblas_ctx_s &C, int d, const std::vector<long long> &lrp, const std::vector<int> &lcol,
+                 const std::vector<double> &lval)
+{
+    const long long lm = (long long)lrp.size() - 1, R = C.chunk_rows;
+    int a = C.algo;
+    if (a == SBLAS_SPMV_AUTO) SBLAS_TRY(sblas_csr_pick(C.A[d], C.st[d], &a));
+    C.palgo[d] = a;
+    for (int p = 0; p < C.parts; ++p) {
+        const long long r0 = std::min(lm, C.plo[p] * R), r1 = std::min(lm, C.plo[p + 1] * R);
+        if (r1 <= r0) continue;
+        sblas_csr &H = C.P[(size_t)d * C.parts + p];
+        SBLAS_TRY(sblas_csr_upload_slice(&H, C.dev[d], C.n, lrp.data(), lcol.data(), lval.data(), (int)r0,
+                                         (int)r1, lrp[r0], lrp[r1], C.st[d]));
+        SBLAS_TRY(sblas_csr_analyse(H, a, C.st[d]));
+    }
+    return SBLAS_OK;
 }
 
 }  // namespace
@@ -298,6 +434,29 @@ int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist)
                 return SBLAS_ERR_INVALID;
             }
     }
+    if (loopback) {
+        // the loopback all-reduce (k_ctx_sum) reads every rank's send buffer
+        // from the summing rank's device: ranks wrapped onto distinct GPUs
+        // need peer access between them (refused if the pair has none)
+        for (int a = 0; a < ngpu; ++a)
+            for (int b = 0; b < ngpu; ++b) {
+                if (dev[a] == dev[b]) continue;
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, dev[a], dev[b]) != hipSuccess || !can) {
+                    set_error("sblas_ctx_create: loopback over devices %d and %d without peer access",
+                              dev[a], dev[b]);
+                    return SBLAS_ERR_UNSUPPORTED;
+                }
+                DeviceGuard gd(dev[a]);
+                const hipError_t e = hipDeviceEnablePeerAccess(dev[b], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                    set_error("sblas_ctx_create: hipDeviceEnablePeerAccess(%d -> %d): %s", dev[a], dev[b],
+                              hipGetErrorString(e));
+                    return SBLAS_ERR_HIP;
+                }
+                (void)hipGetLastError();  // clear an "already enabled" status
+            }
+    }
     auto *C = new sblas_ctx_s();
     C->g = ngpu;
     C->dev = dev;
@@ -346,6 +505,12 @@ int sblas_ctx_destroy(sblas_ctx C)
                 (void)hipEventDestroy(C->ev[(size_t)3 * d + k]);
         if (d < (int)C->evx.size() && C->evx[d]) (void)hipEventDestroy(C->evx[d]);
         if (d < (int)C->evy.size() && C->evy[d]) (void)hipEventDestroy(C->evy[d]);
+        if (d < (int)C->cst.size() && C->cst[d]) (void)hipStreamDestroy(C->cst[d]);
+        if (d < (int)C->evc.size() && C->evc[d]) (void)hipEventDestroy(C->evc[d]);
+    }
+    for (size_t i = 0; i < C->evp.size(); ++i) {
+        DeviceGuard g(C->dev[i / std::max<size_t>(1, C->evp.size() / C->g)]);
+        if (C->evp[i]) (void)hipEventDestroy(C->evp[i]);
     }
     delete C;
     return SBLAS_OK;
@@ -408,6 +573,19 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
     // allgather: each device's padded slice of `stride` rows; allreduce: a
     // zero-padded full-length y whose own rows the kernel writes in place
     C->ylen = exchange == SBLAS_CTX_ALLREDUCE ? std::max(m, 1) : C->stride;
+    // overlapped exchange: parts of consecutive local chunks (at most one
+    // part per chunk of a device's slice)
+    if (partition == 0 && exchange == SBLAS_CTX_ALLGATHER && C->parts_req > 1 && m > 0) {
+        const long long ncmax = C->stride / C->chunk_rows;
+        C->parts = (int)std::min<long long>(C->parts_req, ncmax);
+        if (C->parts > 1) {
+            C->plo.resize((size_t)C->parts + 1);
+            for (int p = 0; p <= C->parts; ++p) C->plo[p] = (long long)p * ncmax / C->parts;
+            C->P.assign((size_t)g * C->parts, nullptr);
+            C->palgo.assign(g, algo);
+            SBLAS_TRY(ensure_overlap_streams(*C));
+        }
+    }
     int st = SBLAS_OK;
     for (int d = 0; d < g && st == SBLAS_OK; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -424,6 +602,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             C->lnnz[d] = lz;
             st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, lrp.data(), lcol.data(), lval.data(), 0,
                                         (int)lm, 0, lz, C->st[d]);
+            if (st == SBLAS_OK && C->parts > 1) st = upload_parts(*C, d, lrp, lcol, lval);
         } else {
             C->lrows[d] = std::max(0, er[d] - sr[d] + 1);
             C->lnnz[d] = C->lrows[d] > 0 ? ei[d] + 1 - si[d] : 0;
@@ -472,6 +651,23 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
     }
     C->last.assign((size_t)3 + 3 * g, 0.0);
     C->loaded = true;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_matrix_upload_parts(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
+                                  const double *val, int algo, int parts)
+{
+    if (!C || parts < 1) return SBLAS_ERR_INVALID;
+    C->parts_req = parts;
+    const int st = sblas_ctx_matrix_upload_ex(C, m, n, rowptr, col, val, algo, 0, SBLAS_CTX_ALLGATHER);
+    C->parts_req = 1;
+    return st;
+}
+
+int sblas_ctx_parts(sblas_ctx C, int *parts)
+{
+    if (!C || !parts) return SBLAS_ERR_INVALID;
+    *parts = C->loaded ? C->parts : 0;
     return SBLAS_OK;
 }
 
@@ -545,6 +741,42 @@ int sblas_ctx_set_y(sblas_ctx C, const double *y)
     return SBLAS_OK;
 }
 
+// The overlapped step: part p's kernels on the main streams, its exchange on
+// the comm streams (xchg_part) while part p + 1's kernels run; the main
+// streams then join their comm streams.  Events: start, after the last part
+// kernel (kernel span), after the join (whole step).
+static int ctx_step_overlapped(sblas_ctx_s &C, double alpha, double beta)
+{
+    const int g = C.g;
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        SBLAS_HIP(hipEventRecord(C.ev[(size_t)3 * d], C.st[d]));
+    }
+    for (int p = 0; p < C.parts; ++p) {
+        const long long lrow0 = C.plo[p] * C.chunk_rows;
+        for (int d = 0; d < g; ++d) {
+            DeviceGuard gd(C.dev[d]);
+            sblas_csr H = C.P[(size_t)d * C.parts + p];
+            if (H) SBLAS_TRY(sblas_spmv(H, C.palgo[d], alpha, C.x[d], beta, C.ylocal[d] + lrow0, C.st[d]));
+            SBLAS_HIP(hipEventRecord(C.evp[(size_t)d * C.parts + p], C.st[d]));
+        }
+        SBLAS_TRY(xchg_part(C, p));
+    }
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        SBLAS_HIP(hipEventRecord(C.ev[(size_t)3 * d + 1], C.st[d]));
+        SBLAS_HIP(hipEventRecord(C.evc[d], C.cst[d]));
+        SBLAS_HIP(hipStreamWaitEvent(C.st[d], C.evc[d], 0));
+    }
+    // loopback: the next step's kernels overwrite slices other devices read
+    if (C.loopback) SBLAS_TRY(lb_barrier(C, C.evy));
+    for (int d = 0; d < g; ++d) {
+        DeviceGuard gd(C.dev[d]);
+        SBLAS_HIP(hipEventRecord(C.ev[(size_t)3 * d + 2], C.st[d]));
+    }
+    return SBLAS_OK;
+}
+
 // Waits for the step issued last and fills C->last (3 + 3g doubles, ms):
 // max over devices of kernel / exchange / step, then per device the same.
 static int ctx_collect(sblas_ctx_s *C)
@@ -587,6 +819,14 @@ int sblas_ctx_spmv_ex(sblas_ctx C, double alpha, double beta, double delay_us, i
             SBLAS_HIP(hipGetLastError());
         }
         SBLAS_TRY(xchg_barrier(*C));
+    }
+    if (C->parts > 1) {
+        SBLAS_TRY(ctx_step_overlapped(*C, alpha, beta));
+        C->pending = true;
+        if (!wait) return SBLAS_OK;
+        SBLAS_TRY(ctx_collect(C));
+        if (stats) std::copy(C->last.begin(), C->last.end(), stats);
+        return SBLAS_OK;
     }
     for (int d = 0; d < g; ++d) {
         DeviceGuard gd(C->dev[d]);

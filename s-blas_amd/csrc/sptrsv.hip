@@ -1078,8 +1078,13 @@ static int trsv_pick(sblas_trsv_s *T, hipStream_t s)
     if (T->auto_algo) return T->auto_algo;
     const int S = std::min(T->n, 65536);
     unsigned long long *d = nullptr, h[2] = {0, 0};
-    SBLAS_HIP(hipMalloc(&d, sizeof(h)));
-    hipError_t e = hipMemsetAsync(d, 0, sizeof(h), s);
+    // errors come back negative (callers read a positive return as the choice)
+    hipError_t e = hipMalloc(&d, sizeof(h));
+    if (e != hipSuccess) {
+        set_error("sblas_trsv_solve (auto): hipMalloc: %s", hipGetErrorString(e));
+        return -SBLAS_ERR_HIP;
+    }
+    e = hipMemsetAsync(d, 0, sizeof(h), s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_trsv_local_deps, dim3((S + 255) / 256), dim3(256), 0, s, T->rrowptr, T->rcol, T->n,
                            T->substitution, S, d);

@@ -750,8 +750,11 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (sub >= 0 && k1 && ht == 0) {
+                // acq_rel: releases this team's partials to the last
+                // arriver and makes every other team's visible to it before
+                // its reduce reads them (the HIP memory model's hand-off)
                 const unsigned old =
-                    __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
                 s_last[half] = old + 1u == 8u * a.epoch;
             }
             if (a.tail) {

@@ -119,6 +119,8 @@ _sig("sblas_ctx_spmv", _i, _p, _d, _d, _p)
 _sig("sblas_ctx_matrix_upload_ex", _i, _p, _i, _i, _p, _p, _p, _i, _i, _i)
 _sig("sblas_ctx_slice_info", _i, _p, _i, _p, _p, _p)
 _sig("sblas_ctx_slice_algo", _i, _p, _i, _p)
+_sig("sblas_ctx_matrix_upload_parts", _i, _p, _i, _i, _p, _p, _p, _i, _i)
+_sig("sblas_ctx_parts", _i, _p, _p)
 _sig("sblas_ctx_spmv_ex", _i, _p, _d, _d, _d, _i, _p)
 _sig("sblas_ctx_sync", _i, _p, _p)
 _sig("sblas_ctx_get_y", _i, _p, _i, _p)
@@ -529,6 +531,21 @@ class DeviceCtx:
         check(lib.sblas_ctx_matrix_upload_ex(self.h, m, n, ptr(rp), ptr(ci), ptr(v), algo, partition,
                                              exchange), "ctx_matrix_upload")
         self.m = m
+
+    def upload_parts(self, m: int, n: int, rowptr, col, val, algo: int, parts: int) -> None:
+        """Cyclic chunks + all-gather with the exchange overlapped over `parts`
+        groups of each device's chunks (sblas_ctx_matrix_upload_parts)."""
+        rp = np.ascontiguousarray(rowptr, np.int64)
+        ci = np.ascontiguousarray(col, np.int32)
+        v = np.ascontiguousarray(val, np.float64)
+        check(lib.sblas_ctx_matrix_upload_parts(self.h, m, n, ptr(rp), ptr(ci), ptr(v), algo, parts),
+              "ctx_matrix_upload_parts")
+        self.m = m
+
+    def parts(self) -> int:
+        p = C.c_int()
+        check(lib.sblas_ctx_parts(self.h, C.byref(p)), "ctx_parts")
+        return p.value
 
     def slice_info(self, d: int):
         """(rows, nnz, algorithmic bytes with beta != 0) of device d's share."""

@@ -89,14 +89,26 @@ class DistSpMV:
         self.dm = r1 - r0
         stride = plan.stride
         f64 = torch.float64
-        self.y_local = torch.zeros(stride, dtype=f64, device=dev)  # padded slice
         self.y_full = torch.zeros(plan.m, dtype=f64, device=dev)
-        self.gathered = torch.zeros(plan.world * stride, dtype=f64, device=dev)
+        if exchange == "allreduce":
+            # BASELINE configs[2]: the kernel writes its rows in place into a
+            # zero-padded full-length send buffer; the exchange copies it into
+            # y_full and sums y_full over the ranks (ncclAllReduce), then the
+            # rank's own rows of the sum become the next call's input
+            # (the C-ABI context's SBLAS_CTX_ALLREDUCE, csrc/ctx.hip)
+            self.y_send = torch.zeros(max(plan.m, 1), dtype=f64, device=dev)
+            self.y_local = self.y_send[r0:r1]
+            self.gathered = None
+        else:
+            self.y_local = torch.zeros(stride, dtype=f64, device=dev)  # padded slice
+            self.gathered = torch.zeros(plan.world * stride, dtype=f64, device=dev)
         self.meta = torch.from_numpy(plan.meta()).to(dev)
 
     def load_y(self, y_full) -> None:
         """Set y (full vector, device tensor) as the next call's input."""
         self.y_full.copy_(y_full)
+        if self.exchange_mode == "allreduce":
+            self.y_send.zero_()
         self.y_local[: self.dm].copy_(self.y_full[self.r0:self.r1])
         if self.cont and self.dm > 0:
             self.y_local[0] = 0.0
@@ -118,16 +130,17 @@ class DistSpMV:
                 self.gathered.data_ptr(), self.plan.world, self.plan.stride, self.meta.data_ptr(),
                 self.y_full.data_ptr(), self.rank, self.y_local.data_ptr(), stream),
                 "assemble_slices")
-        else:  # literal allreduce of y (config 3)
-            self.y_full.zero_()
-            self.y_full[self.r0:self.r1].copy_(self.y_local[: self.dm])
+        else:  # literal allreduce of the zero-padded y (config 3)
+            self.y_full.copy_(self.y_send[: self.plan.m])
             if self.dist.get_backend() == "nccl":
                 self.dist.all_reduce(self.y_full)
             else:
                 h = self.y_full.cpu()
                 self.dist.all_reduce(h)
                 self.y_full.copy_(h.to(self.y_full.device))
-            self.y_local[: self.dm].copy_(self.y_full[self.r0:self.r1])
+            # re-prime: own rows of the sum; a continuation row restarts from
+            # 0 (the previous rank adds beta*y for it)
+            self.y_local.copy_(self.y_full[self.r0:self.r1])
             if self.cont and self.dm > 0:
                 self.y_local[0] = 0.0
 

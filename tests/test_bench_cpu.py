@@ -78,3 +78,24 @@ def test_workload_rows_match_generators(matrix):
         c, v = W.rows(a, b)
         assert (c == col[rp[a]:rp[b]]).all() and (v == val[rp[a]:rp[b]]).all()
     assert matrix[:4] in W.describe("auto").lower() or "r-mat" in W.describe("auto").lower()
+
+
+def test_config3_object_keys():
+    """Every bench line carries BASELINE configs[2] under `config3`
+    (kernel-only, exchange-only and total, max over devices):
+    the object both drivers attach (bench.config3_object), at N > 1 and 1."""
+    for N in (8, 2, 1):
+        c3 = bench.config3_object(N, 0.05, 0.03, 0.08, 39_750_000, [6.7e7] * N, [0.05] * N, True, "cold")
+        for k in ("kernel_ms_max", "exchange_ms_max", "step_ms", "gflops", "roofline", "check",
+                  "kernel_ms_per_device", "algo", "partition", "exchange"):
+            assert k in c3, k
+        assert c3["algo"] == "csr5" and c3["exchange"] == ("allreduce" if N > 1 else "none (one device)")
+        assert abs(c3["gflops"] - 2 * 39_750_000 / 0.08e-3 / 1e9) < 1e-3
+        assert 0 < c3["roofline"]["frac"] < 1
+
+
+def test_config3_is_on_by_default():
+    """Both drivers add the configs[2] leg unless --no-config3 is given."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('out["config3"] = config3') == 2
+    assert src.count("if not args.no_config3:") == 2

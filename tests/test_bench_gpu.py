@@ -16,6 +16,8 @@ from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
+CONFIG3_KEYS = ("kernel_ms_max", "exchange_ms_max", "step_ms", "gflops", "roofline", "check")
+
 
 @pytest.mark.parametrize("algo,partition,exchange", [
     ("xsort", "cyclic", "allgather"),
@@ -39,6 +41,10 @@ def test_bench_ctx_driver(algo, partition, exchange):
     assert line["config"]["exchange"] == exchange
     assert line["ms_per_step"] > 0 and line["kernel_ms_max_over_ranks"] > 0
     assert line["ms_per_step"] >= line["kernel_ms_max_over_ranks"]
+    # BASELINE configs[2] rides on every line
+    c3 = line["config3"]
+    assert set(CONFIG3_KEYS) <= set(c3), c3
+    assert c3["check"] is True and c3["algo"] == "csr5" and c3["n_gpus"] == 1
 
 
 @pytest.mark.parametrize("gpus,algo,partition,exchange", [
@@ -69,3 +75,28 @@ def test_bench_ctx_loopback(gpus, algo, partition, exchange):
     assert line["n_gpus"] == gpus and "loopback" in line["note"]
     assert len(line["kernel_ms_per_device"]) == gpus
     assert sum(line["nnz_per_device"]) == line["config"]["nnz"]
+    c3 = line["config3"]
+    assert c3["check"] is True and c3["n_gpus"] == gpus and c3["exchange"] == "allreduce", c3
+    assert sum(c3["nnz_per_device"]) == line["config"]["nnz"]
+
+
+def test_bench_ctx_loopback_full_config3():
+    """`bench.py --gpus 8 --ctx-loopback --check` on the
+    FULL n = 2e6 matrix (39.75M nnz): the default leg (cyclic chunks, the
+    library's kernel per slice, all-gather + placement) and the configs[2]
+    leg (CSR5 on the nnz split, all-reduce of the zero-padded y) both checked
+    against the oracle under the per-row fp64 bound, every rank's y
+    bit-identical.  8 context ranks share the box's GPU (loopback
+    collectives); the first 8-GPU run executes the same code with RCCL."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--ctx-loopback", "--check",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["config"]["nnz"] == 39_750_000 and line["n_gpus"] == 8
+    assert line["check_vs_oracle"] is True, line
+    c3 = line["config3"]
+    assert set(CONFIG3_KEYS) <= set(c3), c3
+    assert c3["check"] is True and c3["n_gpus"] == 8 and c3["exchange"] == "allreduce", c3
+    assert len(c3["kernel_ms_per_device"]) == 8 and sum(c3["nnz_per_device"]) == 39_750_000

@@ -195,9 +195,14 @@ def bench_2rank(extra, nrows=2_000_000):
          "panel_nnz_allgather", "xsort_cyclic_overlap_halves"])
 def test_config3_two_ranks(extra):
     """BASELINE configs[2]'s dataflow on 2 ranks at full size, checked."""
-    out = bench_2rank(extra)
+    cfg3 = extra[1] == "csr5" and "allreduce" in extra
+    out = bench_2rank(extra if cfg3 else extra + ["--no-config3"])
     assert out["n_gpus"] == 2 and out["check_vs_oracle"] is True, out
     assert out["config"]["nnz"] == 39_750_000
+    if cfg3:  # the line's configs[2] leg (torch path: one process per rank)
+        c3 = out["config3"]
+        assert c3["check"] is True and c3["n_gpus"] == 2 and c3["exchange"] == "allreduce", c3
+        assert sum(c3["nnz_per_device"]) == 39_750_000
 
 
 @pytest.mark.parametrize("split", ["rows", "cols"])
