@@ -466,7 +466,12 @@ def run_ctx(args) -> int:
         os.dup2(saved_fd, 1)
         os.close(saved_fd)
     t0 = time.perf_counter()
-    ctx.upload(n, n, rowptr, col, val, algo, partition, exchange)
+    if args.overlap > 1 and partition == 0 and exchange == sblas.CTX_ALLGATHER:
+        # exchange overlapped over K parts of each device's chunks
+        ctx.upload_parts(n, n, rowptr, col, val, algo, args.overlap)
+    else:
+        ctx.upload(n, n, rowptr, col, val, algo, partition, exchange)
+    parts = ctx.parts()
     plan_s = time.perf_counter() - t0
     # AUTO: each device's slice decided by the library (sblas_csr_pick); the
     # line names device 0's and lists all of them
@@ -559,6 +564,7 @@ def run_ctx(args) -> int:
             "partition": ("cyclic row chunks" if partition == 0 else "nnz-balanced (spMV_mgpu_v1)"),
             "exchange": args.exchange if exchange == sblas.CTX_ALLREDUCE else "allgather",
             "driver": "ctx (one process, sblas_ctx over RCCL, ncclCommInitAll)",
+            "overlap_parts": parts,
         },
         "roofline": {
             "bound": "hbm",
@@ -654,9 +660,10 @@ def main() -> int:
                          "pay) or read+write (add_, round 1's method)")
     ap.add_argument("--no-rowsplit-beside", action="store_true",
                     help="skip the row-split kernel's figure reported beside the headline")
-    ap.add_argument("--overlap", action="store_true",
-                    help="N>1 cyclic allgather: split each rank's chunks in two halves and "
-                         "all-gather the first while the kernel runs on the second")
+    ap.add_argument("--overlap", nargs="?", type=int, const=2, default=0, metavar="K",
+                    help="N>1 cyclic allgather: cut each rank's chunks into K parts (default 2) "
+                         "and all-gather part p while the kernel runs part p+1 (ctx driver: "
+                         "sblas_ctx_matrix_upload_parts, any K; torch driver: two halves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-always", action="store_true",
                     help="join a process group even at WORLD_SIZE 1 (torchrun --nproc-per-node 1): "
@@ -721,7 +728,7 @@ def main() -> int:
         lrp, col, val = sblas_dist.cyclic_local_csr(rowptr, plan, rank, W.rows)
         t_gen = time.perf_counter() - t_gen
         op = sblas_dist.DistSpMVCyclic(plan, rank, dev_idx, lrp, col, val, algo, torch, dist,
-                                       overlap=args.overlap)
+                                       overlap=args.overlap > 0)
         local_nnz = int(lrp[-1])
         partition = f"cyclic row chunks ({plan.chunk_rows} rows, {plan.nchunks} chunks)"
         if op.overlap:

@@ -100,3 +100,18 @@ def test_bench_ctx_loopback_full_config3():
     assert set(CONFIG3_KEYS) <= set(c3), c3
     assert c3["check"] is True and c3["n_gpus"] == 8 and c3["exchange"] == "allreduce", c3
     assert len(c3["kernel_ms_per_device"]) == 8 and sum(c3["nnz_per_device"]) == 39_750_000
+
+
+@pytest.mark.parametrize("gpus,parts", [(2, 2), (4, 4), (8, 2), (8, 4)])
+def test_bench_ctx_loopback_overlap(gpus, parts):
+    """`bench.py --gpus N --overlap K` through the ctx driver (loopback): the
+    exchange overlapped over K parts of every rank's chunks, checked."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--ctx-loopback", "--check",
+           "--nrows", "200000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-config3",
+           "--overlap", str(parts)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["check_vs_oracle"] is True, line
+    assert line["config"]["overlap_parts"] == parts

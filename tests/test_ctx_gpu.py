@@ -197,3 +197,66 @@ def test_ctx_loopback_multi_rank(torch_cuda, sb, orc, monkeypatch, g, algo, part
         y = got[0]
     assert sum(ctx.slice_info(d)[1] for d in range(g)) == int(rp[-1])
     ctx.close()
+
+
+@pytest.mark.parametrize("g", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("parts", [2, 4])
+@pytest.mark.parametrize("algo", [0, 1, 2, 5])
+def test_ctx_overlap_parts(torch_cuda, sb, orc, monkeypatch, g, parts, algo):
+    """The overlapped exchange (sblas_ctx_matrix_upload_parts; VERDICT r03
+    item 2): each rank's cyclic chunks in `parts` groups, part p all-gathered
+    and placed on the comm stream while part p + 1's kernel runs.  g > 1 in
+    loopback (collectives = stream-ordered copies); g = 1 through a one-rank
+    RCCL communicator.  Three chained steps, every rank's y within the fp64
+    bound of the oracle and bit-identical to rank 0's."""
+    if g > 1:
+        monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    rng = np.random.default_rng(1000 * g + 10 * parts + algo)
+    m, n = 7000, 9000
+    rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(2, 7000), (3000, 8000), (6999, 3000)])
+    x = rng.standard_normal(n)
+    y = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(g)
+    ctx.upload_parts(m, n, rp, col, val, algo, parts)
+    assert ctx.parts() == parts
+    ctx.set_x(x)
+    ctx.set_y(y)
+    for step in range(3):
+        st = ctx.spmv_ex(alpha, beta, delay_us=100.0 if step == 1 else 0.0)
+        assert st.shape == (3 + 3 * g,) and st[2] >= st[0] > 0
+        want = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+        bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y)
+        got = [ctx.get_y(d) for d in range(g)]
+        assert np.all(np.abs(got[0] - want) <= bound), (step, np.max(np.abs(got[0] - want) - bound))
+        for d in range(1, g):
+            assert np.array_equal(got[0], got[d]), (step, d)
+        y = got[0]
+    ctx.close()
+
+
+def test_ctx_overlap_config2_full_size_g8(torch_cuda, sb, orc, monkeypatch):
+    """Config 2 at full size (n = 2e6, 39.75M nnz) over 8 loopback ranks with
+    the exchange overlapped in 2 and 4 parts: y within the bound, every rank
+    bit-identical."""
+    monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    n = 2_000_000
+    rp = sb.gen_synth_rowptr(n)
+    col, val = sb.gen_synth_rows(n, rp, 0, n)
+    x = sb.gen_vector(n, 43)
+    y0 = sb.gen_vector(n, 44)
+    alpha, beta = orc.alpha_beta()
+    want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
+    bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y0)
+    for parts in (2, 4):
+        ctx = sb.DeviceCtx(8)
+        ctx.upload_parts(n, n, rp, col, val, 0, parts)
+        assert ctx.parts() == parts
+        ctx.set_x(x)
+        ctx.set_y(y0)
+        ctx.spmv_ex(alpha, beta)
+        got = [ctx.get_y(d) for d in range(8)]
+        assert np.all(np.abs(got[0] - want) <= bound), parts
+        for d in range(1, 8):
+            assert np.array_equal(got[0], got[d]), (parts, d)
+        ctx.close()
