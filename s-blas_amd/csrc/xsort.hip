@@ -55,7 +55,14 @@
 namespace sblas {
 
 constexpr int kXsThreads = 1024;
-constexpr int kXsRows = 16384;     // LDS row accumulators per workgroup (128 KiB)
+// LDS row accumulators per workgroup: 16384 = 128 KiB (default); an
+// experiment build may raise it towards the 160 KiB of a gfx950 CU
+// (SBLAS_XS_LDS_ROWS=19456: 152 KiB of rows + ~6 KiB of bookkeeping)
+#ifndef SBLAS_XS_LDS_ROWS
+#define SBLAS_XS_LDS_ROWS 16384
+#endif
+constexpr int kXsRows = SBLAS_XS_LDS_ROWS;
+static_assert(kXsRows % 512 == 0, "two teams of whole 256-row blocks");
 constexpr int kXsHalfRows = kXsRows / 2;
 constexpr int kXsRowBits = 14;     // packed key: local row in the low 14 bits
 constexpr int kXsColBits = 18;     //             group-local column above
@@ -78,7 +85,10 @@ constexpr int kK24Span = (1 << (24 - kK24RowBits)) - 2;  // largest column offse
 constexpr int kK24Bytes = 1024 + 2560 + 32;              // keys | values | header
 static_assert(kK24Bytes % 16 == 0, "16-B aligned chunks");
 static_assert(kXsRowBits + kXsColBits == 32, "packed key is 32 bits");
-static_assert(kXsRows <= (1 << kXsRowBits), "local row must fit the key");
+static_assert(kXsHalfRows <= (1 << kXsRowBits), "a team's local row must fit the key");
+// a range's rows: a team's half, or (unpaired / solo items) the whole
+// workgroup's accumulators up to what the key's row field addresses
+constexpr int kXsItemRows = kXsRows < (1 << kXsRowBits) ? kXsRows : (1 << kXsRowBits);
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -1027,14 +1037,14 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     const bool all_wide = getenv("SBLAS_XS_ALLWIDE") && atoi(getenv("SBLAS_XS_ALLWIDE")) != 0;
     const bool no_wide = getenv("SBLAS_XS_NOWIDE") && atoi(getenv("SBLAS_XS_NOWIDE")) != 0;
     const bool nosort = getenv("SBLAS_XS_NOSORT") && atoi(getenv("SBLAS_XS_NOSORT")) != 0;
-    int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsRows;
+    int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsItemRows;
     if (const char *e = getenv("SBLAS_XS_ROWS")) rows_cap = std::max(1, std::min(rows_cap, atoi(e)));
     // solo narrow items (SBLAS_XS_SOLO=1, paired dynamic kernel): a narrow
     // range is an item of its own -- both teams' waves and all 16,384 LDS
     // rows -- so its blocks are twice as dense (fewer x line requests per
     // entry); wide ranges still pair (wide, wide) at 8,192 rows a team
     P.solo = P.pair && P.dyn && getenv("SBLAS_XS_SOLO") && atoi(getenv("SBLAS_XS_SOLO")) != 0;
-    const int nrows_cap = P.solo ? kXsRows : rows_cap;  // narrow ranges
+    const int nrows_cap = P.solo ? kXsItemRows : rows_cap;  // narrow ranges
     const double nfac = P.solo ? 2.0 : 1.0;             // a narrow range's cost, in sub-item caps
 
     // Cost model (work units ~ one streamed entry): a sub-item's time is its

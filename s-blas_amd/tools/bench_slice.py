@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--warm-x", action="store_true",
                     help="experiment: read x after each scrub (x in the Infinity Cache and L2s "
                          "when the timed span starts; the matrix stays cold)")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="also time the slice cut into K parts of consecutive local chunks (the "
+                         "overlapped exchange's kernels, sblas_ctx_matrix_upload_parts): the K "
+                         "launches back to back after a cold sweep, events between them")
     ap.add_argument("--floor", action="store_true",
                     help="also time a cold streaming read of the slice's byte count")
     args = ap.parse_args()
@@ -82,6 +86,9 @@ def main():
                                               stream.cuda_stream))
                 out["cold_span_us"] = round(float(np.median(spans[2:])) * 1e3, 1)
                 out["cold_span_min_us"] = round(float(np.min(spans[2:])) * 1e3, 1)
+            if args.parts > 1:
+                out.update(time_parts(args, plan, lrp, col, val, n, algos[name], A.pick() if algos[name] == 0
+                                      else algos[name], x, scrub, stream, torch, sblas))
             A.close()
             print(json.dumps({"world": world, "algo": name, "local_rows": int(len(lrp) - 1),
                               "local_nnz": int(lrp[-1]), **out}), flush=True)
@@ -107,6 +114,44 @@ def main():
                               "bytes": nbytes, "us": round(us, 1),
                               "gbps": round(nbytes / us / 1e3, 1)}), flush=True)
             del buf
+
+
+def time_parts(args, plan, lrp, col, val, n, algo, resolved, x, scrub, stream, torch, sblas):
+    """The slice in K parts of consecutive local chunks, as the ctx's
+    overlapped exchange cuts it (ctx.hip upload_parts): cold sweep, then the
+    K launches back to back; per-part event spans (median over reps)."""
+    K, R = args.parts, plan.chunk_rows
+    lm = len(lrp) - 1
+    ncmax = plan.stride // R
+    bounds = [min(lm, (p * ncmax // K) * R) for p in range(K + 1)]
+    bounds[-1] = lm
+    handles = []
+    for p in range(K):
+        r0, r1 = bounds[p], bounds[p + 1]
+        if r1 <= r0:
+            continue
+        H = sblas.DeviceCSR.upload_slice(0, n, lrp, col, val, r0, r1, int(lrp[r0]), int(lrp[r1]))
+        H.analyse(resolved)
+        handles.append((H, r0))
+    y = torch.zeros(lm, dtype=torch.float64, device=x.device)
+    per = []
+    with torch.cuda.stream(stream):
+        for k in range(args.reps + 2):
+            scrub.sum(dtype=torch.int64)
+            torch.cuda.synchronize()
+            torch.cuda._sleep(500_000)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(handles) + 1)]
+            ev[0].record(stream)
+            for j, (H, r0) in enumerate(handles):
+                H.spmv(resolved, 1.0, x.data_ptr(), 0.5, y.data_ptr() + 8 * r0, stream.cuda_stream)
+                ev[j + 1].record(stream)
+            torch.cuda.synchronize()
+            per.append([ev[j].elapsed_time(ev[j + 1]) for j in range(len(handles))])
+    for H, _ in handles:
+        H.close()
+    med = np.median(np.array(per[2:]), axis=0) * 1e3
+    return {"parts": len(handles), "parts_cold_us": [round(float(v), 1) for v in med],
+            "parts_total_cold_us": round(float(np.sum(med)), 1)}
 
 
 if __name__ == "__main__":

@@ -4,6 +4,8 @@
 //
 //   spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0=cyclic|1=nnz] [reps]
 //            [exchange 0=allgather|1=allreduce (needs partition 1)]
+//            [parts K: cyclic + allgather with the exchange overlapped over K
+//             parts of each device's chunks, sblas_ctx_matrix_upload_parts]
 //
 // `spmv_ctx 8 2000000 2 1 20 1` is BASELINE configs[2] from C++: the CSR5
 // kernel on spMV_mgpu_v1's nnz split over 8 GPUs, y merged by ncclAllReduce.
@@ -26,7 +28,7 @@
 int main(int argc, char **argv)
 {
     if (argc < 3) {
-        printf("Usage: ./spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0|1] [reps] [exchange 0|1]\n");
+        printf("Usage: ./spmv_ctx <ngpu> <n> [algo 1|2|4|5] [partition 0|1] [reps] [exchange 0|1] [parts]\n");
         return -1;
     }
     const int ngpu = atoi(argv[1]);
@@ -35,6 +37,7 @@ int main(int argc, char **argv)
     const int part = argc > 4 ? atoi(argv[4]) : 0;
     const int reps = argc > 5 ? atoi(argv[5]) : 10;
     const int xchg = argc > 6 ? atoi(argv[6]) : SBLAS_CTX_ALLGATHER;
+    const int parts = argc > 7 ? atoi(argv[7]) : 1;
     std::vector<long long> rp((size_t)n + 1);
     sblas_gen_synth_rowptr(n, 96, 9, rp.data());
     const long long nnz = rp[(size_t)n];
@@ -54,7 +57,10 @@ int main(int argc, char **argv)
         return 1;
     }
     const double t0 = sblas_get_time();
-    st = sblas_ctx_matrix_upload_ex(ctx, n, n, rp.data(), col.data(), val.data(), algo, part, xchg);
+    if (parts > 1 && part == 0 && xchg == SBLAS_CTX_ALLGATHER)
+        st = sblas_ctx_matrix_upload_parts(ctx, n, n, rp.data(), col.data(), val.data(), algo, parts);
+    else
+        st = sblas_ctx_matrix_upload_ex(ctx, n, n, rp.data(), col.data(), val.data(), algo, part, xchg);
     const double t_up = sblas_get_time() - t0;
     if (st == SBLAS_OK) st = sblas_ctx_set_x(ctx, x.data());
     if (st != SBLAS_OK) {

@@ -151,13 +151,14 @@ def test_ctx_rejects_shared_devices(torch_cuda, sb):
         sb.DeviceCtx(2, devices=[0, 0])
 
 
-@pytest.mark.parametrize("algo,partition,exchange", [(5, 0, 0), (2, 1, 0), (1, 0, 0), (2, 1, 1)])
-def test_cli_spmv_ctx(algo, partition, exchange):
+@pytest.mark.parametrize("algo,partition,exchange,parts", [(5, 0, 0, 1), (2, 1, 0, 1), (1, 0, 0, 1), (2, 1, 1, 1),
+                                                           (5, 0, 0, 4), (1, 0, 0, 2)])
+def test_cli_spmv_ctx(algo, partition, exchange, parts):
     """The C++ driver (tools/spmv_ctx.cpp): a C caller reaching the RCCL path
     with no Python; it checks device agreement, the host-merge reference API
     and the bound reference API."""
     exe = os.path.join(ROOT, "s-blas_amd", "bin", "spmv_ctx")
-    r = subprocess.run([exe, "1", "2000000", str(algo), str(partition), "5", str(exchange)],
+    r = subprocess.run([exe, "1", "2000000", str(algo), str(partition), "5", str(exchange), str(parts)],
                        capture_output=True,
                        text=True, timeout=120, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr
