@@ -342,6 +342,7 @@ __global__ void k_c5_transpose(const int *__restrict__ col, const double *__rest
 }
 
 // One wave64 tile t of a CSR5 plan (caller: t < ntiles, wave-uniform).
+// (csr5_tile_pf below is the same tile with its loads issued in phases.)
 template <bool kBeta>
 __device__ __forceinline__ void csr5_tile(
     long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
@@ -435,7 +436,181 @@ __device__ __forceinline__ void csr5_tile(
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
 
+
+// The same tile with every load of a lane issued before the first use, in
+// phases the compiler may not interleave (sched_barrier):
+//   1. the stream (col quads, value pairs) and the tile's flags;
+//   2. the scan of row starts (shuffles, no memory), then -- gap tiles only --
+//      the rows of the lane's first kC5Pre segment ends;
+//   3. all 16 x gathers and the beta*y inputs of those kC5Pre rows;
+//   4. products, the segmented sum and the y stores.
+// The plain form lets the compiler interleave gathers with products (~8 in
+// flight per lane) and loads each row end's y inside the sum loop, one
+// dependent round trip per row end: on config 2's 9-entry rows (~2 row ends
+// per lane) that made the light rows alone take 215 us
+// (profiles/r04/split/).  Results are bit-identical to the plain form (same
+// products, same summation order).
+constexpr int kC5Pre = 4;
 template <bool kBeta>
+__device__ __forceinline__ void csr5_tile_pf(
+    long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+    const double *__restrict__ tval, const int *__restrict__ tcol,
+    const int *__restrict__ seg_off, const int *__restrict__ seg_row,
+    const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
+    double beta, double *__restrict__ y, double *__restrict__ carry)
+{
+    const int lane = threadIdx.x & 63;
+    const double *tv = tval + t * kC5Tile;
+    const int *tc = tcol + t * kC5Tile;
+    const uint32_t f = flags[t * 64 + lane];
+    const int trow = tile_row[t];
+    const bool gap = trow < 0;  // bit31: tile contains empty rows (wave-uniform)
+    const int r0 = trow & 0x7fffffff;
+    v4i cq[kC5Sigma / 4];
+    v2d vq[kC5Sigma / 2];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        cq[q] = ld_nt_v4i(tc + q * 256 + 4 * lane);
+        vq[2 * q] = ld_nt_v2d(tv + (2 * q) * 128 + 2 * lane);
+        vq[2 * q + 1] = ld_nt_v2d(tv + (2 * q + 1) * 128 + 2 * lane);
+    }
+    const int soff = gap ? seg_off[t] : 0;
+    __builtin_amdgcn_sched_barrier(0);
+
+    // exclusive prefix count of row starts over lanes -> segment index base
+    const int cnt = __popc(f);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const int segbase = incl - cnt;
+    const uint32_t f0 = __shfl(f, 0, 64);
+    const int first_row = (f0 & 1u) ? r0 : r0 + 1;  // row of segment 0 (no gaps)
+    // rows of the lane's first kC5Pre segment ends (index clamped into the
+    // lane's own segments; a lane without any reads the tile's first slot --
+    // a gap tile holds at least one row start -- and ignores it)
+    int qr[kC5Pre];
+    const int last = cnt - 1;
+    if (gap) {
+#pragma unroll
+        for (int j = 0; j < kC5Pre; ++j) qr[j] = seg_row[cnt > 0 ? soff + segbase + (j < last ? j : last) : soff];
+    } else {
+#pragma unroll
+        for (int j = 0; j < kC5Pre; ++j) qr[j] = first_row + segbase + j;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    double xv[kC5Sigma];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        xv[4 * q + 0] = x[cq[q].x];
+        xv[4 * q + 1] = x[cq[q].y];
+        xv[4 * q + 2] = x[cq[q].z];
+        xv[4 * q + 3] = x[cq[q].w];
+    }
+    double qy[kC5Pre];
+#pragma unroll
+    for (int j = 0; j < kC5Pre; ++j) qy[j] = 0.0;
+    if (kBeta) {
+#pragma unroll
+        for (int j = 0; j < kC5Pre; ++j)
+            if (j < cnt) qy[j] = y[qr[j]];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    double p[kC5Sigma];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        p[4 * q + 0] = vq[2 * q].x * xv[4 * q + 0];
+        p[4 * q + 1] = vq[2 * q].y * xv[4 * q + 1];
+        p[4 * q + 2] = vq[2 * q + 1].x * xv[4 * q + 2];
+        p[4 * q + 3] = vq[2 * q + 1].y * xv[4 * q + 3];
+    }
+    if (t == ntiles - 1) {  // zero the padding past nnz (x[0] may be inf/nan)
+        const long long e0 = t * kC5Tile + (long long)lane * kC5Sigma;
+#pragma unroll
+        for (int k = 0; k < kC5Sigma; ++k)
+            if (e0 + k >= nnz) p[k] = 0.0;
+    }
+    // row ends in segment order: the prefetched ones first (shift register,
+    // no dynamic register index), then loaded on the spot
+    int nq = 0;
+    auto next_row = [&](int sg, double &yin) {
+        int row;
+        if (nq < kC5Pre) {
+            row = qr[0];
+            yin = qy[0];
+#pragma unroll
+            for (int j = 0; j + 1 < kC5Pre; ++j) {
+                qr[j] = qr[j + 1];
+                qy[j] = qy[j + 1];
+            }
+        } else {
+            row = gap ? seg_row[soff + sg] : first_row + sg;
+            yin = kBeta ? y[row] : 0.0;
+        }
+        ++nq;
+        return row;
+    };
+
+    double head = 0.0, sum = 0.0;
+    int seg = -1;
+#pragma unroll
+    for (int k = 0; k < kC5Sigma; ++k) {
+        if ((f >> k) & 1u) {
+            if (seg < 0) {
+                head = sum;
+                seg = segbase;
+            } else {
+                double yin;
+                const int row = next_row(seg, yin);
+                y[row] = kBeta ? alpha * sum + beta * yin : alpha * sum;
+                ++seg;
+            }
+            sum = 0.0;
+        }
+        sum += p[k];
+    }
+    const bool has = seg >= 0;
+    if (!has) head = sum;
+
+    // suffix segmented scan: S_l = head_l + (has_l ? 0 : S_{l+1})
+    double S = head;
+    bool stop = has;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double vS = __shfl_down(S, off, 64);
+        const int vstop = __shfl_down((int)stop, off, 64);
+        if (!stop) {
+            if (lane + off < 64) {
+                S += vS;
+                stop = vstop != 0;
+            } else {
+                stop = true;
+            }
+        }
+    }
+    double Snext = __shfl_down(S, 1, 64);
+    if (lane == 63) Snext = 0.0;
+    if (has) {
+        double yin;
+        const int row = next_row(seg, yin);
+        const double tot = sum + Snext;
+        y[row] = kBeta ? alpha * tot + beta * yin : alpha * tot;
+    }
+    if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
+}
+
+// SBLAS_C5_PF=0 selects the plain tile (A/B timing); read once
+static bool c5_pf()
+{
+    static const bool on = !(getenv("SBLAS_C5_PF") && atoi(getenv("SBLAS_C5_PF")) == 0);
+    return on;
+}
+
+template <bool kBeta, bool kPf = true>
 __global__ __launch_bounds__(256) void k_spmv_csr5(
     const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
     const double *__restrict__ tval, const int *__restrict__ tcol,
@@ -445,7 +620,10 @@ __global__ __launch_bounds__(256) void k_spmv_csr5(
 {
     const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= ntiles) return;  // wave-uniform
-    csr5_tile<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
+    if constexpr (kPf)
+        csr5_tile_pf<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
+    else
+        csr5_tile<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
 }
 
 // CSR5 over XCD-affine column panels: block b runs tiles of panel b % P (the
@@ -796,13 +974,13 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
         if (beta != 0.0)
-            SBLAS_LAUNCH(k_spmv_csr5<true>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
-                               P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
-                               beta, y, P.carry);
+            SBLAS_LAUNCH((c5_pf() ? k_spmv_csr5<true, true> : k_spmv_csr5<true, false>), dim3(nb), dim3(256), 0, s,
+                         P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
+                         beta, y, P.carry);
         else
-            SBLAS_LAUNCH(k_spmv_csr5<false>, dim3(nb), dim3(256), 0, s, P.tile_row, P.flags,
-                               P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
-                               beta, y, P.carry);
+            SBLAS_LAUNCH((c5_pf() ? k_spmv_csr5<false, true> : k_spmv_csr5<false, false>), dim3(nb), dim3(256), 0,
+                         s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
+                         beta, y, P.carry);
         SBLAS_LAUNCH(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
                            0, s, P.tile_row, P.flags, P.carry, P.ntiles, alpha, y);
     }
