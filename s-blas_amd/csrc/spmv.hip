@@ -603,14 +603,143 @@ __device__ __forceinline__ void csr5_tile_pf(
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
 
-// SBLAS_C5_PF=0 selects the plain tile (A/B timing); read once
-static bool c5_pf()
+// Staged form: a tile without empty rows writes rows [first_row, first_row +
+// starts) -- consecutive -- so the lanes put their row sums into a per-wave
+// LDS run and the wave then reads y0 and writes y with coalesced 512-B wave
+// accesses (the first 128 rows' y0 loaded before the gathers), instead of
+// one scattered 8-B store (and load) per row end: a 9-entry-row tile ends
+// ~114 rows spread over 16 partially active store instructions.  Tiles with
+// empty rows take csr5_tile_pf.  Same products and sums: bit-identical.
+template <bool kBeta, bool kNt>
+__device__ __forceinline__ void csr5_tile_st(
+    long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+    const double *__restrict__ tval, const int *__restrict__ tcol,
+    const int *__restrict__ seg_off, const int *__restrict__ seg_row,
+    const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
+    double beta, double *__restrict__ y, double *__restrict__ carry, double *__restrict__ sy)
 {
-    static const bool on = !(getenv("SBLAS_C5_PF") && atoi(getenv("SBLAS_C5_PF")) == 0);
-    return on;
+    const int trow = tile_row[t];
+    if (trow < 0) {  // empty rows inside the tile (wave-uniform)
+        csr5_tile_pf<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y,
+                            carry);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const double *tv = tval + t * kC5Tile;
+    const int *tc = tcol + t * kC5Tile;
+    const uint32_t f = flags[t * 64 + lane];
+    const int r0 = trow;
+    v4i cq[kC5Sigma / 4];
+    v2d vq[kC5Sigma / 2];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        cq[q] = ld_nt_v4i(tc + q * 256 + 4 * lane);
+        vq[2 * q] = ld_nt_v2d(tv + (2 * q) * 128 + 2 * lane);
+        vq[2 * q + 1] = ld_nt_v2d(tv + (2 * q + 1) * 128 + 2 * lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int cnt = __popc(f);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const int segbase = incl - cnt;
+    const int total = __shfl(incl, 63, 64);  // row starts in the tile = rows it writes
+    const uint32_t f0 = __shfl(f, 0, 64);
+    const int first_row = (f0 & 1u) ? r0 : r0 + 1;
+    // y is touched once: non-temporal loads / stores keep it from displacing
+    // x lines in L2 (SBLAS_C5_PF=3 keeps plain accesses, A/B)
+    double y0a = 0.0, y0b = 0.0;
+    if (kBeta) {
+        if (lane < total) y0a = kNt ? __builtin_nontemporal_load(y + first_row + lane) : y[first_row + lane];
+        if (lane + 64 < total)
+            y0b = kNt ? __builtin_nontemporal_load(y + first_row + 64 + lane) : y[first_row + 64 + lane];
+    }
+    double xv[kC5Sigma];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        xv[4 * q + 0] = x[cq[q].x];
+        xv[4 * q + 1] = x[cq[q].y];
+        xv[4 * q + 2] = x[cq[q].z];
+        xv[4 * q + 3] = x[cq[q].w];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double p[kC5Sigma];
+#pragma unroll
+    for (int q = 0; q < kC5Sigma / 4; ++q) {
+        p[4 * q + 0] = vq[2 * q].x * xv[4 * q + 0];
+        p[4 * q + 1] = vq[2 * q].y * xv[4 * q + 1];
+        p[4 * q + 2] = vq[2 * q + 1].x * xv[4 * q + 2];
+        p[4 * q + 3] = vq[2 * q + 1].y * xv[4 * q + 3];
+    }
+    if (t == ntiles - 1) {  // zero the padding past nnz (x[0] may be inf/nan)
+        const long long e0 = t * kC5Tile + (long long)lane * kC5Sigma;
+#pragma unroll
+        for (int k = 0; k < kC5Sigma; ++k)
+            if (e0 + k >= nnz) p[k] = 0.0;
+    }
+    double head = 0.0, sum = 0.0;
+    int seg = -1;
+#pragma unroll
+    for (int k = 0; k < kC5Sigma; ++k) {
+        if ((f >> k) & 1u) {
+            if (seg < 0) {
+                head = sum;
+                seg = segbase;
+            } else {
+                sy[seg] = alpha * sum;
+                ++seg;
+            }
+            sum = 0.0;
+        }
+        sum += p[k];
+    }
+    const bool has = seg >= 0;
+    if (!has) head = sum;
+    double S = head;
+    bool stop = has;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double vS = __shfl_down(S, off, 64);
+        const int vstop = __shfl_down((int)stop, off, 64);
+        if (!stop) {
+            if (lane + off < 64) {
+                S += vS;
+                stop = vstop != 0;
+            } else {
+                stop = true;
+            }
+        }
+    }
+    double Snext = __shfl_down(S, 1, 64);
+    if (lane == 63) Snext = 0.0;
+    if (has) sy[seg] = alpha * (sum + Snext);
+    if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
+    // the wave's LDS writes are done before its reads (LDS keeps one wave's
+    // operations in order; the wait makes the data dependence explicit)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < total; i += 64) {
+        const double v = sy[i];
+        const double b = i < 64 ? y0a : i < 128 ? y0b : (kBeta ? y[first_row + i] : 0.0);
+        if (kNt)
+            __builtin_nontemporal_store(kBeta ? v + beta * b : v, y + first_row + i);
+        else
+            y[first_row + i] = kBeta ? v + beta * b : v;
+    }
 }
 
-template <bool kBeta, bool kPf = true>
+// SBLAS_C5_PF selects the tile form (A/B timing; read once): 0 plain,
+// 1 phased loads + prefetched row ends, 2 (default) staged y with
+// non-temporal y accesses, 3 staged y with plain accesses
+static int c5_form()
+{
+    static const int v = getenv("SBLAS_C5_PF") ? std::max(0, std::min(3, atoi(getenv("SBLAS_C5_PF")))) : 2;
+    return v;
+}
+
+template <bool kBeta, int kForm = 2>
 __global__ __launch_bounds__(256) void k_spmv_csr5(
     const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
     const double *__restrict__ tval, const int *__restrict__ tcol,
@@ -620,10 +749,15 @@ __global__ __launch_bounds__(256) void k_spmv_csr5(
 {
     const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= ntiles) return;  // wave-uniform
-    if constexpr (kPf)
+    if constexpr (kForm >= 2) {
+        __shared__ double s_y[4][kC5Tile + 1];  // one tile's row sums per wave
+        csr5_tile_st<kBeta, kForm == 2>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta,
+                                        y, carry, s_y[threadIdx.x >> 6]);
+    } else if constexpr (kForm == 1) {
         csr5_tile_pf<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
-    else
+    } else {
         csr5_tile<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y, carry);
+    }
 }
 
 // CSR5 over XCD-affine column panels: block b runs tiles of panel b % P (the
@@ -974,13 +1108,19 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
         if (beta != 0.0)
-            SBLAS_LAUNCH((c5_pf() ? k_spmv_csr5<true, true> : k_spmv_csr5<true, false>), dim3(nb), dim3(256), 0, s,
-                         P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
-                         beta, y, P.carry);
+            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5<true, 2>
+                          : c5_form() == 3 ? k_spmv_csr5<true, 3>
+                          : c5_form() == 1 ? k_spmv_csr5<true, 1>
+                                           : k_spmv_csr5<true, 0>),
+                         dim3(nb), dim3(256), 0, s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x,
+                         P.ntiles, A.nnz, alpha, beta, y, P.carry);
         else
-            SBLAS_LAUNCH((c5_pf() ? k_spmv_csr5<false, true> : k_spmv_csr5<false, false>), dim3(nb), dim3(256), 0,
-                         s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x, P.ntiles, A.nnz, alpha,
-                         beta, y, P.carry);
+            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5<false, 2>
+                          : c5_form() == 3 ? k_spmv_csr5<false, 3>
+                          : c5_form() == 1 ? k_spmv_csr5<false, 1>
+                                           : k_spmv_csr5<false, 0>),
+                         dim3(nb), dim3(256), 0, s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x,
+                         P.ntiles, A.nnz, alpha, beta, y, P.carry);
         SBLAS_LAUNCH(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
                            0, s, P.tile_row, P.flags, P.carry, P.ntiles, alpha, y);
     }
