@@ -266,7 +266,7 @@ CONFIG3 = ("BASELINE configs[2]: the same matrix, CSR5 segmented-sum kernel, row
 
 
 def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, check, how, exchange=None,
-                   **extra):
+                   traffic=None, **extra):
     """The `config3` object every bench line carries:
     kernel-only, exchange-only and total, max over devices."""
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9 if dev_kern[0] > 0 else 0.0
@@ -281,7 +281,7 @@ def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, chec
         "gflops": round(2.0 * nnz / (step_ms * 1e-3) / 1e9, 3),
         "kernel_only_gflops": round(2.0 * nnz / (kern_max * 1e-3) / 1e9, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved0, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved0 / HBM_PEAK_GBS, 4),
+                     "frac": round(achieved0 / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "aggregate_GBps": round(agg, 1), "aggregate_frac": round(agg / (HBM_PEAK_GBS * N), 4)},
         "kernel_ms_per_device": [round(k, 5) for k in dev_kern],
         "algorithmic_bytes_per_device": [int(b) for b in dev_bytes],
@@ -292,7 +292,7 @@ def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, chec
     return out
 
 
-def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us):
+def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us, profiled=False):
     """configs[2] through the C-ABI context: the matrix re-uploaded as CSR5
     slices of the nnz split with the SBLAS_CTX_ALLREDUCE exchange, timed with
     the default leg's cold protocol (scrub, device-side hold, aligning
@@ -322,7 +322,7 @@ def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us):
         N, float(np.mean(st[:, 0])), float(np.mean(st[:, 1])), float(np.mean(st[:, 2])), int(rowptr[-1]),
         dev_bytes, [float(np.mean(st[:, 3 + 3 * d])) for d in range(N)], check,
         "cold steps (1 GiB read sweep before each), sblas_ctx_spmv_ex per-device spans, max over devices",
-        exchange="allreduce", nnz_per_device=[int(z) for _, z, _ in info])
+        exchange="allreduce", traffic=pmc_traffic("csr5") if profiled else None, nnz_per_device=[int(z) for _, z, _ in info])
 
 
 def _oracle_check(rowptr, col, val, x_h, y0, ys):
@@ -422,6 +422,7 @@ def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx,
         ("cold steps: sblas_spmv_timed device span (one GPU, no exchange)" if world == 1 else
          "cold steps: HIP events on the launch stream around kernel and exchange after a device-side "
          "hold, max over ranks"),
+        traffic=pmc_traffic("csr5") if (world == 1 and W.default) else None,
         nnz_per_device=[int(plan.end_idx[d] - plan.start_idx[d] + 1) for d in range(world)])
 
 
@@ -539,7 +540,8 @@ def run_ctx(args) -> int:
         check = _oracle_check(rowptr, col, val, x_h, y0, ys)
     config3 = None
     if not args.no_config3:
-        config3 = ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us)
+        config3 = ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us,
+                              profiled=N == 1 and W.default)
     del scrubs
     total_flops = 2.0 * nnz
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
