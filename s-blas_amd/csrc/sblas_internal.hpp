@@ -55,7 +55,10 @@ LaunchTimer &launch_timer();
 
 // Row-split (CSR-adaptive) tuning. One 256-thread workgroup per row block.
 constexpr int kRsThreads = 256;
-constexpr int kRsBlockNnz = 2048;   // LDS product stream capacity (16 KiB f64)
+#ifndef SBLAS_RS_BLOCK_NNZ  // experiment builds only (Makefile `alt`)
+#define SBLAS_RS_BLOCK_NNZ 2048
+#endif
+constexpr int kRsBlockNnz = SBLAS_RS_BLOCK_NNZ;  // LDS product stream capacity (16 KiB f64)
 constexpr int kRsMaxRows = 1024;    // rows per stream block
 constexpr int kRsLongChunk = 8192;  // nnz per workgroup for long rows
 
