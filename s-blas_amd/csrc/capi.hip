@@ -201,19 +201,23 @@ namespace {
 // cnt = {adjacent, counted, then the sampled entries per eighth of the
 // columns [k*n/8, (k+1)*n/8): how evenly the x gathers would spread over the
 // XCDs' column groups of the column-sorted kernel}.
+constexpr int kProbeWords = 12;  // adjacent, counted, 8 eighths, scattered rows, sampled rows
 __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ rowptr,
                                                        const int *__restrict__ col, int m, int n, int S,
                                                        unsigned long long *cnt)
 {
     const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
     const int lane = threadIdx.x & 63;
-    if (w >= S) return;  // wave-uniform
-    const int r = (int)((long long)w * m / S);
-    const int a = rowptr[r];
-    const int b = min(rowptr[r + 1], a + 1024);
+    // waves past S count nothing (no early return: the block reduces below)
+    const int r = w < S ? (int)((long long)w * m / S) : 0;
+    const int a = w < S ? rowptr[r] : 0;
+    const int b = w < S ? min(rowptr[r + 1], a + 1024) : 0;
     unsigned adj = 0, tot = 0, h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int cmin = 0x7fffffff, cmax = -1;
     for (int e = a + lane; e < b; e += 64) {
         const int c = col[e];
+        cmin = min(cmin, c);
+        cmax = max(cmax, c);
         const int k = (int)min(7LL, max(0LL, (long long)c * 8 / max(n, 1)));
 #pragma unroll
         for (int q = 0; q < 8; ++q) h[q] += q == k ? 1u : 0u;
@@ -226,41 +230,71 @@ __global__ __launch_bounds__(256) void k_col_adjacency(const int *__restrict__ r
     for (int o = 32; o > 0; o >>= 1) {
         adj += __shfl_down(adj, o, 64);
         tot += __shfl_down(tot, o, 64);
+        cmin = min(cmin, __shfl_down(cmin, o, 64));
+        cmax = max(cmax, __shfl_down(cmax, o, 64));
 #pragma unroll
         for (int q = 0; q < 8; ++q) h[q] += __shfl_down(h[q], o, 64);
     }
-    if (lane == 0 && tot) {
-        atomicAdd(&cnt[0], (unsigned long long)adj);
-        atomicAdd(&cnt[1], (unsigned long long)tot);
-    }
-    if (lane == 0)
+    // a row whose columns span more than a quarter of x ("scattered": its
+    // gathers cannot stay in one XCD's share of x)
+    const unsigned wide = (w < S && b > a && (long long)(cmax - cmin) * 4 > (long long)n) ? 1u : 0u;
+    const unsigned sampled = (w < S && b > a) ? 1u : 0u;
+    // one partial per workgroup (its waves' sums added in LDS), stored plainly
+    // to part[blockIdx.x][10]; the host adds them (no memory-side atomics on
+    // ten shared words, which serialised the probe to ~5 ms on config 2)
+    __shared__ unsigned s_c[4][kProbeWords];
+    const int wv = (int)(threadIdx.x / 64);
+    if (lane == 0) {
+        s_c[wv][0] = adj;
+        s_c[wv][1] = tot;
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (h[q]) atomicAdd(&cnt[2 + q], (unsigned long long)h[q]);
+        for (int q = 0; q < 8; ++q) s_c[wv][2 + q] = h[q];
+        s_c[wv][10] = wide;
+        s_c[wv][11] = sampled;
+    }
+    __syncthreads();
+    if (threadIdx.x < kProbeWords) {
+        unsigned long long v = 0;
+        for (int k = 0; k < (int)(blockDim.x / 64); ++k) v += s_c[k][threadIdx.x];
+        cnt[(size_t)blockIdx.x * kProbeWords + threadIdx.x] = v;
+    }
 }
 
 constexpr long long kAutoXsortMinNnz = 2000000;  // bench slices: xsort leads from ~2M nnz
 
-int pick_algo(sblas_csr_s &A, hipStream_t s)
+}  // namespace
+
+extern "C++" {
+namespace sblas {
+// The column-locality probe (k_col_adjacency), run once per handle: fills
+// A.col_adjacency and A.col_maxshare.  Used by AUTO (pick_algo) and by the
+// CSR5 plan's panel choice (spmv.hip).
+int probe_columns(sblas_csr_s &A, hipStream_t s)
 {
-    if (A.auto_algo) return A.auto_algo;
+    if (A.col_adjacency >= 0.0) return SBLAS_OK;
     double adj = 0.0, share = 0.0;
     const int S = (int)std::min<long long>(A.m, 65536);
     if (S > 0 && A.nnz > 1) {
-        unsigned long long *d = nullptr, h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        hipError_t e = hipMalloc(&d, sizeof(h));
-        if (e == hipSuccess) e = hipMemsetAsync(d, 0, sizeof(h), s);
+        const int nb = (S + 3) / 4;
+        std::vector<unsigned long long> part((size_t)nb * kProbeWords);
+        unsigned long long *d = nullptr;
+        hipError_t e = hipMalloc(&d, sizeof(unsigned long long) * part.size());
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_col_adjacency, dim3((S + 3) / 4), dim3(256), 0, s, A.rowptr, A.col, A.m, A.n, S, d);
+            hipLaunchKernelGGL(k_col_adjacency, dim3(nb), dim3(256), 0, s, A.rowptr, A.col, A.m, A.n, S, d);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(part.data(), d, sizeof(unsigned long long) * part.size(), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (d) (void)hipFree(d);
         if (e != hipSuccess) {
-            set_error("sblas_csr_pick: %s", hipGetErrorString(e));
-            return -SBLAS_ERR_HIP;
+            set_error("column probe: %s", hipGetErrorString(e));
+            return SBLAS_ERR_HIP;
         }
+        unsigned long long h[kProbeWords] = {};
+        for (int b = 0; b < nb; ++b)
+            for (int q = 0; q < kProbeWords; ++q) h[q] += part[(size_t)b * kProbeWords + q];
+        A.col_scattered = h[11] ? (double)h[10] / (double)h[11] : 0.0;
         adj = h[1] ? (double)h[0] / (double)h[1] : 0.0;
         unsigned long long hs = 0, hm = 0;
         for (int q = 0; q < 8; ++q) {
@@ -271,6 +305,18 @@ int pick_algo(sblas_csr_s &A, hipStream_t s)
     }
     A.col_adjacency = adj;
     A.col_maxshare = share;
+    return SBLAS_OK;
+}
+}  // namespace sblas
+}  // extern "C++"
+
+namespace {
+
+int pick_algo(sblas_csr_s &A, hipStream_t s)
+{
+    if (A.auto_algo) return A.auto_algo;
+    if (const int st = probe_columns(A, s)) return -st;
+    const double adj = A.col_adjacency, share = A.col_maxshare;
     // The column-sorted kernel wherever it applies at size and its column
     // groups share the work: it leads on random columns (config 2: 0.51 of
     // 8 TB/s vs 0.21 row split) and on banded / stencil matrices too (3-D

@@ -316,6 +316,7 @@ struct sblas_csr_s {
     int auto_algo = 0;          // SBLAS_SPMV_AUTO's choice (capi.hip pick_algo), 0 = not yet
     double col_adjacency = -1;  // its locality probe
     double col_maxshare = -1;   // its largest eighth-of-the-columns share of the sampled entries
+    double col_scattered = -1;  // share of sampled rows whose columns span > n/4
 };
 
 namespace sblas {
@@ -327,6 +328,8 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s);
 int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
                      double beta, double *y, hipStream_t s);
 int build_csr5_plan(sblas_csr_s &A, hipStream_t s);
+// the column-locality probe (capi.hip): fills col_adjacency / col_maxshare once
+int probe_columns(sblas_csr_s &A, hipStream_t s);
 void free_plans(sblas_csr_s &A);
 
 int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x,

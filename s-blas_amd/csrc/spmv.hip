@@ -603,13 +603,15 @@ __device__ __forceinline__ void csr5_tile_pf(
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
 
-// Staged form: a tile without empty rows writes rows [first_row, first_row +
-// starts) -- consecutive -- so the lanes put their row sums into a per-wave
-// LDS run and the wave then reads y0 and writes y with coalesced 512-B wave
-// accesses (the first 128 rows' y0 loaded before the gathers), instead of
-// one scattered 8-B store (and load) per row end: a 9-entry-row tile ends
-// ~114 rows spread over 16 partially active store instructions.  Tiles with
-// empty rows take csr5_tile_pf.  Same products and sums: bit-identical.
+// Staged form: the lanes put their row sums into a per-wave LDS run (slot =
+// the row end's index among the tile's row starts), then the wave reads the
+// run and y0 and writes y with wave-wide accesses: rows [first_row, first_row
+// + starts) are consecutive in a tile without empty rows (one 512-B access
+// per 64 rows), and increasing, listed in seg_row, in a tile with empty rows.
+// The plain form issues one scattered 8-B store (and load) per row end: a
+// 9-entry-row tile ends ~114 rows spread over 16 partially active store
+// instructions.  The first 128 rows' y0 are loaded before the x gathers.
+// Same products and sums as csr5_tile: bit-identical.
 template <bool kBeta, bool kNt>
 __device__ __forceinline__ void csr5_tile_st(
     long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
@@ -618,17 +620,13 @@ __device__ __forceinline__ void csr5_tile_st(
     const double *__restrict__ x, long long ntiles, long long nnz, double alpha,
     double beta, double *__restrict__ y, double *__restrict__ carry, double *__restrict__ sy)
 {
-    const int trow = tile_row[t];
-    if (trow < 0) {  // empty rows inside the tile (wave-uniform)
-        csr5_tile_pf<kBeta>(t, tile_row, flags, tval, tcol, seg_off, seg_row, x, ntiles, nnz, alpha, beta, y,
-                            carry);
-        return;
-    }
     const int lane = threadIdx.x & 63;
     const double *tv = tval + t * kC5Tile;
     const int *tc = tcol + t * kC5Tile;
     const uint32_t f = flags[t * 64 + lane];
-    const int r0 = trow;
+    const int trow = tile_row[t];
+    const bool gap = trow < 0;  // bit31: tile contains empty rows (wave-uniform)
+    const int r0 = trow & 0x7fffffff;
     v4i cq[kC5Sigma / 4];
     v2d vq[kC5Sigma / 2];
 #pragma unroll
@@ -637,6 +635,7 @@ __device__ __forceinline__ void csr5_tile_st(
         vq[2 * q] = ld_nt_v2d(tv + (2 * q) * 128 + 2 * lane);
         vq[2 * q + 1] = ld_nt_v2d(tv + (2 * q + 1) * 128 + 2 * lane);
     }
+    const int soff = gap ? seg_off[t] : 0;
     __builtin_amdgcn_sched_barrier(0);
     const int cnt = __popc(f);
     int incl = cnt;
@@ -649,13 +648,19 @@ __device__ __forceinline__ void csr5_tile_st(
     const int total = __shfl(incl, 63, 64);  // row starts in the tile = rows it writes
     const uint32_t f0 = __shfl(f, 0, 64);
     const int first_row = (f0 & 1u) ? r0 : r0 + 1;
-    // y is touched once: non-temporal loads / stores keep it from displacing
-    // x lines in L2 (SBLAS_C5_PF=3 keeps plain accesses, A/B)
+    // rows of run slots lane and lane + 64
+    int ra = 0, rb = 0;
+    if (gap) {
+        if (lane < total) ra = seg_row[soff + lane];
+        if (lane + 64 < total) rb = seg_row[soff + 64 + lane];
+    } else {
+        ra = first_row + lane;
+        rb = first_row + 64 + lane;
+    }
     double y0a = 0.0, y0b = 0.0;
     if (kBeta) {
-        if (lane < total) y0a = kNt ? __builtin_nontemporal_load(y + first_row + lane) : y[first_row + lane];
-        if (lane + 64 < total)
-            y0b = kNt ? __builtin_nontemporal_load(y + first_row + 64 + lane) : y[first_row + 64 + lane];
+        if (lane < total) y0a = kNt ? __builtin_nontemporal_load(y + ra) : y[ra];
+        if (lane + 64 < total) y0b = kNt ? __builtin_nontemporal_load(y + rb) : y[rb];
     }
     double xv[kC5Sigma];
 #pragma unroll
@@ -722,11 +727,22 @@ __device__ __forceinline__ void csr5_tile_st(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (int i = lane; i < total; i += 64) {
         const double v = sy[i];
-        const double b = i < 64 ? y0a : i < 128 ? y0b : (kBeta ? y[first_row + i] : 0.0);
+        int row;
+        double b;
+        if (i < 64) {
+            row = ra;
+            b = y0a;
+        } else if (i < 128) {
+            row = rb;
+            b = y0b;
+        } else {
+            row = gap ? seg_row[soff + i] : first_row + i;
+            b = kBeta ? y[row] : 0.0;
+        }
         if (kNt)
-            __builtin_nontemporal_store(kBeta ? v + beta * b : v, y + first_row + i);
+            __builtin_nontemporal_store(kBeta ? v + beta * b : v, y + row);
         else
-            y[first_row + i] = kBeta ? v + beta * b : v;
+            y[row] = kBeta ? v + beta * b : v;
     }
 }
 
@@ -764,6 +780,7 @@ __global__ __launch_bounds__(256) void k_spmv_csr5(
 // hardware deals blocks to the XCDs round robin, so an XCD keeps to the
 // panels b % 8 selects: its x gathers stay in ~n*8/P bytes of x), writing
 // the panel's alpha-scaled partial y (beta applied by the reduce).
+template <int kForm>
 __global__ __launch_bounds__(256) void k_spmv_csr5_panel(const Csr5Desc *__restrict__ desc, int P,
                                                          const double *__restrict__ x, double alpha)
 {
@@ -771,8 +788,14 @@ __global__ __launch_bounds__(256) void k_spmv_csr5_panel(const Csr5Desc *__restr
     const long long t = (long long)(blockIdx.x / P) * 4 + (threadIdx.x >> 6);
     const Csr5Desc &d = desc[p];
     if (t >= d.ntiles) return;  // wave-uniform
-    csr5_tile<false>(t, d.tile_row, d.flags, d.tval, d.tcol, d.seg_off, d.seg_row, x, d.ntiles, d.nnz, alpha,
-                     0.0, d.y, d.carry);
+    if constexpr (kForm >= 2) {
+        __shared__ double s_y[4][kC5Tile + 1];  // one tile's row sums per wave
+        csr5_tile_st<false, kForm == 2>(t, d.tile_row, d.flags, d.tval, d.tcol, d.seg_off, d.seg_row, x, d.ntiles,
+                                        d.nnz, alpha, 0.0, d.y, d.carry, s_y[threadIdx.x >> 6]);
+    } else {
+        csr5_tile<false>(t, d.tile_row, d.flags, d.tval, d.tcol, d.seg_off, d.seg_row, x, d.ntiles, d.nnz, alpha,
+                         0.0, d.y, d.carry);
+    }
 }
 
 // Adds each tile's head (the part of the row that started in an earlier
@@ -1004,7 +1027,22 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     Csr5Plan &P = A.c5;
     const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
     const char *pe = getenv("SBLAS_CSR5_PANEL");
-    if (pe && atoi(pe) == 1 && !(hp && atoi(hp) == 1)) {
+    // Tiles per XCD column panel (each XCD's gathers in ~4 MiB of x) when x
+    // outgrows an XCD's L2, the rows' columns are scattered (the probe: most
+    // sampled rows span > n/4 of the columns, spread over the eighths) and
+    // the matrix is large enough to amortise the panels' partial-y pass:
+    // config 2 285 -> 251 us, its N = 2 slice 150 -> 137 us; N = 4 (9.9M nnz)
+    // even, N = 8 (5M) slower (profiles/r04/csr5_auto/).  Banded / stencil /
+    // prefix-column matrices keep the plain tiles, whose gathers share lines.
+    // SBLAS_CSR5_PANEL=1 / 0 forces either form.
+    bool panels = false;
+    if (pe) {
+        panels = atoi(pe) == 1;
+    } else if ((long long)A.n * 8 > (8LL << 20) && A.nnz >= 12000000LL) {
+        SBLAS_TRY(probe_columns(A, s));
+        panels = A.col_scattered >= 0.5 && A.col_maxshare <= 0.25;
+    }
+    if (panels && !(hp && atoi(hp) == 1)) {
         const int rc = build_csr5_panels(A, s);
         if (rc == SBLAS_OK) return SBLAS_OK;
         free_csr5_arrays(P);
@@ -1091,7 +1129,10 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
         if (A.m == 0) return SBLAS_OK;
         const long long grid = (P.maxtiles + 3) / 4 * P.P;
         if (grid > 0)
-            SBLAS_LAUNCH(k_spmv_csr5_panel, dim3((unsigned)grid), dim3(256), 0, s, P.desc, P.P, x, alpha);
+            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5_panel<2>
+                          : c5_form() == 3 ? k_spmv_csr5_panel<3>
+                                           : k_spmv_csr5_panel<0>),
+                         dim3((unsigned)grid), dim3(256), 0, s, P.desc, P.P, x, alpha);
         long long mc = P.maxtiles;
         for (const Csr5Plan &Q : P.panels) mc = std::max<long long>(mc, Q.nempty);
         if (mc > 0)
