@@ -87,6 +87,8 @@ struct Csr5Plan {
     int *empty_rows = nullptr;     // rows with no entries (y = beta*y)
     int nempty = 0;
     double *carry = nullptr;       // [ntiles] tile head partial sums
+    int *head_run = nullptr;       // [ntiles] > 0: tile t starts a run of that many tiles whose heads
+                                   // continue one row (calibrated together), else 0
     bool ready = false;
     // XCD-affine form (spmv.hip "CSR5 over column panels"): one tile plan per
     // column panel of the panel plan, panel p's tiles dealt to the XCDs with
@@ -111,8 +113,9 @@ struct Csr5Desc {
     double *carry;
     long long ntiles;
     long long nnz;
-    int nempty;
+    int nempty;  // empty rows zeroed per call (0: the partial's empty rows stay zero from the plan build)
     int pad;
+    const int *head_run;
 };
 
 // XCD-panel plan: A split into P column panels (x panel ~2 MiB), each a CSR

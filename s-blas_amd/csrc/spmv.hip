@@ -798,38 +798,53 @@ __global__ __launch_bounds__(256) void k_spmv_csr5_panel(const Csr5Desc *__restr
     }
 }
 
-// Adds each tile's head (the part of the row that started in an earlier
-// tile) to y, one thread per run of tiles sharing that row: deterministic.
+// Head runs, found once at plan build: tile t starts a run when its head
+// (the part of a row that started in an earlier tile) is not the
+// continuation of the previous tile's head row; head_run[t] = the number of
+// consecutive tiles whose heads belong to that row (else 0).
+__global__ void k_c5_headruns(const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+                              long long ntiles, int *__restrict__ head_run)
+{
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    auto has_head = [&](long long u) { return (flags[u * 64] & 1u) == 0u; };
+    int L = 0;
+    const int R = tile_row[t] & 0x7fffffff;
+    if (has_head(t) && !(t > 0 && (tile_row[t - 1] & 0x7fffffff) == R && has_head(t - 1)))
+        for (long long u = t; u < ntiles && (tile_row[u] & 0x7fffffff) == R && has_head(u); ++u) ++L;
+    head_run[t] = L;
+}
+
+// Adds each head run's carries (in tile order) to its row: deterministic.
 __device__ __forceinline__ void csr5_calibrate(long long t, const int *__restrict__ tile_row,
-                                               const uint32_t *__restrict__ flags,
+                                               const int *__restrict__ head_run,
                                                const double *__restrict__ carry, long long ntiles,
                                                double alpha, double *__restrict__ y)
 {
     if (t >= ntiles) return;
-    auto has_head = [&](long long u) { return (flags[u * 64] & 1u) == 0u; };
-    if (!has_head(t)) return;
+    const int L = head_run[t];
+    if (L == 0) return;
     const int R = tile_row[t] & 0x7fffffff;
-    if (t > 0 && (tile_row[t - 1] & 0x7fffffff) == R && has_head(t - 1)) return;
     double s = 0.0;
-    for (long long u = t; u < ntiles && (tile_row[u] & 0x7fffffff) == R && has_head(u); ++u)
-        s += carry[u];
+    for (int u = 0; u < L; ++u) s += carry[t + u];
     y[R] += alpha * s;
 }
 
-__global__ void k_csr5_calibrate(const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
+__global__ void k_csr5_calibrate(const int *__restrict__ tile_row, const int *__restrict__ head_run,
                                  const double *__restrict__ carry, long long ntiles, double alpha,
                                  double *__restrict__ y)
 {
-    csr5_calibrate((long long)blockIdx.x * blockDim.x + threadIdx.x, tile_row, flags, carry, ntiles, alpha, y);
+    csr5_calibrate((long long)blockIdx.x * blockDim.x + threadIdx.x, tile_row, head_run, carry, ntiles, alpha, y);
 }
 
-// panel form: blockIdx.y = panel; also zeroes the panel's empty rows
+// panel form: blockIdx.y = panel (the partials' empty rows were zeroed once
+// at plan build and are never written; d.nempty > 0 would zero them here)
 __global__ void k_csr5_calibrate_panel(const Csr5Desc *__restrict__ desc, double alpha)
 {
     const Csr5Desc &d = desc[blockIdx.y];
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d.nempty) d.y[d.empty_rows[i]] = 0.0;
-    csr5_calibrate(i, d.tile_row, d.flags, d.carry, d.ntiles, alpha, d.y);
+    csr5_calibrate(i, d.tile_row, d.head_run, d.carry, d.ntiles, alpha, d.y);
 }
 
 template <bool kBeta>
@@ -959,9 +974,13 @@ static int build_csr5_core(Csr5Plan &P, const int *rowptr, const int *col, const
     SBLAS_HIP(hipMalloc(&P.tval, sizeof(double) * std::max<long long>(total, 1)));
     SBLAS_HIP(hipMalloc(&P.tcol, sizeof(int) * std::max<long long>(total, 1)));
     SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
+    SBLAS_HIP(hipMalloc(&P.head_run, sizeof(int) * std::max<long long>(nt, 1)));
     if (total) {
         hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, col, val, nnz,
                            total, P.tcol, P.tval);
+        SBLAS_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_c5_headruns, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, P.tile_row, P.flags, nt,
+                           P.head_run);
         SBLAS_HIP(hipGetLastError());
     }
     SBLAS_HIP(hipStreamSynchronize(s));
@@ -979,6 +998,7 @@ static void free_csr5_arrays(Csr5Plan &P)
     (void)hipFree(P.seg_row);
     (void)hipFree(P.empty_rows);
     (void)hipFree(P.carry);
+    (void)hipFree(P.head_run);
     for (Csr5Plan &Q : P.panels) free_csr5_arrays(Q);
     (void)hipFree(P.desc);
     (void)hipFree(P.ypart);
@@ -1004,13 +1024,16 @@ static int build_csr5_panels(sblas_csr_s &A, hipStream_t s)
     P.panels.assign((size_t)Q.P, Csr5Plan{});
     std::vector<Csr5Desc> hd((size_t)Q.P);
     SBLAS_HIP(hipMalloc(&P.ypart, sizeof(double) * std::max<long long>(Q.P * m, 1)));
+    // a panel's empty rows get no segment, so their partials are never
+    // written: zero them here once instead of on every call
+    SBLAS_HIP(hipMemsetAsync(P.ypart, 0, sizeof(double) * std::max<long long>(Q.P * m, 1), s));
     for (int q = 0; q < Q.P; ++q) {
         int nz = 0;
         SBLAS_HIP(hipMemcpy(&nz, pd[(size_t)q].rowptr + m, sizeof(int), hipMemcpyDeviceToHost));
         Csr5Plan &S = P.panels[(size_t)q];
         SBLAS_TRY(build_csr5_core(S, pd[(size_t)q].rowptr, pd[(size_t)q].col, pd[(size_t)q].val, (int)m, nz, s));
-        hd[(size_t)q] = Csr5Desc{S.tile_row, S.flags, S.tval, S.tcol, S.seg_off, S.seg_row, S.empty_rows,
-                                 P.ypart + (size_t)q * m, S.carry, S.ntiles, (long long)nz, S.nempty, 0};
+        hd[(size_t)q] = Csr5Desc{S.tile_row, S.flags,    S.tval, S.tcol, S.seg_off, S.seg_row, S.empty_rows,
+                                 P.ypart + (size_t)q * m, S.carry, S.ntiles, (long long)nz, 0, 0, S.head_run};
         P.maxtiles = std::max(P.maxtiles, S.ntiles);
     }
     SBLAS_HIP(hipMalloc(&P.desc, sizeof(Csr5Desc) * Q.P));
@@ -1102,6 +1125,7 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     SBLAS_HIP(hipMalloc(&P.seg_row, sizeof(int) * std::max<size_t>(seg_row.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.empty_rows, sizeof(int) * std::max<size_t>(empty.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.carry, sizeof(double) * std::max<long long>(nt, 1)));
+    SBLAS_HIP(hipMalloc(&P.head_run, sizeof(int) * std::max<long long>(nt, 1)));
     SBLAS_HIP(hipMemcpyAsync(P.tile_row, trow.data(), sizeof(int) * (nt + 1), hipMemcpyHostToDevice, s));
     if (nt) SBLAS_HIP(hipMemcpyAsync(P.flags, flags.data(), sizeof(uint32_t) * nt * 64, hipMemcpyHostToDevice, s));
     SBLAS_HIP(hipMemcpyAsync(P.seg_off, seg_off.data(), sizeof(int) * (nt + 1), hipMemcpyHostToDevice, s));
@@ -1113,6 +1137,9 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     if (total) {
         hipLaunchKernelGGL(k_c5_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                            A.col, A.val, nnz, total, P.tcol, P.tval);
+        SBLAS_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_c5_headruns, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, P.tile_row, P.flags, nt,
+                           P.head_run);
         SBLAS_HIP(hipGetLastError());
     }
     SBLAS_HIP(hipStreamSynchronize(s));
@@ -1133,8 +1160,7 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
                           : c5_form() == 3 ? k_spmv_csr5_panel<3>
                                            : k_spmv_csr5_panel<0>),
                          dim3((unsigned)grid), dim3(256), 0, s, P.desc, P.P, x, alpha);
-        long long mc = P.maxtiles;
-        for (const Csr5Plan &Q : P.panels) mc = std::max<long long>(mc, Q.nempty);
+        const long long mc = P.maxtiles;
         if (mc > 0)
             SBLAS_LAUNCH(k_csr5_calibrate_panel, dim3((unsigned)((mc + 255) / 256), (unsigned)P.P), dim3(256), 0, s,
                          P.desc, alpha);
@@ -1163,7 +1189,7 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
                          dim3(nb), dim3(256), 0, s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x,
                          P.ntiles, A.nnz, alpha, beta, y, P.carry);
         SBLAS_LAUNCH(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),
-                           0, s, P.tile_row, P.flags, P.carry, P.ntiles, alpha, y);
+                           0, s, P.tile_row, P.head_run, P.carry, P.ntiles, alpha, y);
     }
     if (P.nempty) {
         if (beta != 0.0)
