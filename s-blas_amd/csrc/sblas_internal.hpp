@@ -291,6 +291,7 @@ struct RsPlan {
     double *partial = nullptr;     // [nslots]
     int nslots = 0;
     bool ready = false;
+    bool panels = false;           // run as the panel plan (XCD column panels, spmv.hip xcd_panels_pay)
 };
 
 }  // namespace sblas

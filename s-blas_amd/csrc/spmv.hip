@@ -238,6 +238,26 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
     }
 }
 
+// Whether a row-oriented kernel (row split, CSR5) should run over XCD column
+// panels (~4 MiB of x each, P = 4 partials added after): x outgrows an XCD's
+// L2, the rows' columns are scattered (the column probe: most sampled rows
+// span > n/4 of the columns, spread over the eighths) and the matrix is large
+// enough to amortise the partial-y pass.  Measured on config 2: CSR5 285 ->
+// 249 us, row split 307 -> ~240 us; its N = 4 slice (9.9M nnz) even, N = 8
+// (5M) slower (profiles/r04/csr5_auto/).  `env` = 1 / 0 forces either form.
+static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, bool *use)
+{
+    *use = false;
+    if (const char *e = getenv(env)) {
+        *use = atoi(e) == 1;
+        return SBLAS_OK;
+    }
+    if ((long long)A.n * 8 <= (8LL << 20) || A.nnz < 12000000LL) return SBLAS_OK;
+    SBLAS_TRY(probe_columns(A, s));
+    *use = A.col_scattered >= 0.5 && A.col_maxshare <= 0.25;
+    return SBLAS_OK;
+}
+
 int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.rs.ready) return SBLAS_OK;
@@ -263,6 +283,16 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
     }
     SBLAS_HIP(hipStreamSynchronize(s));
     A.rs.ready = true;
+    // the same row blocks per XCD column panel on large scattered matrices
+    // (the panel plan, algo 4's layout); SBLAS_RS_PANEL=1 / 0 forces
+    if (!A.pn.degenerate) {
+        bool use = false;
+        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", &use));
+        if (use) {
+            SBLAS_TRY(build_panel_plan(A, s));
+            A.rs.panels = !A.pn.degenerate;
+        }
+    }
     return SBLAS_OK;
 }
 
@@ -294,6 +324,7 @@ int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
                          double beta, double *y, hipStream_t s)
 {
     if (!A.rs.ready) return SBLAS_ERR_INVALID;
+    if (A.rs.panels) return launch_spmv_panel(A, alpha, x, beta, y, s);
     if (A.rs.nblocks == 0) return SBLAS_OK;
     static const int seq = [] {
         const char *e = getenv("SBLAS_RS_SEQ");
@@ -1058,13 +1089,9 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     // even, N = 8 (5M) slower (profiles/r04/csr5_auto/).  Banded / stencil /
     // prefix-column matrices keep the plain tiles, whose gathers share lines.
     // SBLAS_CSR5_PANEL=1 / 0 forces either form.
+    (void)pe;
     bool panels = false;
-    if (pe) {
-        panels = atoi(pe) == 1;
-    } else if ((long long)A.n * 8 > (8LL << 20) && A.nnz >= 12000000LL) {
-        SBLAS_TRY(probe_columns(A, s));
-        panels = A.col_scattered >= 0.5 && A.col_maxshare <= 0.25;
-    }
+    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", &panels));
     if (panels && !(hp && atoi(hp) == 1)) {
         const int rc = build_csr5_panels(A, s);
         if (rc == SBLAS_OK) return SBLAS_OK;
