@@ -224,3 +224,24 @@ def test_spmm_multi_rank_config4(split, ranks):
     assert res["n_gpus"] == ranks and res["config"]["nnz"] == 11_279_748, res
     chk = res["check_vs_oracle"]
     assert chk["entries"] == 4284 * 64 and chk["pass"] and chk["abs_1e-3"], chk
+
+
+def test_torchrun_8_ranks_full_size():
+    """The path the driver's 8-GPU scaling run takes (torch.distributed.run,
+    one process per rank, `bench.py --gpus 8`), rehearsed with 8 ranks sharing
+    the box's GPU over gloo at the full config-2 size: the default leg
+    (cyclic chunks, all-gather + placement) and the configs[2] leg (CSR5 on
+    the nnz split, all-reduce of y) both checked against the oracle, every
+    rank's configs[2] y bit-identical."""
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+            os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1",
+            "--dist-backend", "gloo", "--check", "--no-cpu-baseline"]
+    rc, out, err = run(args, timeout=115)
+    assert rc == 0, out[-3000:] + err[-3000:]
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["check_vs_oracle"] is True, line
+    assert line["config"]["nnz"] == 39_750_000
+    c3 = line["config3"]
+    assert c3["check"] is True and c3["n_gpus"] == 8 and c3["exchange"] == "allreduce", c3
+    assert len(c3["kernel_ms_per_device"]) == 8 and sum(c3["nnz_per_device"]) == 39_750_000
