@@ -168,6 +168,12 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
  * is unsupported for the matrix, sblas_csr_analyse falls back to PANEL and the
  * choice becomes PANEL.  SBLAS_AUTO=<1..5> overrides the choice. */
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
+/* XCD column panels the analysed plan of `algo` runs over (0: the plain
+ * layout / not analysed).  ROWSPLIT and CSR5 build per-panel plans on large
+ * scattered-column matrices (x > 8 MiB, nnz >= 12M, most sampled rows span
+ * > n/4 of the columns; SBLAS_RS_PANEL / SBLAS_CSR5_PANEL = 0 / 1 force);
+ * PANEL always does (unless only one panel holds entries). */
+int sblas_csr_panels(sblas_csr A, int algo, int *panels);
 /* Device bytes held by the analysis of `algo` (free memory before - after
  * sblas_csr_analyse; 0 if not analysed): the layout's cost beside the CSR. */
 long long sblas_csr_plan_bytes(sblas_csr A, int algo);

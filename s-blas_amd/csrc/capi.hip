@@ -399,6 +399,19 @@ int sblas_csr_analyse(sblas_csr A, int algo, void *stream)
     return st;
 }
 
+int sblas_csr_panels(sblas_csr A, int algo, int *panels)
+{
+    if (!A || !panels) return SBLAS_ERR_INVALID;
+    switch (algo) {
+    case SBLAS_SPMV_ROWSPLIT: *panels = A->rs.ready && A->rs.panels ? A->pn.P : 0; break;
+    case SBLAS_SPMV_CSR5:
+    case SBLAS_SPMV_CSR5_ALT: *panels = A->c5.ready ? A->c5.P : 0; break;
+    case SBLAS_SPMV_PANEL: *panels = A->pn.ready && !A->pn.degenerate ? A->pn.P : 0; break;
+    default: *panels = 0; break;
+    }
+    return SBLAS_OK;
+}
+
 long long sblas_csr_plan_bytes(sblas_csr A, int algo)
 {
     if (!A || algo < 0 || algo > SBLAS_SPMV_XSORT) return -1;

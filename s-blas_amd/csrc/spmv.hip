@@ -326,10 +326,8 @@ int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
     if (!A.rs.ready) return SBLAS_ERR_INVALID;
     if (A.rs.panels) return launch_spmv_panel(A, alpha, x, beta, y, s);
     if (A.rs.nblocks == 0) return SBLAS_OK;
-    static const int seq = [] {
-        const char *e = getenv("SBLAS_RS_SEQ");
-        return e ? atoi(e) : 1;
-    }();
+    const char *seq_env = getenv("SBLAS_RS_SEQ");  // read per launch (tests switch it)
+    const int seq = seq_env ? atoi(seq_env) : 1;
     if (beta != 0.0) {
         auto kern = seq ? k_spmv_rowsplit<true, true> : k_spmv_rowsplit<true, false>;
         SBLAS_LAUNCH(kern, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
@@ -782,8 +780,8 @@ __device__ __forceinline__ void csr5_tile_st(
 // non-temporal y accesses, 3 staged y with plain accesses
 static int c5_form()
 {
-    static const int v = getenv("SBLAS_C5_PF") ? std::max(0, std::min(3, atoi(getenv("SBLAS_C5_PF")))) : 2;
-    return v;
+    const char *e = getenv("SBLAS_C5_PF");  // read per launch (tests switch it within one process)
+    return e ? std::max(0, std::min(3, atoi(e))) : 2;
 }
 
 template <bool kBeta, int kForm = 2>
@@ -1201,18 +1199,19 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     }
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
+        const int form = c5_form();
         if (beta != 0.0)
-            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5<true, 2>
-                          : c5_form() == 3 ? k_spmv_csr5<true, 3>
-                          : c5_form() == 1 ? k_spmv_csr5<true, 1>
-                                           : k_spmv_csr5<true, 0>),
+            SBLAS_LAUNCH((form == 2   ? k_spmv_csr5<true, 2>
+                          : form == 3 ? k_spmv_csr5<true, 3>
+                          : form == 1 ? k_spmv_csr5<true, 1>
+                                      : k_spmv_csr5<true, 0>),
                          dim3(nb), dim3(256), 0, s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x,
                          P.ntiles, A.nnz, alpha, beta, y, P.carry);
         else
-            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5<false, 2>
-                          : c5_form() == 3 ? k_spmv_csr5<false, 3>
-                          : c5_form() == 1 ? k_spmv_csr5<false, 1>
-                                           : k_spmv_csr5<false, 0>),
+            SBLAS_LAUNCH((form == 2   ? k_spmv_csr5<false, 2>
+                          : form == 3 ? k_spmv_csr5<false, 3>
+                          : form == 1 ? k_spmv_csr5<false, 1>
+                                      : k_spmv_csr5<false, 0>),
                          dim3(nb), dim3(256), 0, s, P.tile_row, P.flags, P.tval, P.tcol, P.seg_off, P.seg_row, x,
                          P.ntiles, A.nnz, alpha, beta, y, P.carry);
         SBLAS_LAUNCH(k_csr5_calibrate, dim3((unsigned)((P.ntiles + 255) / 256)), dim3(256),

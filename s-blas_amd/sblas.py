@@ -121,6 +121,7 @@ _sig("sblas_ctx_slice_info", _i, _p, _i, _p, _p, _p)
 _sig("sblas_ctx_slice_algo", _i, _p, _i, _p)
 _sig("sblas_ctx_matrix_upload_parts", _i, _p, _i, _i, _p, _p, _p, _i, _i)
 _sig("sblas_ctx_parts", _i, _p, _p)
+_sig("sblas_csr_panels", _i, _p, _i, _p)
 _sig("sblas_ctx_spmv_ex", _i, _p, _d, _d, _d, _i, _p)
 _sig("sblas_ctx_sync", _i, _p, _p)
 _sig("sblas_ctx_get_y", _i, _p, _i, _p)
@@ -487,6 +488,12 @@ class DeviceCSR:
         a = C.c_int()
         check(lib.sblas_csr_pick(self.h, stream, C.byref(a)), "csr_pick")
         return a.value
+
+    def panels(self, algo: int) -> int:
+        """XCD column panels the analysed plan of `algo` runs over (0 = plain)."""
+        p = C.c_int()
+        check(lib.sblas_csr_panels(self.h, algo, C.byref(p)), "csr_panels")
+        return p.value
 
     def plan_bytes(self, algo: int) -> int:
         """Device bytes the algorithm's analysis holds beside the CSR."""

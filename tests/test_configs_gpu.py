@@ -73,11 +73,15 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
 
 
 @pytest.mark.parametrize("algo,env", [
-    (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
+    (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (2, {"SBLAS_CSR5_PANEL": "0"}),
+    (2, {"SBLAS_C5_PF": "0"}), (2, {"SBLAS_C5_PF": "1"}), (2, {"SBLAS_C5_PF": "3", "SBLAS_CSR5_PANEL": "0"}),
+    (1, {"SBLAS_RS_PANEL": "0"}), (1, {"SBLAS_RS_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
     (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_K24": "0"}),
     (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2"}), (5, {"SBLAS_XS_TAIL": "1"}),
     (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (1, {"SBLAS_RS_SEQ": "0"})],
-    ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "panel", "xsort", "xsort_static", "xsort_q3", "xsort_fused",
+    ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "csr5_plain", "csr5_form0", "csr5_form1",
+         "csr5_form3_plain", "rowsplit_plain", "rowsplit_panels", "panel", "xsort", "xsort_static", "xsort_q3",
+         "xsort_fused",
          "xsort_k32", "xsort_k24_u2", "xsort_tail", "xsort_tail_allwide", "xsort_solo", "rowsplit_vec4"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
@@ -86,6 +90,22 @@ def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     launches = 25 if (algo == 5 and (not env or env in ({"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}))
                       and not cfg2["prefix"]) else 1
     _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
+
+
+def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
+    """Row split and CSR5 run over 4 XCD column panels on config 2's random
+    columns (x = 16 MB > 8 MiB, 39.75M nnz, rows spanning most of x) and keep
+    the plain layout on the reference generator's prefix columns; PANEL
+    always uses panels (sblas_csr_panels, spmv.hip xcd_panels_pay)."""
+    A = sb.DeviceCSR.upload(0, N2, cfg2["rp"], cfg2["col"], cfg2["val"])
+    try:
+        for algo in (sb.ROWSPLIT, sb.CSR5, sb.PANEL):
+            A.analyse(algo)
+        want = 0 if cfg2["prefix"] else 4
+        assert A.panels(sb.ROWSPLIT) == want and A.panels(sb.CSR5) == want
+        assert A.panels(sb.PANEL) == 4 or cfg2["prefix"]
+    finally:
+        A.close()
 
 
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
