@@ -415,6 +415,7 @@ def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx,
             check = _oracle_check(rowptr, col_all, val_all, x_h, np.zeros(plan.m), [y.cpu().numpy()]) and same
         elif not same:
             check = False
+    panels = op.A.panels(sblas.CSR5)
     op.close()
     return config3_object(
         world, max(p[0] for p in per), max(p[1] for p in per), max(p[2] for p in per), W.nnz,
@@ -423,6 +424,7 @@ def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx,
          "cold steps: HIP events on the launch stream around kernel and exchange after a device-side "
          "hold, max over ranks"),
         traffic=pmc_traffic("csr5") if (world == 1 and W.default) else None,
+        xcd_panels_rank0=panels,
         nnz_per_device=[int(plan.end_idx[d] - plan.start_idx[d] + 1) for d in range(world)])
 
 
@@ -885,7 +887,9 @@ def main() -> int:
         rowsplit_beside = {"kernel_ms": round(rk, 5),
                            "gflops": round(2.0 * nnz / (rk * 1e-3) / 1e9, 3),
                            "roofline_frac": round(local_bytes / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                           "cache": "cold"}
+                           "cache": "cold",
+                           # the row blocks' layout: 0 = plain, P = per XCD column panel
+                           "xcd_panels": op.A.panels(sblas.ROWSPLIT)}
     config3 = None
     if not args.no_config3:
         config3 = torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream,
