@@ -64,6 +64,9 @@ struct sblas_ctx_s {
     std::vector<hipEvent_t> evc;       // [g] comm stream done (joins the main stream)
     std::vector<int> palgo;            // [g] the algorithm the part handles run (AUTO resolved)
     int parts_req = 1;                 // requested by sblas_ctx_matrix_upload_parts
+    // one device, one part: nothing to exchange; yfull[0] IS ylocal[0] (its
+    // first m rows are y in row order under either partition)
+    bool yalias = false;
 };
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
@@ -297,7 +300,7 @@ void free_matrix(sblas_ctx_s &C)
         (void)hipFree(C.x[d]);
         (void)hipFree(C.ylocal[d]);
         (void)hipFree(C.gathered[d]);
-        (void)hipFree(C.yfull[d]);
+        if (!C.yalias) (void)hipFree(C.yfull[d]);
         (void)hipFree(C.meta[d]);
         (void)hipFree(C.bar[d]);
         if (d < (int)C.yptr.size()) (void)hipFree(C.yptr[d]);
@@ -308,6 +311,7 @@ void free_matrix(sblas_ctx_s &C)
     C.ylocal.clear();
     C.gathered.clear();
     C.yfull.clear();
+    C.yalias = false;
     C.meta.clear();
     C.bar.clear();
     C.h_meta.clear();
@@ -586,6 +590,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             SBLAS_TRY(ensure_overlap_streams(*C));
         }
     }
+    C->yalias = g == 1 && C->parts <= 1;
     int st = SBLAS_OK;
     for (int d = 0; d < g && st == SBLAS_OK; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -615,9 +620,12 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
         if (st != SBLAS_OK) break;
         hipError_t e = hipMalloc(&C->x[d], sizeof(double) * std::max(n, 1));
         if (e == hipSuccess) e = hipMalloc(&C->ylocal[d], sizeof(double) * C->ylen);
-        if (e == hipSuccess && exchange == SBLAS_CTX_ALLGATHER)
+        if (e == hipSuccess && exchange == SBLAS_CTX_ALLGATHER && !C->yalias)
             e = hipMalloc(&C->gathered[d], sizeof(double) * C->stride * g);
-        if (e == hipSuccess) e = hipMalloc(&C->yfull[d], sizeof(double) * std::max(m, 1));
+        if (e == hipSuccess && C->yalias)
+            C->yfull[d] = C->ylocal[d];
+        else if (e == hipSuccess)
+            e = hipMalloc(&C->yfull[d], sizeof(double) * std::max(m, 1));
         if (e == hipSuccess) e = hipMalloc(&C->bar[d], sizeof(double));
         if (e == hipSuccess) e = hipMemsetAsync(C->bar[d], 0, sizeof(double), C->st[d]);
         if (e == hipSuccess) e = hipMemsetAsync(C->ylocal[d], 0, sizeof(double) * C->ylen, C->st[d]);
@@ -836,10 +844,12 @@ int sblas_ctx_spmv_ex(sblas_ctx C, double alpha, double beta, double delay_us, i
                                  C->st[d]));
         SBLAS_HIP(hipEventRecord(C->ev[(size_t)3 * d + 1], C->st[d]));
     }
-    SBLAS_TRY(xchg_spmv(*C));
+    if (!C->yalias) SBLAS_TRY(xchg_spmv(*C));
     for (int d = 0; d < g; ++d) {
         DeviceGuard gd(C->dev[d]);
-        if (C->exchange == SBLAS_CTX_ALLREDUCE) {
+        if (C->yalias) {
+            // single device: the kernel wrote y in place
+        } else if (C->exchange == SBLAS_CTX_ALLREDUCE) {
             const long long nr = C->lrows[d];
             if (nr > 0) {
                 hipLaunchKernelGGL(k_ctx_reprime, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, C->st[d],
