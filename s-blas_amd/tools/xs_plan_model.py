@@ -41,7 +41,7 @@ def config2_rowptr(n, heavy=96, light=9, world=1):
     return rp
 
 
-def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid"):
+def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid", lsplit=None):
     """pairing: leftover light sub-items two to an item only as far as the
     grid needs ("grid", the planner since round 3) or always ("always")."""
     m, nnz = len(rp) - 1, int(rp[-1])
@@ -101,6 +101,22 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
         return L * (1 - math.exp(-c / L)) + c * 12 / 128
 
     nsub = [req(c, False) for _, w, c in ranges if not w]
+    if lsplit:
+        # the light rows re-cut into ranges of R rows, each
+        # split S ways by column group (S sub-items over G / S groups, partials
+        # added by the reduce).  A sub-item's block density (entries per x
+        # line) is R * nnz_row * 16 / n whatever S is: only R (the LDS rows of
+        # one team) sets it; S only makes the work units smaller.
+        S, R = lsplit
+        light = [(r, c) for r, w, c in ranges if not w]
+        lrows = sum(r for r, _ in light)
+        lnnz = sum(c for _, c in light)
+        nr = max(1, math.ceil(lrows / R))
+        c = lnnz / nr / S
+        L = G * Lg / S
+        # + the sub-item's partial stores (8 B per row, 128-B lines)
+        one = L * (1 - math.exp(-c / L)) + c * 12 / 128 + (lrows / nr) * 8 / 128
+        nsub = [one] * (nr * S)
     wsub = [[req(c, True) for _, w, c in ranges if w] for _ in range(8)]
     # items in queue order (xsort.hip: pairing per XCD, queues interleaved)
     queues = [[] for _ in range(8)]
@@ -160,9 +176,11 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
             heapq.heappush(heap, heapq.heappop(heap) + v)
         busiest = max(busiest, max(heap))
     total_req = sum(nsub) + sum(map(sum, wsub))
-    return {"mode": mode, "rows_cap": cap_rows, "narrow": len(nsub), "wide_ranges": sum(1 for _, w, _ in ranges if w),
+    return {"mode": mode + (f" lsplit S={lsplit[0]} R={lsplit[1]}" if lsplit else ""), "rows_cap": cap_rows, "narrow": len(nsub), "wide_ranges": sum(1 for _, w, _ in ranges if w),
             "items": sum(map(len, queues)), "requests_M": round(total_req / 1e6, 2),
             "busiest_cu_k": round(busiest / 1e3, 1),
+            # perfect balance: the chip's requests spread evenly over the CUs
+            "balanced_k": round(total_req / CUS / 1e3, 1),
             "model_us": round(busiest * CYCLES_PER_REQUEST / CLOCK * 1e6, 1)}
 
 
@@ -171,6 +189,7 @@ def main():
     ap.add_argument("--n", type=int, default=2_000_000)
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rmat", type=int, default=0, help="model an R-MAT graph of this scale instead")
+    ap.add_argument("--lsplit", action="store_true", help="also model light ranges split S ways by columns")
     args = ap.parse_args()
     rp = config2_rowptr(args.n, world=args.world)
     if args.rmat:
@@ -183,6 +202,17 @@ def main():
         return
     for mode, rc in (("paired", None), ("solo", None), ("unpaired", None)):
         print(plan(rp, args.n, mode, rows_cap=rc))
+    if args.lsplit:
+        # light ranges split S ways by columns at R rows per range (R <= 8192:
+        # a team's LDS rows), partial bytes 8 * S per light row written + read
+        base = plan(rp, args.n, "paired")
+        for S in (1, 2, 4):
+            for R in (4096, 6912, 8192):
+                r = plan(rp, args.n, "paired", lsplit=(S, R))
+                lrows = int(np.sum(np.diff(rp) < 96)) if args.world == 1 else None
+                extra = None if lrows is None or S == 1 else round(2 * 8 * S * lrows / 1e6, 1)
+                print(r, "partial MB (write + read):", extra,
+                      "vs default busiest", base["busiest_cu_k"])
 
 
 if __name__ == "__main__":
