@@ -368,7 +368,8 @@ int sblas_ctx_set_y(sblas_ctx ctx, const double *y); /* host y (beta input) */
 /* y = alpha*A*x + beta*y on every device; afterwards each device holds the
  * full y, which is also the next call's y input.  stats (optional, 3
  * doubles, ms, max over devices): kernel, exchange (collective + placement),
- * whole step. */
+ * whole step.  A one-device context (not overlapped) has nothing to
+ * exchange: its kernel writes the full y in place (exchange ~0). */
 int sblas_ctx_spmv(sblas_ctx ctx, double alpha, double beta, double *stats);
 /* sblas_ctx_spmv for timing.  delay_us > 0: every device's stream first
  * waits delay_us on the device (the host enqueues the whole step meanwhile)
