@@ -242,17 +242,19 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
 // panels (~4 MiB of x each, P = 4 partials added after): x outgrows an XCD's
 // L2, the rows' columns are scattered (the column probe: most sampled rows
 // span > n/4 of the columns, spread over the eighths) and the matrix is large
-// enough to amortise the partial-y pass.  Measured on config 2: CSR5 285 ->
-// 249 us, row split 307 -> ~240 us; its N = 4 slice (9.9M nnz) even, N = 8
-// (5M) slower (profiles/r04/csr5_auto/).  `env` = 1 / 0 forces either form.
-static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, bool *use)
+// enough to amortise the partial-y pass (`min_nnz`).  Measured on config 2
+// and its rank-0 slices (cold spans, profiles/r04/slicepanels/): CSR5 286 ->
+// 238 us, N = 4 slice (9.9M nnz) 81 -> 74 us, N = 8 (5M) 47 -> 49 us (so
+// CSR5 from 8M entries); row split 307 -> 244 us, N = 4 84 -> 71 us, N = 8
+// 46 -> 43 us (from 4M entries).  `env` = 1 / 0 forces either form.
+static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, long long min_nnz, bool *use)
 {
     *use = false;
     if (const char *e = getenv(env)) {
         *use = atoi(e) == 1;
         return SBLAS_OK;
     }
-    if ((long long)A.n * 8 <= (8LL << 20) || A.nnz < 12000000LL) return SBLAS_OK;
+    if ((long long)A.n * 8 <= (8LL << 20) || A.nnz < min_nnz) return SBLAS_OK;
     SBLAS_TRY(probe_columns(A, s));
     *use = A.col_scattered >= 0.5 && A.col_maxshare <= 0.25;
     return SBLAS_OK;
@@ -287,7 +289,7 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
     // (the panel plan, algo 4's layout); SBLAS_RS_PANEL=1 / 0 forces
     if (!A.pn.degenerate) {
         bool use = false;
-        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", &use));
+        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", 4000000LL, &use));
         if (use) {
             SBLAS_TRY(build_panel_plan(A, s));
             A.rs.panels = !A.pn.degenerate;
@@ -1089,7 +1091,7 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     // SBLAS_CSR5_PANEL=1 / 0 forces either form.
     (void)pe;
     bool panels = false;
-    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", &panels));
+    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", 8000000LL, &panels));
     if (panels && !(hp && atoi(hp) == 1)) {
         const int rc = build_csr5_panels(A, s);
         if (rc == SBLAS_OK) return SBLAS_OK;

@@ -41,7 +41,7 @@ def config2_rowptr(n, heavy=96, light=9, world=1):
     return rp
 
 
-def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid", lsplit=None):
+def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid", lsplit=None, k=1, allwide=False):
     """pairing: leftover light sub-items two to an item only as far as the
     grid needs ("grid", the planner since round 3) or always ("always")."""
     m, nnz = len(rp) - 1, int(rp[-1])
@@ -55,7 +55,7 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
     cap_rows = rows_cap or (8192 if pair else 16384)
     ncap_rows = 16384 if solo else cap_rows
     nfac = 2.0 if solo else 1.0
-    slots = CUS * (2 if pair else 1)
+    slots = CUS * (2 if pair else 1) * k  # k: items per CU (SBLAS_XS_K)
 
     def nc(c):
         return c + lam * G * Lg * (1 - math.exp(-c / (G * Lg)))
@@ -80,7 +80,7 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
         out, r = [], 0
         while r < m:
             e, cnt = cut(r, True, cap)
-            wide = cnt > 0 and nc(cnt) > nfac * cap and cnt >= 16 * (e - r)
+            wide = cnt > 0 and (allwide or (nc(cnt) > nfac * cap and cnt >= 16 * (e - r)))
             if not wide:
                 e, cnt = cut(r, False, cap)
             out.append((e - r, wide, cnt))
@@ -156,7 +156,7 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
                 queues[k].append(left[k][j] + (left[k][j + 1] if j + 1 < len(left[k]) else 0))
         t = 0
         left = len(nsub) - ni
-        free = max(0, CUS - sum(map(len, queues)))
+        free = max(0, CUS * k - sum(map(len, queues)))
         npairs = max(0, left - free) if pairing == "grid" else left // 2
         npairs = min(npairs, left // 2)
         while ni < len(nsub):
@@ -169,6 +169,11 @@ def plan(rp, n, mode="paired", lam=1.0, rows_cap=None, wstar=None, pairing="grid
                 ni += 1
             t += 1
     # 32 CUs per XCD claim from their own queue first (greedy list schedule)
+    if os.environ.get("XS_MODEL_DEBUG"):
+        print("queue totals (k req):", [round(sum(qq) / 1e3) for qq in queues],
+              "items:", [len(qq) for qq in queues], "largest items (k):",
+              sorted((round(v / 1e3, 1) for qq in queues for v in qq), reverse=True)[:6],
+              "wide sub-items per XCD:", [len(w) for w in wsub], "narrow:", len(nsub))
     busiest = 0.0
     for k in range(8):
         heap = [0.0] * (CUS // 8)

@@ -108,6 +108,35 @@ def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
         A.close()
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_config2_slice_xcd_panel_choice(torch_cuda, sb, orc, cfg2, world):
+    """Rank 0's cyclic slice at N = 4 (9.9M nnz) and N = 8 (5M): the row split
+    takes panels from 4M entries, CSR5 from 8M (profiles/r04/slicepanels/);
+    both stay within the bound against the oracle on the slice."""
+    import sblas_dist
+    rp = cfg2["rp"]
+    plan = sblas_dist.make_cyclic_plan(rp, N2, world)
+    lrp, col, val = sblas_dist.cyclic_local_csr(rp, plan, 0, lambda a, b: (cfg2["col"][rp[a]:rp[b]],
+                                                                         cfg2["val"][rp[a]:rp[b]]))
+    m = len(lrp) - 1
+    x = cfg2["xd"]
+    y0 = sb.gen_vector(m, 45)
+    want = orc.csr_spmv(lrp, col, val, x.cpu().numpy(), cfg2["alpha"], cfg2["beta"], y0.copy())
+    bound = orc.spmv_bound(lrp, col, val, x.cpu().numpy(), cfg2["alpha"], cfg2["beta"], y0)
+    A = sb.DeviceCSR.upload(0, N2, lrp, col, val)
+    try:
+        for algo, thr in ((sb.ROWSPLIT, 4_000_000), (sb.CSR5, 8_000_000)):
+            A.analyse(algo)
+            want_p = 0 if cfg2["prefix"] or int(lrp[-1]) < thr else 4
+            assert A.panels(algo) == want_p, (world, algo)
+            y = torch_cuda.from_numpy(y0.copy()).cuda()
+            A.spmv(algo, cfg2["alpha"], x.data_ptr(), cfg2["beta"], y.data_ptr(), 0)
+            torch_cuda.cuda.synchronize()
+            _check_spmv(want, bound, y.cpu().numpy(), f"slice N={world} algo {algo}")
+    finally:
+        A.close()
+
+
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
 @pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}],
                          ids=["default", "batch", "tail", "solo"])

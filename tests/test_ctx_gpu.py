@@ -98,6 +98,7 @@ def test_ctx_timed_steps_and_slice_info(torch_cuda, sb, orc):
     st = ctx.spmv_ex(alpha, beta, delay_us=200.0)
     assert st.shape == (6,) and st[0] > 0 and st[2] >= st[0] and st[2] < 50.0
     assert st[3] == st[0] and st[5] == st[2]
+    assert st[1] < 0.02  # one device: the kernel writes y in place, nothing to exchange
     y = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
     for _ in range(3):
         assert ctx.spmv_ex(alpha, beta, wait=False) is None
