@@ -32,6 +32,10 @@ def main():
                     help="also time the slice cut into K parts of consecutive local chunks (the "
                          "overlapped exchange's kernels, sblas_ctx_matrix_upload_parts): the K "
                          "launches back to back after a cold sweep, events between them")
+    ap.add_argument("--partition", choices=["cyclic", "nnz"], default="cyclic",
+                    help="cyclic (bench.py's default leg) or nnz (configs[2]'s spMV_mgpu_v1 split, the "
+                         "config3 leg: ranks hold different row classes, so --ranks all)")
+    ap.add_argument("--ranks", default="0", help="ranks whose slices to time: a list or 'all'")
     ap.add_argument("--floor", action="store_true",
                     help="also time a cold streaming read of the slice's byte count")
     args = ap.parse_args()
@@ -48,10 +52,19 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     algos = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
              "xsort": sblas.XSORT}
+    rows_fn = lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, 96, 9, seed=42)
     for world in [int(w) for w in args.worlds.split(",")]:
-        plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
-        lrp, col, val = sblas_dist.cyclic_local_csr(
-            rowptr, plan, 0, lambda a, b: sblas.gen_synth_rows(n, rowptr, a, b, 96, 9, seed=42))
+      ranks = range(world) if args.ranks == "all" else [int(r) for r in args.ranks.split(",") if int(r) < world]
+      for rank in ranks:
+        plan = None
+        if args.partition == "cyclic":
+            plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
+            lrp, col, val = sblas_dist.cyclic_local_csr(rowptr, plan, rank, rows_fn)
+        else:  # whole rows of the nnz split (its split rows' shares rounded to whole rows)
+            _, _, sr, er, _ = sblas.partition_nnz(rowptr, world)
+            a, b = int(sr[rank]), int(er[rank]) + 1
+            lrp = np.asarray(rowptr[a:b + 1], np.int64) - int(rowptr[a])
+            col, val = rows_fn(a, b)
         for name in args.algos.split(","):
             A = sblas.DeviceCSR.upload(0, n, lrp, col, val)
             A.analyse(algos[name])
@@ -86,11 +99,12 @@ def main():
                                               stream.cuda_stream))
                 out["cold_span_us"] = round(float(np.median(spans[2:])) * 1e3, 1)
                 out["cold_span_min_us"] = round(float(np.min(spans[2:])) * 1e3, 1)
-            if args.parts > 1:
+            if args.parts > 1 and plan is not None:
                 out.update(time_parts(args, plan, lrp, col, val, n, algos[name], A.pick() if algos[name] == 0
                                       else algos[name], x, scrub, stream, torch, sblas))
             A.close()
-            print(json.dumps({"world": world, "algo": name, "local_rows": int(len(lrp) - 1),
+            print(json.dumps({"world": world, "rank": rank, "partition": args.partition,
+                              "algo": name, "local_rows": int(len(lrp) - 1),
                               "local_nnz": int(lrp[-1]), **out}), flush=True)
         if args.floor:
             # streaming floor for the slice's bytes: a cold torch sum over a
