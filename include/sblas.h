@@ -170,7 +170,8 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
 /* XCD column panels the analysed plan of `algo` runs over (0: the plain
  * layout / not analysed).  ROWSPLIT and CSR5 build per-panel plans on large
- * scattered-column matrices (x > 8 MiB, nnz >= 4M row split / 8M CSR5, most sampled rows span
+ * scattered-column matrices (x > 8 MiB, nnz >= 4M row split / 8M CSR5 -- 4M with 2 panels
+ * on rows of < 12 entries on average --, most sampled rows span
  * > n/4 of the columns; SBLAS_RS_PANEL / SBLAS_CSR5_PANEL = 0 / 1 force);
  * PANEL always does (unless only one panel holds entries). */
 int sblas_csr_panels(sblas_csr A, int algo, int *panels);

@@ -245,8 +245,9 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
 // enough to amortise the partial-y pass (`min_nnz`).  Measured on config 2
 // and its rank-0 slices (cold spans, profiles/r04/slicepanels/): CSR5 286 ->
 // 238 us, N = 4 slice (9.9M nnz) 81 -> 74 us, N = 8 (5M) 47 -> 49 us (so
-// CSR5 from 8M entries); row split 307 -> 244 us, N = 4 84 -> 71 us, N = 8
-// 46 -> 43 us (from 4M entries).  `env` = 1 / 0 forces either form.
+// CSR5 from 8M entries, from 4M on short rows: build_csr5_plan); row split
+// 307 -> 244 us, N = 4 84 -> 71 us, N = 8 46 -> 43 us (from 4M entries).
+// `env` = 1 / 0 forces either form.
 static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, long long min_nnz, bool *use)
 {
     *use = false;
@@ -1035,41 +1036,64 @@ static void free_csr5_arrays(Csr5Plan &P)
     (void)hipFree(P.ypart);
 }
 
-// CSR5 over the panel plan's column panels (XCD-affine x gathers): one tile
-// plan per non-empty panel.  Opt-in (SBLAS_CSR5_PANEL=1; SBLAS_PANELS sets
-// the panel count).  Measured on config 2 (profiles/r03/csr5_panel/): P = 2 /
-// 4 / 8 run 309 / 349 / 427 us against 329 us for the plain form, and the
-// N = 8 slice 49.6 against 50.1 us: a panel row holds ~2.25 entries, so each
-// tile ends ~7 rows per lane (scattered 8-B partial-y writes) and nearly
-// every tile holds empty rows (the seg_row path), which eats what the
-// XCD-local gathers save.
-static int build_csr5_panels(sblas_csr_s &A, hipStream_t s)
+// A's columns cut into P panels of W columns: a panel-local CSR each
+// (rowptr [P][m+1]; col / val panel-major from base[p], each panel 16-B
+// aligned).  The caller owns (and frees) rowptr / col / val.
+struct PanelCsr {
+    int P = 0;
+    long long W = 0;
+    int *rowptr = nullptr;
+    int *col = nullptr;
+    double *val = nullptr;
+    std::vector<int> hrp;         // host copy of rowptr
+    std::vector<long long> base;  // panel p's first element in col / val
+};
+
+static int split_panels(const sblas_csr_s &A, int P, hipStream_t s, PanelCsr &o);
+static void free_panel_csr(PanelCsr &o);
+static int default_panels(const sblas_csr_s &A);
+
+// CSR5 over XCD column panels (XCD-affine x gathers): the columns cut into P
+// panels of their own (split_panels; not the row-split panel plan, whose
+// panel count is the row split's), one tile plan per non-empty panel, the
+// panel CSR freed once the tiles are built.  Each panel's empty rows get no
+// segment, so their partials are zeroed once here and never written.
+static int build_csr5_panels(sblas_csr_s &A, int Preq, hipStream_t s)
 {
     Csr5Plan &P = A.c5;
-    SBLAS_TRY(build_panel_plan(A, s));
-    const PanelPlan &Q = A.pn;
-    if (Q.degenerate || Q.P < 2) return SBLAS_ERR_UNSUPPORTED;
-    std::vector<PanelDesc> pd((size_t)Q.P);
-    SBLAS_HIP(hipMemcpy(pd.data(), Q.desc, sizeof(PanelDesc) * Q.P, hipMemcpyDeviceToHost));
     const long long m = A.m;
-    P.panels.assign((size_t)Q.P, Csr5Plan{});
-    std::vector<Csr5Desc> hd((size_t)Q.P);
-    SBLAS_HIP(hipMalloc(&P.ypart, sizeof(double) * std::max<long long>(Q.P * m, 1)));
-    // a panel's empty rows get no segment, so their partials are never
-    // written: zero them here once instead of on every call
-    SBLAS_HIP(hipMemsetAsync(P.ypart, 0, sizeof(double) * std::max<long long>(Q.P * m, 1), s));
-    for (int q = 0; q < Q.P; ++q) {
-        int nz = 0;
-        SBLAS_HIP(hipMemcpy(&nz, pd[(size_t)q].rowptr + m, sizeof(int), hipMemcpyDeviceToHost));
+    PanelCsr pc;
+    int st = split_panels(A, Preq, s, pc);
+    std::vector<int> live;
+    for (int p = 0; st == SBLAS_OK && p < pc.P; ++p)
+        if (pc.hrp[(size_t)p * (m + 1) + m] > 0) live.push_back(p);
+    if (st == SBLAS_OK && live.size() < 2) st = SBLAS_ERR_UNSUPPORTED;
+    const int PL = (int)live.size();
+    if (st == SBLAS_OK) {
+        P.panels.assign((size_t)PL, Csr5Plan{});
+        if (hipMalloc(&P.ypart, sizeof(double) * std::max<long long>(PL * m, 1)) != hipSuccess ||
+            hipMemsetAsync(P.ypart, 0, sizeof(double) * std::max<long long>(PL * m, 1), s) != hipSuccess) {
+            set_error("csr5 panels: %s", hipGetErrorString(hipGetLastError()));
+            st = SBLAS_ERR_HIP;
+        }
+    }
+    std::vector<Csr5Desc> hd((size_t)std::max(PL, 0));
+    for (int q = 0; st == SBLAS_OK && q < PL; ++q) {
+        const int p = live[q];
+        const int nz = pc.hrp[(size_t)p * (m + 1) + m];
         Csr5Plan &S = P.panels[(size_t)q];
-        SBLAS_TRY(build_csr5_core(S, pd[(size_t)q].rowptr, pd[(size_t)q].col, pd[(size_t)q].val, (int)m, nz, s));
+        st = build_csr5_core(S, pc.rowptr + (size_t)p * (m + 1), pc.col + pc.base[p], pc.val + pc.base[p], (int)m, nz,
+                             s);
         hd[(size_t)q] = Csr5Desc{S.tile_row, S.flags,    S.tval, S.tcol, S.seg_off, S.seg_row, S.empty_rows,
                                  P.ypart + (size_t)q * m, S.carry, S.ntiles, (long long)nz, 0, 0, S.head_run};
         P.maxtiles = std::max(P.maxtiles, S.ntiles);
     }
-    SBLAS_HIP(hipMalloc(&P.desc, sizeof(Csr5Desc) * Q.P));
-    SBLAS_HIP(hipMemcpy(P.desc, hd.data(), sizeof(Csr5Desc) * Q.P, hipMemcpyHostToDevice));
-    P.P = Q.P;
+    if (st == SBLAS_OK && hipStreamSynchronize(s) != hipSuccess) st = SBLAS_ERR_HIP;
+    free_panel_csr(pc);
+    if (st != SBLAS_OK) return st;
+    SBLAS_HIP(hipMalloc(&P.desc, sizeof(Csr5Desc) * PL));
+    SBLAS_HIP(hipMemcpy(P.desc, hd.data(), sizeof(Csr5Desc) * PL, hipMemcpyHostToDevice));
+    P.P = PL;
     P.ready = true;
     return SBLAS_OK;
 }
@@ -1081,19 +1105,27 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     Csr5Plan &P = A.c5;
     const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
     const char *pe = getenv("SBLAS_CSR5_PANEL");
-    // Tiles per XCD column panel (each XCD's gathers in ~4 MiB of x) when x
+    // Tiles per XCD column panel (each XCD's gathers in a slice of x) when x
     // outgrows an XCD's L2, the rows' columns are scattered (the probe: most
     // sampled rows span > n/4 of the columns, spread over the eighths) and
-    // the matrix is large enough to amortise the panels' partial-y pass:
-    // config 2 285 -> 251 us, its N = 2 slice 150 -> 137 us; N = 4 (9.9M nnz)
-    // even, N = 8 (5M) slower (profiles/r04/csr5_auto/).  Banded / stencil /
+    // the matrix is large enough to amortise the panels' partial-y pass.
+    // Short rows (< 12 entries on average) take 2 panels from 4M entries:
+    // a 9-entry row cut 4 ways ends ~4 rows per lane and tile; others 4
+    // panels from 8M.  Measured per slice of configs[2]'s nnz split (cold
+    // spans, profiles/r04/c5P/; plain / 2 / 4 panels): full 286 / 251 / 241,
+    // N = 2 heavy 110 / 112 / 95 and light 192 / 161 / 165, N = 4 light
+    // 114 / 95 / 100, N = 8 heavy (5M) 36 / 42 / 38 and light (5M) 62 / 55
+    // / 60 us; R-MAT (15.5 per row) 315 / 248 / 234.  Banded / stencil /
     // prefix-column matrices keep the plain tiles, whose gathers share lines.
-    // SBLAS_CSR5_PANEL=1 / 0 forces either form.
+    // SBLAS_CSR5_PANEL=1 / 0 forces either form, SBLAS_PANELS the count.
     (void)pe;
+    const bool short_rows = A.m > 0 && A.nnz < 12LL * A.m;
+    int npanels = short_rows ? std::min(2, default_panels(A)) : default_panels(A);
+    if (getenv("SBLAS_PANELS")) npanels = default_panels(A);
     bool panels = false;
-    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", 8000000LL, &panels));
-    if (panels && !(hp && atoi(hp) == 1)) {
-        const int rc = build_csr5_panels(A, s);
+    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", short_rows ? 4000000LL : 8000000LL, &panels));
+    if (panels && npanels >= 2 && !(hp && atoi(hp) == 1)) {
+        const int rc = build_csr5_panels(A, npanels, s);
         if (rc == SBLAS_OK) return SBLAS_OK;
         free_csr5_arrays(P);
         A.c5 = Csr5Plan{};
@@ -1313,54 +1345,90 @@ __global__ void k_panel_scatter(const int *__restrict__ rowptr, const int *__res
     }
 }
 
+static int split_panels(const sblas_csr_s &A, int P, hipStream_t s, PanelCsr &o)
+{
+    o.P = P;
+    o.W = ((long long)A.n + P - 1) / P;
+    const long long m = A.m;
+    SBLAS_HIP(hipMalloc(&o.rowptr, sizeof(int) * P * (m + 1)));
+    SBLAS_HIP(hipMemsetAsync(o.rowptr, 0, sizeof(int) * P * (m + 1), s));
+    const long long cap = ((A.nnz + 3) & ~3LL) + 4 * P + 4;
+    SBLAS_HIP(hipMalloc(&o.col, sizeof(int) * cap));
+    SBLAS_HIP(hipMalloc(&o.val, sizeof(double) * cap));
+    SBLAS_HIP(hipMemsetAsync(o.col, 0, sizeof(int) * cap, s));
+    SBLAS_HIP(hipMemsetAsync(o.val, 0, sizeof(double) * cap, s));
+    if (m > 0) {
+        hipLaunchKernelGGL(k_panel_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                           A.rowptr, A.col, (int)m, o.W, P, o.rowptr);
+        int *scratch = nullptr;
+        SBLAS_HIP(hipMalloc(&scratch, sizeof(int) * ((m + 1) / 1024 + 256)));
+        for (int p = 0; p < P; ++p) SBLAS_TRY(scan_inclusive(o.rowptr + p * (m + 1), m + 1, scratch, s));
+        SBLAS_HIP(hipStreamSynchronize(s));
+        (void)hipFree(scratch);
+    }
+    o.hrp.assign((size_t)P * (m + 1), 0);
+    SBLAS_HIP(hipMemcpy(o.hrp.data(), o.rowptr, sizeof(int) * o.hrp.size(), hipMemcpyDeviceToHost));
+    o.base.assign(P, 0);
+    long long acc = 0;
+    for (int p = 0; p < P; ++p) {
+        o.base[p] = acc;
+        acc += o.hrp[(size_t)p * (m + 1) + m];
+        acc = (acc + 3) & ~3LL;
+    }
+    long long *dbase = nullptr;
+    SBLAS_HIP(hipMalloc(&dbase, sizeof(long long) * P));
+    SBLAS_HIP(hipMemcpy(dbase, o.base.data(), sizeof(long long) * P, hipMemcpyHostToDevice));
+    if (m > 0)
+        hipLaunchKernelGGL(k_panel_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                           A.rowptr, A.col, A.val, (int)m, o.W, P, o.rowptr, dbase, o.col, o.val);
+    SBLAS_HIP(hipStreamSynchronize(s));
+    (void)hipFree(dbase);
+    return SBLAS_OK;
+}
+
+static void free_panel_csr(PanelCsr &o)
+{
+    (void)hipFree(o.rowptr);
+    (void)hipFree(o.col);
+    (void)hipFree(o.val);
+    o.rowptr = nullptr;
+    o.col = nullptr;
+    o.val = nullptr;
+}
+
+// ~4 MiB of x per panel (one XCD's L2), at most one panel per XCD (config 2:
+// P = 4 beats 8, fewer partial-y bytes); SBLAS_PANELS overrides
+static int default_panels(const sblas_csr_s &A)
+{
+    int P = (int)std::min<long long>(8, std::max<long long>(1, ((long long)A.n * 8 + (4 << 20) - 1) >> 22));
+    if (const char *e = getenv("SBLAS_PANELS")) P = std::max(1, std::min(64, atoi(e)));
+    if (A.n < P) P = std::max(1, A.n);
+    return P;
+}
+
 int build_panel_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.pn.ready) return SBLAS_OK;
     DeviceGuard g(A.device);
     PanelPlan &Q = A.pn;
-    // ~4 MiB of x per panel (one XCD's L2), at most one panel per XCD; measured
-    // on config 2: P = 4 beats 8 (fewer partial-y bytes), DESIGN.md.
-    int P = (int)std::min<long long>(8, std::max<long long>(1, ((long long)A.n * 8 + (4 << 20) - 1) >> 22));
-    if (const char *e = getenv("SBLAS_PANELS")) P = std::max(1, std::min(64, atoi(e)));
-    if (A.n < P) P = std::max(1, A.n);
-    Q.P = P;
-    Q.W = ((long long)A.n + P - 1) / P;
+    const int P = default_panels(A);
     const long long m = A.m;
-    SBLAS_HIP(hipMalloc(&Q.rowptr, sizeof(int) * P * (m + 1)));
-    SBLAS_HIP(hipMemsetAsync(Q.rowptr, 0, sizeof(int) * P * (m + 1), s));
-    const long long cap = ((A.nnz + 3) & ~3LL) + 4 * P + 4;
-    SBLAS_HIP(hipMalloc(&Q.col, sizeof(int) * cap));
-    SBLAS_HIP(hipMalloc(&Q.val, sizeof(double) * cap));
-    SBLAS_HIP(hipMemsetAsync(Q.col, 0, sizeof(int) * cap, s));
-    SBLAS_HIP(hipMemsetAsync(Q.val, 0, sizeof(double) * cap, s));
+    PanelCsr pc;
+    {
+        const int st = split_panels(A, P, s, pc);
+        if (st != SBLAS_OK) {
+            free_panel_csr(pc);
+            return st;
+        }
+    }
+    Q.P = P;
+    Q.W = pc.W;
+    Q.rowptr = pc.rowptr;
+    Q.col = pc.col;
+    Q.val = pc.val;
     SBLAS_HIP(hipMalloc(&Q.ypart, sizeof(double) * std::max<long long>(P * m, 1)));
-    if (m > 0) {
-        hipLaunchKernelGGL(k_panel_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
-                           A.rowptr, A.col, (int)m, Q.W, P, Q.rowptr);
-        int *scratch = nullptr;
-        SBLAS_HIP(hipMalloc(&scratch, sizeof(int) * ((m + 1) / 1024 + 256)));
-        for (int p = 0; p < P; ++p) SBLAS_TRY(scan_inclusive(Q.rowptr + p * (m + 1), m + 1, scratch, s));
-        SBLAS_HIP(hipStreamSynchronize(s));
-        (void)hipFree(scratch);
-    }
-    std::vector<int> hrp((size_t)P * (m + 1));
-    SBLAS_HIP(hipMemcpy(hrp.data(), Q.rowptr, sizeof(int) * hrp.size(), hipMemcpyDeviceToHost));
-    // panel bases, 4-element aligned so each panel starts 16-B aligned
-    std::vector<long long> base(P);
-    long long acc = 0;
-    for (int p = 0; p < P; ++p) {
-        base[p] = acc;
-        acc += hrp[(size_t)p * (m + 1) + m];
-        acc = (acc + 3) & ~3LL;
-    }
-    long long *dbase = nullptr;
-    SBLAS_HIP(hipMalloc(&dbase, sizeof(long long) * P));
-    SBLAS_HIP(hipMemcpy(dbase, base.data(), sizeof(long long) * P, hipMemcpyHostToDevice));
-    if (m > 0)
-        hipLaunchKernelGGL(k_panel_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
-                           A.rowptr, A.col, A.val, (int)m, Q.W, P, Q.rowptr, dbase, Q.col, Q.val);
-    SBLAS_HIP(hipStreamSynchronize(s));
-    (void)hipFree(dbase);
+    const std::vector<int> &hrp = pc.hrp;
+    const std::vector<long long> &base = pc.base;
     // Only non-empty panels take part.  One non-empty panel (all columns in
     // one x slice, e.g. the prefix layout) is plain row split: use it.
     std::vector<int> live;

@@ -137,6 +137,35 @@ def test_config2_slice_xcd_panel_choice(torch_cuda, sb, orc, cfg2, world):
         A.close()
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
+    """configs[2]'s nnz split puts the light rows on the last rank (9-entry
+    rows): CSR5 takes 2 XCD panels there from 4M entries (4 panels from 8M on
+    longer rows), within the bound against the oracle on that slice."""
+    rp = cfg2["rp"]
+    _, _, sr, er, _ = sb.partition_nnz(rp, world)
+    a, b = int(sr[world - 1]), int(er[world - 1]) + 1
+    lrp = np.asarray(rp[a:b + 1], np.int64) - int(rp[a])
+    col, val = cfg2["col"][rp[a]:rp[b]], cfg2["val"][rp[a]:rp[b]]
+    m = len(lrp) - 1
+    assert int(lrp[-1]) < 12 * m  # short rows
+    x = cfg2["xd"]
+    y0 = sb.gen_vector(m, 46)
+    xh = x.cpu().numpy()
+    want = orc.csr_spmv(lrp, col, val, xh, cfg2["alpha"], cfg2["beta"], y0.copy())
+    bound = orc.spmv_bound(lrp, col, val, xh, cfg2["alpha"], cfg2["beta"], y0)
+    A = sb.DeviceCSR.upload(0, N2, lrp, col, val)
+    try:
+        A.analyse(sb.CSR5)
+        assert A.panels(sb.CSR5) == (0 if cfg2["prefix"] else 2)
+        y = torch_cuda.from_numpy(y0.copy()).cuda()
+        A.spmv(sb.CSR5, cfg2["alpha"], x.data_ptr(), cfg2["beta"], y.data_ptr(), 0)
+        torch_cuda.cuda.synchronize()
+        _check_spmv(want, bound, y.cpu().numpy(), f"nnz split N={world} last rank, CSR5")
+    finally:
+        A.close()
+
+
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
 @pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}],
                          ids=["default", "batch", "tail", "solo"])
