@@ -432,7 +432,7 @@ __device__ __forceinline__ void csr5_tile(
                 seg = segbase;
             } else {
                 const int row = gap ? seg_row[soff + seg] : first_row + seg;
-                y[row] = kBeta ? alpha * sum + beta * y[row] : alpha * sum;
+                y[row] = kBeta ? __builtin_fma(beta, y[row], alpha * sum) : alpha * sum;
                 ++seg;
             }
             sum = 0.0;
@@ -463,7 +463,7 @@ __device__ __forceinline__ void csr5_tile(
     if (has) {
         const int row = gap ? seg_row[soff + seg] : first_row + seg;
         const double tot = sum + Snext;
-        y[row] = kBeta ? alpha * tot + beta * y[row] : alpha * tot;
+        y[row] = kBeta ? __builtin_fma(beta, y[row], alpha * tot) : alpha * tot;
     }
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
@@ -598,7 +598,7 @@ __device__ __forceinline__ void csr5_tile_pf(
             } else {
                 double yin;
                 const int row = next_row(seg, yin);
-                y[row] = kBeta ? alpha * sum + beta * yin : alpha * sum;
+                y[row] = kBeta ? __builtin_fma(beta, yin, alpha * sum) : alpha * sum;
                 ++seg;
             }
             sum = 0.0;
@@ -630,7 +630,7 @@ __device__ __forceinline__ void csr5_tile_pf(
         double yin;
         const int row = next_row(seg, yin);
         const double tot = sum + Snext;
-        y[row] = kBeta ? alpha * tot + beta * yin : alpha * tot;
+        y[row] = kBeta ? __builtin_fma(beta, yin, alpha * tot) : alpha * tot;
     }
     if (lane == 0) carry[t] = (f0 & 1u) ? 0.0 : S;
 }
@@ -643,7 +643,10 @@ __device__ __forceinline__ void csr5_tile_pf(
 // The plain form issues one scattered 8-B store (and load) per row end: a
 // 9-entry-row tile ends ~114 rows spread over 16 partially active store
 // instructions.  The first 128 rows' y0 are loaded before the x gathers.
-// Same products and sums as csr5_tile: bit-identical.
+// Same products and row sums as csr5_tile, and every form writes
+// y = fma(beta, y0, alpha * sum) explicitly (contraction left to the
+// compiler differed between forms): bit-identical
+// (tests/test_spmv_gpu.py::test_csr5_forms_bit_identical).
 template <bool kBeta, bool kNt>
 __device__ __forceinline__ void csr5_tile_st(
     long long t, const int *__restrict__ tile_row, const uint32_t *__restrict__ flags,
@@ -772,9 +775,9 @@ __device__ __forceinline__ void csr5_tile_st(
             b = kBeta ? y[row] : 0.0;
         }
         if (kNt)
-            __builtin_nontemporal_store(kBeta ? v + beta * b : v, y + row);
+            __builtin_nontemporal_store(kBeta ? __builtin_fma(beta, b, v) : v, y + row);
         else
-            y[row] = kBeta ? v + beta * b : v;
+            y[row] = kBeta ? __builtin_fma(beta, b, v) : v;
     }
 }
 

@@ -346,3 +346,31 @@ def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
         check(orc, rp, col, val, x, alpha, beta, y0, yd2.cpu().numpy())
     finally:
         A.close()
+
+
+@pytest.mark.parametrize("case", ["synth", "empty_rows", "long_rows"])
+def test_csr5_forms_bit_identical(torch_cuda, sb, orc, monkeypatch, case):
+    """The CSR5 tile forms (SBLAS_C5_PF: plain, phased loads, staged y with and
+    without non-temporal accesses) compute the same products and row sums in
+    the same order: their y are bit-identical (plain tiles, no panels)."""
+    rng = np.random.default_rng(77)
+    if case == "synth":
+        n = m = 30000
+        rp, col, val = orc.gen_synth(n)
+    else:
+        m, n = 40000, 50000
+        lens = rng.choice([0, 3, 9, 40] if case == "empty_rows" else [1, 9, 300, 3000], m,
+                          p=[0.3, 0.3, 0.3, 0.1] if case == "empty_rows" else [0.4, 0.5, 0.09, 0.01])
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+        val = rng.standard_normal(int(rp[-1]))
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    monkeypatch.setenv("SBLAS_CSR5_PANEL", "0")
+    outs = []
+    for form in ("0", "1", "2", "3"):
+        monkeypatch.setenv("SBLAS_C5_PF", form)
+        outs.append(run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 0.75, -1.25, y0))
+    for f, o in zip("123", outs[1:]):
+        assert np.array_equal(outs[0], o), f"form {f}: {np.sum(outs[0] != o)} rows differ"
+    check(orc, rp, col, val, x, 0.75, -1.25, y0, outs[0])
