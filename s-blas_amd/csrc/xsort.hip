@@ -1043,7 +1043,18 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // range is an item of its own -- both teams' waves and all 16,384 LDS
     // rows -- so its blocks are twice as dense (fewer x line requests per
     // entry); wide ranges still pair (wide, wide) at 8,192 rows a team
-    P.solo = P.pair && P.dyn && getenv("SBLAS_XS_SOLO") && atoi(getenv("SBLAS_XS_SOLO")) != 0;
+    // Chosen by default when >= 40% of the rows are empty (power-law graphs:
+    // an empty row spends an accumulator row, so 16,384 rows per light range
+    // hold what 8,192 would without them): R-MAT scale 21 (50% empty) 158.8
+    // -> 147.3 us; config 2 and the stencils have none and keep pairs (solo
+    // there: 146.7 vs 131 us; profiles/r04/rmat/).  SBLAS_XS_SOLO=0/1 forces.
+    {
+        long long empty = 0;
+        for (int r = 0; r < m; ++r) empty += rp[r + 1] == rp[r];
+        const char *se = getenv("SBLAS_XS_SOLO");
+        const bool want = se ? atoi(se) != 0 : (m > 0 && 5 * empty >= 2LL * m);
+        P.solo = P.pair && P.dyn && want;
+    }
     const int nrows_cap = P.solo ? kXsItemRows : rows_cap;  // narrow ranges
     const double nfac = P.solo ? 2.0 : 1.0;             // a narrow range's cost, in sub-item caps
 
