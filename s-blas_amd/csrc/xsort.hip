@@ -141,7 +141,8 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 // bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0],
 // bit 3 (xs_stream_dyn only) = no gather at all (a key-derived constant),
 // bit 4 (xs_stream_dyn only) = gathers folded into x[0, 65536) (same lane
-// pattern, an L2-resident 512 KiB: separates L2 fills from L2 requests).
+// pattern, an L2-resident 512 KiB: separates L2 fills from L2 requests),
+// bit 5 (xs_stream_dyn only) = gathers as sc1 loads (L1 bypassed, L2-served).
 template <int kMode, int S>
 __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
                                           const v2d *__restrict__ val2, int ks, int vs, long long c0,
@@ -265,7 +266,10 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
             for (int j = 0; j < 4; ++j) {
                 const uint32_t k = kk[u][j];
                 const int idx = k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits);
-                xx[u][j] = (kMode & 8) ? (double)(k & 1) : x[(kMode & 2) ? 0 : (kMode & 16) ? (idx & 0xffff) : idx];
+                if constexpr ((kMode & 32) != 0)  // experiment: L1-bypassing (sc1) gathers, L2-served
+                    xx[u][j] = __hip_atomic_load(x + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    xx[u][j] = (kMode & 8) ? (double)(k & 1) : x[(kMode & 2) ? 0 : (kMode & 16) ? (idx & 0xffff) : idx];
             }
     };
     auto accumulate = [&](long long cb, const v4u *kk, const v2d *va, const v2d *vb,
@@ -1627,6 +1631,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else kern = mm == 4 ? XS_DYN(4, 2) : XS_DYN(6, 2);
         if ((mode & ~1) == 8 && xu == 1) kern = (mode & 1) ? XS_DYN(9, 1) : XS_DYN(8, 1);  // experiment: no gathers
         if (mode == 16 && xu == 1) kern = XS_DYN(16, 1);  // experiment: L2-resident gathers
+        if (mode == 32 && xu == 1) kern = XS_DYN(32, 1);  // experiment: sc1 (L1-bypassing) gathers
 #undef XS_DYN
     }
     if (P.k24) {  // 24-bit keys: the paired dynamic kernel only (planner)
