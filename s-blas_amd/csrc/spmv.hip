@@ -21,6 +21,7 @@
 //  * alpha/beta are honoured by both (the reference's CSR5 ignored them, Q4);
 //    beta == 0 never reads y (BLAS/cuSPARSE convention).
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <vector>
 
@@ -1315,11 +1316,17 @@ __global__ void k_panel_reduce(const double *__restrict__ ypart, int P, long lon
 }
 
 // thread per row: counts of the row's entries per panel -> rowptr[p][r+1]
+// Rows of >= kPanelLongRow entries are split by a wave each (the _long
+// kernels below): one thread walking a power-law hub row of 62k entries P
+// times made the split of an R-MAT graph take 73 ms.
+constexpr int kPanelLongRow = 256;
+
 __global__ void k_panel_count(const int *__restrict__ rowptr, const int *__restrict__ col, int m,
-                              long long W, int P, int *__restrict__ prp)
+                              long long W, int P, int lmin, int *__restrict__ prp)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= m) return;
+    if (rowptr[r + 1] - rowptr[r] >= lmin) return;  // k_panel_count_long
     for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
         const int p = (int)(col[j] / W);
         prp[(long long)p * (m + 1) + r + 1]++;
@@ -1328,13 +1335,14 @@ __global__ void k_panel_count(const int *__restrict__ rowptr, const int *__restr
 
 // thread per row: stable scatter of the row's entries into the panels
 __global__ void k_panel_scatter(const int *__restrict__ rowptr, const int *__restrict__ col,
-                                const double *__restrict__ val, int m, long long W, int P,
+                                const double *__restrict__ val, int m, long long W, int P, int lmin,
                                 const int *__restrict__ prp, const long long *__restrict__ base,
                                 int *__restrict__ pcol, double *__restrict__ pval)
 {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= m) return;
     const int a = rowptr[r], b = rowptr[r + 1];
+    if (b - a >= lmin) return;  // k_panel_scatter_long
     for (int p = 0; p < P; ++p) {
         long long o = base[p] + prp[(long long)p * (m + 1) + r];
         for (int j = a; j < b; ++j) {
@@ -1344,6 +1352,61 @@ __global__ void k_panel_scatter(const int *__restrict__ rowptr, const int *__res
                 pval[o] = val[j];
                 ++o;
             }
+        }
+    }
+}
+
+// a wave per long row (rows[i]): per 64 entries, one ballot per panel counts
+// (and, in the scatter, ranks) the entries of that panel: the same stable
+// order as the thread-per-row kernels
+__global__ __launch_bounds__(256) void k_panel_count_long(const int *__restrict__ rowptr,
+                                                          const int *__restrict__ col, int m, long long W,
+                                                          int P, const int *__restrict__ rows, int nrows,
+                                                          int *__restrict__ prp)
+{
+    const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= nrows) return;  // wave-uniform
+    const int r = rows[w];
+    const int a = rowptr[r], b = rowptr[r + 1];
+    for (int p = 0; p < P; ++p) {
+        int cnt = 0;
+        for (int j0 = a; j0 < b; j0 += 64) {
+            const int j = j0 + lane;
+            const bool in = j < b && (int)(col[j] / W) == p;
+            cnt += __popcll(__ballot(in));
+        }
+        if (lane == 0) prp[(long long)p * (m + 1) + r + 1] = cnt;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_panel_scatter_long(const int *__restrict__ rowptr,
+                                                            const int *__restrict__ col,
+                                                            const double *__restrict__ val, int m, long long W,
+                                                            int P, const int *__restrict__ rows, int nrows,
+                                                            const int *__restrict__ prp,
+                                                            const long long *__restrict__ base,
+                                                            int *__restrict__ pcol, double *__restrict__ pval)
+{
+    const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= nrows) return;  // wave-uniform
+    const int r = rows[w];
+    const int a = rowptr[r], b = rowptr[r + 1];
+    const unsigned long long below = (1ULL << lane) - 1ULL;
+    for (int p = 0; p < P; ++p) {
+        long long o = base[p] + prp[(long long)p * (m + 1) + r];
+        for (int j0 = a; j0 < b; j0 += 64) {
+            const int j = j0 + lane;
+            const int c = j < b ? col[j] : 0;
+            const bool in = j < b && (int)(c / W) == p;
+            const unsigned long long mask = __ballot(in);
+            if (in) {
+                const long long d = o + __popcll(mask & below);
+                pcol[d] = c;
+                pval[d] = val[j];
+            }
+            o += __popcll(mask);
         }
     }
 }
@@ -1360,9 +1423,24 @@ static int split_panels(const sblas_csr_s &A, int P, hipStream_t s, PanelCsr &o)
     SBLAS_HIP(hipMalloc(&o.val, sizeof(double) * cap));
     SBLAS_HIP(hipMemsetAsync(o.col, 0, sizeof(int) * cap, s));
     SBLAS_HIP(hipMemsetAsync(o.val, 0, sizeof(double) * cap, s));
+    // rows split by a wave each (host rowptr: A.h_rowptr)
+    std::vector<int> hlong;
+    const bool have_h = (long long)A.h_rowptr.size() > m;
+    const int lmin = have_h ? kPanelLongRow : INT_MAX;  // no host copy: every row thread-per-row
+    for (long long r = 0; have_h && r < m; ++r)
+        if (A.h_rowptr[r + 1] - A.h_rowptr[r] >= lmin) hlong.push_back((int)r);
+    int *dlong = nullptr;
+    const int nlong = (int)hlong.size();
+    if (nlong) {
+        SBLAS_HIP(hipMalloc(&dlong, sizeof(int) * nlong));
+        SBLAS_HIP(hipMemcpy(dlong, hlong.data(), sizeof(int) * nlong, hipMemcpyHostToDevice));
+    }
     if (m > 0) {
         hipLaunchKernelGGL(k_panel_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
-                           A.rowptr, A.col, (int)m, o.W, P, o.rowptr);
+                           A.rowptr, A.col, (int)m, o.W, P, lmin, o.rowptr);
+        if (nlong)
+            hipLaunchKernelGGL(k_panel_count_long, dim3((unsigned)((nlong + 3) / 4)), dim3(256), 0, s, A.rowptr,
+                               A.col, (int)m, o.W, P, dlong, nlong, o.rowptr);
         int *scratch = nullptr;
         SBLAS_HIP(hipMalloc(&scratch, sizeof(int) * ((m + 1) / 1024 + 256)));
         for (int p = 0; p < P; ++p) SBLAS_TRY(scan_inclusive(o.rowptr + p * (m + 1), m + 1, scratch, s));
@@ -1383,9 +1461,13 @@ static int split_panels(const sblas_csr_s &A, int P, hipStream_t s, PanelCsr &o)
     SBLAS_HIP(hipMemcpy(dbase, o.base.data(), sizeof(long long) * P, hipMemcpyHostToDevice));
     if (m > 0)
         hipLaunchKernelGGL(k_panel_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
-                           A.rowptr, A.col, A.val, (int)m, o.W, P, o.rowptr, dbase, o.col, o.val);
+                           A.rowptr, A.col, A.val, (int)m, o.W, P, lmin, o.rowptr, dbase, o.col, o.val);
+    if (m > 0 && nlong)
+        hipLaunchKernelGGL(k_panel_scatter_long, dim3((unsigned)((nlong + 3) / 4)), dim3(256), 0, s, A.rowptr,
+                           A.col, A.val, (int)m, o.W, P, dlong, nlong, o.rowptr, dbase, o.col, o.val);
     SBLAS_HIP(hipStreamSynchronize(s));
     (void)hipFree(dbase);
+    (void)hipFree(dlong);
     return SBLAS_OK;
 }
 
