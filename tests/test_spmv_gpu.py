@@ -132,6 +132,19 @@ def test_ragged_long_empty(torch_cuda, sb, orc, algo, beta):
     check(orc, rp, col, val, x, 1.25, beta, y0c, got)
 
 
+@pytest.mark.parametrize("beta", [0.0, 0.75])
+def test_mostly_empty_rows(torch_cuda, sb, orc, algo, beta):
+    """60% empty rows (a power-law graph's share): xsort takes its solo layout
+    by default (>= 40% empty), the other algorithms their usual one."""
+    rng = np.random.default_rng(11)
+    m, n = 60000, 70000
+    rp, col, val = random_csr(rng, m, n, 40, long_rows=[(3, 3000), (31000, 12000)], empty_frac=0.6)
+    x = rng.standard_normal(n)
+    y0 = rng.standard_normal(m)
+    got = run_gpu(torch_cuda, sb, algo, n, rp, col, val, x, 0.5, beta, y0)
+    check(orc, rp, col, val, x, 0.5, beta, y0, got)
+
+
 def test_edge_shapes(torch_cuda, sb, orc, algo):
     rng = np.random.default_rng(3)
     # all rows empty
