@@ -10,3 +10,8 @@ for g in 1 2; do
     grep -i "average\|Average" $O/qh768_g${g}_k$k.txt | head -3 | sed "s/^/g$g k$k: /"
   done
 done
+# the SpMM row of results.csv: qh768 x 128 dense columns, 1 and 2 GPUs (run_test.py:146-160's argv)
+for g in 1 2; do
+  timeout -k 10 120 s-blas_amd/bin/test_spmm tests/golden/qh768.mtx 128 $g 1 > $O/spmm_qh768_g$g.txt 2>&1 || { tail $O/spmm_qh768_g$g.txt; exit 1; }
+  grep -i "SPMM\|check" $O/spmm_qh768_g$g.txt | head -3 | sed "s/^/spmm g$g: /"
+done
