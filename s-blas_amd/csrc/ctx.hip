@@ -61,12 +61,20 @@ struct sblas_ctx_s {
     std::vector<sblas_csr> P;          // [g * parts] part handles (device-major)
     std::vector<hipStream_t> cst;      // [g] comm streams
     std::vector<hipEvent_t> evp;       // [g * parts] part kernel done (main stream)
+    std::vector<int> evp_dev;          // [g * parts] the device each evp event was created on
     std::vector<hipEvent_t> evc;       // [g] comm stream done (joins the main stream)
     std::vector<int> palgo;            // [g] the algorithm the part handles run (AUTO resolved)
     int parts_req = 1;                 // requested by sblas_ctx_matrix_upload_parts
     // one device, one part: nothing to exchange; yfull[0] IS ylocal[0] (its
     // first m rows are y in row order under either partition)
     bool yalias = false;
+    // SBLAS_CTX_NOALIAS=1 (read once, at sblas_ctx_create): a one-device
+    // context still runs the exchange (ncclAllGather + placement, or
+    // ncclAllReduce + re-prime) on its 1-rank communicator, so the
+    // collectives execute on a one-GPU box
+    bool noalias = false;
+    // loopback all-reduce: peer access this context enabled (a -> b), undone on destroy
+    std::vector<std::pair<int, int>> peers;
 };
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
@@ -337,17 +345,20 @@ int ensure_overlap_streams(sblas_ctx_s &C)
         if (!C.evc[d]) SBLAS_HIP(hipEventCreateWithFlags(&C.evc[d], hipEventDisableTiming));
     }
     const size_t need = (size_t)g * C.parts;
-    if (C.evp.size() < need) {
-        // device-major: event i belongs to device i / (evp.size() / g)
-        std::vector<hipEvent_t> old = C.evp;
-        const size_t per_old = old.empty() ? 0 : old.size() / g;
-        for (size_t i = 0; i < old.size(); ++i) {
-            DeviceGuard gd(C.dev[i / per_old]);
-            (void)hipEventDestroy(old[i]);
+    if (C.evp.size() != need) {
+        // device-major: event i belongs to device i / parts.  Rebuilt whenever
+        // the part count changes (a re-upload with fewer parts must not record
+        // an event created on another device), each old event destroyed on
+        // the device it was created on
+        for (size_t i = 0; i < C.evp.size(); ++i) {
+            DeviceGuard gd(C.evp_dev[i]);
+            if (C.evp[i]) (void)hipEventDestroy(C.evp[i]);
         }
         C.evp.assign(need, nullptr);
+        C.evp_dev.assign(need, 0);
         for (size_t i = 0; i < need; ++i) {
-            DeviceGuard gd(C.dev[i / C.parts]);
+            C.evp_dev[i] = C.dev[i / C.parts];
+            DeviceGuard gd(C.evp_dev[i]);
             SBLAS_HIP(hipEventCreateWithFlags(&C.evp[i], hipEventDisableTiming));
         }
     }
@@ -356,7 +367,8 @@ int ensure_overlap_streams(sblas_ctx_s &C)
 
 // device d's part handles: part p = its local rows of local chunks
 // [plo[p], plo[p+1]), all run with the whole slice's algorithm (AUTO
-// resolved once on the whole slice, so every part runs the same kernel)
+// resolved once on the whole slice, after sblas_csr_analyse has applied its
+// fallback, so every part runs the same kernel the plain path would)
 int upload_parts(sblas_ctx_s &C, int d, const std::vector<long long> &lrp, const std::vector<int> &lcol,
                  const std::vector<double> &lval)
 {
@@ -372,6 +384,40 @@ int upload_parts(sblas_ctx_s &C, int d, const std::vector<long long> &lrp, const
                                          (int)r1, lrp[r0], lrp[r1], C.st[d]));
         SBLAS_TRY(sblas_csr_analyse(H, a, C.st[d]));
     }
+    return SBLAS_OK;
+}
+
+// The loopback all-reduce (k_ctx_sum) reads every rank's send buffer from
+// the summing rank's device: ranks wrapped onto distinct GPUs need peer
+// access between them (refused if a pair has none).  Only this exchange
+// needs it -- the all-gather's device-to-device copies do not -- and what
+// the context enables here it disables on destroy.
+int enable_loopback_peers(sblas_ctx_s &C)
+{
+    for (int a = 0; a < C.g; ++a)
+        for (int b = 0; b < C.g; ++b) {
+            const int da = C.dev[a], db = C.dev[b];
+            if (da == db) continue;
+            if (std::find(C.peers.begin(), C.peers.end(), std::make_pair(da, db)) != C.peers.end()) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, da, db) != hipSuccess || !can) {
+                set_error("sblas_ctx_matrix_upload: loopback all-reduce over devices %d and %d without peer "
+                          "access", da, db);
+                return SBLAS_ERR_UNSUPPORTED;
+            }
+            DeviceGuard gd(da);
+            const hipError_t e = hipDeviceEnablePeerAccess(db, 0);
+            if (e == hipErrorPeerAccessAlreadyEnabled) {  // enabled by someone else: leave it on
+                (void)hipGetLastError();
+                continue;
+            }
+            if (e != hipSuccess) {
+                set_error("sblas_ctx_matrix_upload: hipDeviceEnablePeerAccess(%d -> %d): %s", da, db,
+                          hipGetErrorString(e));
+                return SBLAS_ERR_HIP;
+            }
+            C.peers.emplace_back(da, db);
+        }
     return SBLAS_OK;
 }
 
@@ -438,33 +484,12 @@ int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist)
                 return SBLAS_ERR_INVALID;
             }
     }
-    if (loopback) {
-        // the loopback all-reduce (k_ctx_sum) reads every rank's send buffer
-        // from the summing rank's device: ranks wrapped onto distinct GPUs
-        // need peer access between them (refused if the pair has none)
-        for (int a = 0; a < ngpu; ++a)
-            for (int b = 0; b < ngpu; ++b) {
-                if (dev[a] == dev[b]) continue;
-                int can = 0;
-                if (hipDeviceCanAccessPeer(&can, dev[a], dev[b]) != hipSuccess || !can) {
-                    set_error("sblas_ctx_create: loopback over devices %d and %d without peer access",
-                              dev[a], dev[b]);
-                    return SBLAS_ERR_UNSUPPORTED;
-                }
-                DeviceGuard gd(dev[a]);
-                const hipError_t e = hipDeviceEnablePeerAccess(dev[b], 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
-                    set_error("sblas_ctx_create: hipDeviceEnablePeerAccess(%d -> %d): %s", dev[a], dev[b],
-                              hipGetErrorString(e));
-                    return SBLAS_ERR_HIP;
-                }
-                (void)hipGetLastError();  // clear an "already enabled" status
-            }
-    }
     auto *C = new sblas_ctx_s();
     C->g = ngpu;
     C->dev = dev;
     C->loopback = loopback;
+    const char *nae = getenv("SBLAS_CTX_NOALIAS");
+    C->noalias = nae && atoi(nae) != 0;
     C->comm.assign(ngpu, nullptr);
     if (!loopback) {
         ncclResult_t r = ncclCommInitAll(C->comm.data(), ngpu, dev.data());
@@ -513,9 +538,14 @@ int sblas_ctx_destroy(sblas_ctx C)
         if (d < (int)C->evc.size() && C->evc[d]) (void)hipEventDestroy(C->evc[d]);
     }
     for (size_t i = 0; i < C->evp.size(); ++i) {
-        DeviceGuard g(C->dev[i / std::max<size_t>(1, C->evp.size() / C->g)]);
+        DeviceGuard g(C->evp_dev[i]);
         if (C->evp[i]) (void)hipEventDestroy(C->evp[i]);
     }
+    for (const auto &pr : C->peers) {
+        DeviceGuard g(pr.first);
+        (void)hipDeviceDisablePeerAccess(pr.second);
+    }
+    (void)hipGetLastError();
     delete C;
     return SBLAS_OK;
 }
@@ -540,6 +570,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
     }
     free_matrix(*C);
     const int g = C->g;
+    if (C->loopback && exchange == SBLAS_CTX_ALLREDUCE) SBLAS_TRY(enable_loopback_peers(*C));
     C->m = m;
     C->n = n;
     C->nnz = rowptr[m];
@@ -590,7 +621,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             SBLAS_TRY(ensure_overlap_streams(*C));
         }
     }
-    C->yalias = g == 1 && C->parts <= 1;
+    C->yalias = g == 1 && C->parts <= 1 && !C->noalias;
     int st = SBLAS_OK;
     for (int d = 0; d < g && st == SBLAS_OK; ++d) {
         DeviceGuard gd(C->dev[d]);
@@ -607,6 +638,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             C->lnnz[d] = lz;
             st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, lrp.data(), lcol.data(), lval.data(), 0,
                                         (int)lm, 0, lz, C->st[d]);
+            if (st == SBLAS_OK) st = sblas_csr_analyse(C->A[d], algo, C->st[d]);
             if (st == SBLAS_OK && C->parts > 1) st = upload_parts(*C, d, lrp, lcol, lval);
         } else {
             C->lrows[d] = std::max(0, er[d] - sr[d] + 1);
@@ -614,9 +646,8 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
             if (exchange == SBLAS_CTX_ALLREDUCE) C->yoff[d] = sr[d];
             st = sblas_csr_upload_slice(&C->A[d], C->dev[d], n, rowptr, col, val, sr[d], er[d] + 1,
                                         si[d], ei[d] + 1, C->st[d]);
+            if (st == SBLAS_OK) st = sblas_csr_analyse(C->A[d], algo, C->st[d]);
         }
-        if (st != SBLAS_OK) break;
-        st = sblas_csr_analyse(C->A[d], algo, C->st[d]);
         if (st != SBLAS_OK) break;
         hipError_t e = hipMalloc(&C->x[d], sizeof(double) * std::max(n, 1));
         if (e == hipSuccess) e = hipMalloc(&C->ylocal[d], sizeof(double) * C->ylen);

@@ -2,11 +2,17 @@
 
 The context is the C-ABI's multi-GPU SpMV: ncclCommInitAll over distinct
 devices, resident slices, ncclBroadcast of x, ONE ncclAllGather of the y
-slices and device placement.  On the one-GPU box it runs with a 1-rank
-communicator (the collectives execute; the partition/placement logic for
-g > 1 is covered on the CPU by tests/test_host.py and by the torch
-ranks of tests/test_cli_gpu.py, which use the same distribution).  Parity:
-the oracle's CSR SpMV with the per-row fp64 bound.
+slices and device placement (or configs[2]'s ncclAllReduce of the
+zero-padded y).  On the one-GPU box the communicator has one rank:
+ncclBroadcast and the timing protocol's aligning ncclAllReduce run on every
+context; a plain one-device context aliases y and skips the y exchange, so
+the y collectives (ncclAllGather, ncclAllReduce of y) run only where the
+tests set SBLAS_CTX_NOALIAS=1 (test_ctx_noalias_exchange_rccl) and in the
+overlapped form (test_ctx_overlap_parts, g = 1).  The g > 1 partition /
+exchange / placement logic runs in loopback (SBLAS_CTX_LOOPBACK=1: ranks on
+one GPU, collectives as stream-ordered device copies) and on the CPU in
+tests/test_host.py and tests/test_dist_cpu.py.  Parity: the oracle's CSR
+SpMV with the per-row fp64 bound.
 """
 import os
 import subprocess
@@ -262,3 +268,82 @@ def test_ctx_overlap_config2_full_size_g8(torch_cuda, sb, orc, monkeypatch):
         for d in range(1, 8):
             assert np.array_equal(got[0], got[d]), (parts, d)
         ctx.close()
+
+
+@pytest.mark.parametrize("algo", [1, 2, 5])
+@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
+def test_ctx_noalias_exchange_rccl(torch_cuda, sb, orc, monkeypatch, algo, partition, exchange):
+    """SBLAS_CTX_NOALIAS=1: a one-device context keeps
+    its y exchange, so xchg_spmv's ncclAllGather (exchange 0) and the literal
+    ncclAllReduce of the zero-padded y (exchange 1, BASELINE configs[2]) run
+    on the 1-rank communicator, followed by the placement / re-prime kernels.
+    Three chained steps against the oracle; the exchange takes device time."""
+    monkeypatch.setenv("SBLAS_CTX_NOALIAS", "1")
+    rng = np.random.default_rng(500 + 10 * algo + 3 * partition + exchange)
+    m, n = 6000, 8000
+    rp, col, val = rand_csr(rng, m, n, 40, long_rows=[(5, 7000), (5999, 2000)])
+    x = rng.standard_normal(n)
+    y = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(1)
+    ctx.upload(m, n, rp, col, val, algo, partition, exchange)
+    ctx.set_x(x)
+    ctx.set_y(y)
+    for step in range(3):
+        st = ctx.spmv_ex(alpha, beta, delay_us=100.0 if step == 1 else 0.0)
+        assert st[1] > 0.0, st  # the collective + placement ran after the kernel
+        want = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+        got = ctx.get_y()
+        assert np.all(np.abs(got - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y)), step
+        y = got
+    ctx.close()
+
+
+def test_ctx_noalias_config3_full_size(torch_cuda, sb, orc, monkeypatch):
+    """configs[2]'s dataflow at full size on one device with the y exchange
+    kept: CSR5, nnz partition, ncclAllReduce of the 2e6-row zero-padded y."""
+    monkeypatch.setenv("SBLAS_CTX_NOALIAS", "1")
+    n = 2_000_000
+    rp = sb.gen_synth_rowptr(n)
+    col, val = sb.gen_synth_rows(n, rp, 0, n)
+    x = sb.gen_vector(n, 43)
+    y0 = sb.gen_vector(n, 44)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(1)
+    ctx.upload(n, n, rp, col, val, sb.CSR5, 1, sb.CTX_ALLREDUCE)
+    ctx.set_x(x)
+    ctx.set_y(y0)
+    st = ctx.spmv_ex(alpha, beta, delay_us=200.0)
+    assert st[1] > 0.0
+    got = ctx.get_y()
+    want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
+    assert np.all(np.abs(got - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+    ctx.close()
+
+
+@pytest.mark.parametrize("g", [1, 2])
+def test_ctx_reupload_fewer_parts(torch_cuda, sb, orc, monkeypatch, g):
+    """one context re-uploaded with 4 parts, then 2, then 3; the
+    part events are rebuilt for each part count (each on its own device),
+    and every step matches the oracle."""
+    if g > 1:
+        monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    rng = np.random.default_rng(77 + g)
+    m, n = 7000, 9000
+    rp, col, val = rand_csr(rng, m, n, 30)
+    x = rng.standard_normal(n)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(g)
+    for parts in (4, 2, 3):
+        ctx.upload_parts(m, n, rp, col, val, 0, parts)
+        assert ctx.parts() == parts
+        y = rng.standard_normal(m)
+        ctx.set_x(x)
+        ctx.set_y(y)
+        ctx.spmv_ex(alpha, beta)
+        want = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+        got = [ctx.get_y(d) for d in range(g)]
+        assert np.all(np.abs(got[0] - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y)), parts
+        for d in range(1, g):
+            assert np.array_equal(got[0], got[d])
+    ctx.close()
