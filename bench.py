@@ -119,10 +119,7 @@ class Workload:
                 f"y=alpha*A*x+beta*y, {algo} kernel")
 
 
-def _time_cpu(rowptr, col, val, x, m, nnz, budget_s, threads, runs=3):
-    """Times the oracle port (oracle/liboracle.so) `runs` times each, multi-
-    threaded and single-core, and returns the medians.  Called only in the
-    --cpu-baseline-only child (cpu_baseline below)."""
+def _cpu_lib():
     import ctypes as C
     lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     f = lib.orc_csr_spmv_omp
@@ -132,23 +129,69 @@ def _time_cpu(rowptr, col, val, x, m, nnz, budget_s, threads, runs=3):
     g = lib.orc_csr_spmv
     g.restype = None
     g.argtypes = f.argtypes[:-1]
-    y = np.zeros(m)
-    args = (m, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data, x.ctypes.data, ALPHA, BETA,
-            y.ctypes.data)
+    return f, g
 
-    def timeit(fn, extra, share):
-        fn(*args, *extra)  # warm-up (page-in, thread pool)
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            fn(*args, *extra)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el > share or reps >= 200:
-                return reps, el / reps
 
-    mt = [timeit(f, (threads,), budget_s * 0.5 / runs) for _ in range(runs)]
-    st = [timeit(g, (), budget_s * 0.5 / runs) for _ in range(runs)]
-    return mt, st
+def _time_cpu(fn, args, extra, share, max_reps=200):
+    """(reps, seconds per call) of fn over about `share` seconds, after one
+    warm-up call (page-in, thread pool)."""
+    fn(*args, *extra)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn(*args, *extra)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > share or reps >= max_reps:
+            return reps, el / reps
+
+
+def _interleave_memory():
+    """Interleave this process's future pages over every online NUMA node
+    (set_mempolicy(MPOL_INTERLEAVE), what `numactl --interleave=all` does; the
+    image has no numactl), so a multi-socket host's threads read the matrix
+    from every socket's memory.  Returns the node list string, or None."""
+    try:
+        with open("/sys/devices/system/node/online") as fh:
+            spec = fh.read().strip()
+    except OSError:
+        return None
+    nodes = []
+    for part in spec.split(","):
+        a, _, b = part.partition("-")
+        nodes.extend(range(int(a), int(b or a) + 1))
+    if len(nodes) < 2:
+        return spec + " (one node: nothing to interleave)"
+    import ctypes as C
+    mask = (C.c_ulong * 16)()
+    for nd in nodes:
+        mask[nd // 64] |= 1 << (nd % 64)
+    libc = C.CDLL(None, use_errno=True)
+    MPOL_INTERLEAVE, SYS_set_mempolicy = 3, 238  # x86_64
+    if libc.syscall(SYS_set_mempolicy, MPOL_INTERLEAVE, mask, C.c_ulong(16 * 64)) != 0:
+        return spec + f" (set_mempolicy failed: errno {C.get_errno()})"
+    return spec + " (pages interleaved)"
+
+
+def _cpu_quota():
+    """The cgroup CPU quota (cores), or None when unlimited / unreadable."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as fh:
+                txt = fh.read().strip()
+        except OSError:
+            continue
+        if parse:
+            q, per = parse(txt)
+            if q == "max":
+                return None
+            return float(q) / float(per)
+        q = float(txt)
+        if q < 0:
+            return None
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            return q / float(fh.read().strip())
+    return None
 
 
 def cpu_baseline_child(args) -> int:
@@ -157,15 +200,35 @@ def cpu_baseline_child(args) -> int:
     object.  Runs in its own process so that the OpenMP runtime starts with
     the pinning environment cpu_baseline() sets (OMP_PROC_BIND is read once,
     when libgomp initialises -- in the bench process torch/libsblas have
-    already done that)."""
+    already done that).  SURVEY §8 M1-cpu asks for all host cores: the
+    thread count is swept (16, 32, 64, 128, ... up to the affinity mask's
+    CPU count, which is included), each count timed briefly, and the best
+    count timed again as the median of 3 runs; pages are interleaved over
+    the NUMA nodes first."""
+    try:  # before libgomp loads: it pins the initial thread to the first place
+        mask = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        mask = os.cpu_count() or 1
+    numa = _interleave_memory()
     import sblas
     W = Workload(args, sblas)
     col, val = W.rows(0, W.n)
     x = sblas.gen_vector(W.n, 43)
     rp = np.ascontiguousarray(W.rowptr, np.int64)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    mt, st = _time_cpu(rp, np.ascontiguousarray(col, np.int32), np.ascontiguousarray(val, np.float64),
-                       x, W.n, W.nnz, args.cpu_budget, threads)
+    col = np.ascontiguousarray(col, np.int32)
+    val = np.ascontiguousarray(val, np.float64)
+    f, g = _cpu_lib()
+    y = np.zeros(W.n)
+    cargs = (W.n, rp.ctypes.data, col.ctypes.data, val.ctypes.data, x.ctypes.data, ALPHA, BETA, y.ctypes.data)
+    counts = sorted({c for c in (16, 32, 64, 128, 256, 512) if c < mask} | {mask})
+    gf = lambda t: 2.0 * W.nnz / t / 1e9  # noqa: E731
+    budget = args.cpu_budget
+    sweep = {}
+    for c in counts:
+        sweep[c] = gf(_time_cpu(f, cargs, (c,), budget * 0.25 / len(counts))[1])
+    best = max(sweep, key=sweep.get)
+    mt = [_time_cpu(f, cargs, (best,), budget * 0.4 / 3) for _ in range(3)]
+    st = [_time_cpu(g, cargs, (), budget * 0.35 / 3) for _ in range(3)]
     t_mt = float(np.median([t for _, t in mt]))
     t_st = float(np.median([t for _, t in st]))
     model = "unknown"
@@ -177,18 +240,21 @@ def cpu_baseline_child(args) -> int:
                     break
     except OSError:
         pass
-    allowed = os.environ.get("SBLAS_BENCH_AFFINITY", "?")  # the parent's mask (libgomp pins ours)
-    gf = lambda t: 2.0 * W.nnz / t / 1e9  # noqa: E731
+    quota = _cpu_quota()
     print(json.dumps({
-        "value": round(gf(t_mt), 3), "unit": "GFLOP/s", "cores": threads,
+        "value": round(gf(t_mt), 3), "unit": "GFLOP/s", "cores": best,
         "kind": "port", "cpu_model": model,
         "sample": (f"full matrix of the workload, orc_csr_spmv_omp (OpenMP, schedule dynamic, "
-                   f"{threads} threads, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} "
-                   f"OMP_PLACES={os.environ.get('OMP_PLACES')}, {allowed} CPUs in the affinity mask): "
-                   f"median of {len(mt)} runs of {'/'.join(str(r) for r, _ in mt)} reps = "
-                   f"{t_mt * 1e3:.2f} ms/SpMV (runs: {', '.join(f'{gf(t):.1f}' for _, t in mt)} GFLOP/s); "
-                   f"single-core scalar port orc_csr_spmv, median of {len(st)} runs: "
-                   f"{t_st * 1e3:.1f} ms/SpMV = {gf(t_st):.3f} GFLOP/s"),
+                   f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} OMP_PLACES={os.environ.get('OMP_PLACES')}, "
+                   f"{mask} CPUs in the affinity mask, cgroup quota "
+                   f"{'none' if quota is None else f'{quota:.1f} CPUs'}, NUMA {numa}); thread sweep "
+                   + ", ".join(f"{c}: {v:.1f}" for c, v in sweep.items()) +
+                   f" GFLOP/s; best {best} threads, median of {len(mt)} runs of "
+                   f"{'/'.join(str(r) for r, _ in mt)} reps = {t_mt * 1e3:.2f} ms/SpMV (runs: "
+                   f"{', '.join(f'{gf(t):.1f}' for _, t in mt)} GFLOP/s); single-core scalar port orc_csr_spmv, "
+                   f"median of {len(st)} runs: {t_st * 1e3:.1f} ms/SpMV = {gf(t_st):.3f} GFLOP/s"),
+        "thread_sweep_gflops": {str(c): round(v, 3) for c, v in sweep.items()},
+        "affinity_cpus": mask, "cgroup_cpu_quota": quota, "numa": numa,
         "runs_gflops": [round(gf(t), 3) for _, t in mt],
         "single_core_value": round(gf(t_st), 3),
     }), flush=True)
@@ -198,17 +264,12 @@ def cpu_baseline_child(args) -> int:
 def cpu_baseline(args):
     """The oracle restatement (oracle/liboracle.so) timed on this host's cores,
     in a child process (cpu_baseline_child) with the threads pinned
-    (OMP_PROC_BIND=close, OMP_PLACES=cores); the median of 3 runs.  Only this
-    leg of bench.py (and the post-timing --check) touches oracle/."""
+    (OMP_PROC_BIND=close, OMP_PLACES=cores) and the thread count swept.  Only
+    this leg of bench.py (and the post-timing --check) touches oracle/."""
     import subprocess
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    env = dict(os.environ, OMP_PROC_BIND="close", OMP_PLACES="cores")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    try:
-        env["SBLAS_BENCH_AFFINITY"] = str(len(os.sched_getaffinity(0)))
-    except (AttributeError, OSError):
-        pass
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--matrix", args.matrix,
            "--nrows", str(args.nrows), "--heavy", str(args.heavy), "--light", str(args.light),
            "--cols", args.cols, "--grid", str(args.grid), "--scale", str(args.scale),
@@ -217,6 +278,47 @@ def cpu_baseline(args):
     if r.returncode != 0:
         return {"error": f"cpu baseline child exited {r.returncode}: {r.stderr[-400:]}"}
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def measured_peak(torch, sblas, dev, stream):
+    """this GPU's streaming ceiling, measured with the
+    library's hand-written probes (csrc/probe.hip: 16-B loads, 8 in flight
+    per lane, grid-stride) over a 4 GiB buffer (16x the 256 MB Infinity
+    Cache, so every pass streams from HBM): plain and non-temporal reads, and
+    a 1 GiB -> 1 GiB copy; 4 / 8 / 16 workgroups per CU; best of 3 per shape,
+    HIP events on the launch stream.  Reported beside the 8 TB/s spec, which
+    stays the roofline's `peak`."""
+    nbytes = 4 << 30
+    src = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
+    sink = torch.zeros(1, dtype=torch.float64, device=dev)
+    dst = torch.empty(1 << 27, dtype=torch.float64, device=dev)  # 1 GiB
+    sp = stream.cuda_stream
+    best = {}
+    with torch.cuda.stream(stream):
+        for mode, nb, out in ((0, nbytes, sink), (1, nbytes, sink), (3, nbytes, sink), (4, nbytes, sink),
+                              (2, 1 << 30, dst)):
+            for wg in (2, 4, 8, 16):
+                sblas.hbm_probe(mode, src.data_ptr(), out.data_ptr(), nb, wg, sp)
+                for _ in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    sblas.hbm_probe(mode, src.data_ptr(), out.data_ptr(), nb, wg, sp)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    moved = nb * (2 if mode == 2 else 1)
+                    gbs = moved / (e0.elapsed_time(e1) * 1e-3) / 1e9
+                    if gbs > best.get(mode, (0.0, 0))[0]:
+                        best[mode] = (gbs, wg)
+    del src, sink, dst
+    names = {0: "read_grid_stride", 1: "read_nt_grid_stride", 3: "read_blocked", 4: "read_nt_blocked"}
+    rd = max(best[k][0] for k in names)
+    return {"read_GBps": round(rd, 1),
+            **{f"{v}_GBps": round(best[k][0], 1) for k, v in names.items()},
+            "copy_GBps": round(best[2][0], 1),
+            "wg_per_cu": {**{v: best[k][1] for k, v in names.items()}, "copy": best[2][1]},
+            "how": ("sblas_hbm_probe (csrc/probe.hip): 16-B loads, 8 in flight per lane, plain / non-temporal, "
+                    "grid-stride / one contiguous span per workgroup, over 4 GiB (read) and 1 GiB -> 1 GiB "
+                    "(copy, bytes read + written), 2/4/8/16 WG per CU, best of 3, HIP events")}
 
 
 def choose_driver(gpus: int, env, ndev: int, requested: str = "auto", loopback: bool = False) -> str:
@@ -247,17 +349,51 @@ def choose_driver(gpus: int, env, ndev: int, requested: str = "auto", loopback: 
     return "ctx"
 
 
-def pmc_traffic(algo_name: str):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary
-    (profiles/pmc_<algo>.json, written by tools/pmc_traffic.py), or None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{algo_name}.json")
+def lib_sha256() -> str:
+    """sha256 of the libsblas.so this process loaded (sblas.LIB_PATH)."""
+    import hashlib
+    import sblas
+    h = hashlib.sha256()
+    with open(sblas.LIB_PATH, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+TRAFFIC_NOTES = {}
+
+
+def _stamped_traffic(name: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary
+    profiles/pmc_<name>.json (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE,
+    separate passes), reported only while that summary's `lib_sha256` equals
+    the hash of the libsblas.so loaded now: a kernel change invalidates it
+    and the line says so (TRAFFIC_NOTES) instead of carrying a stale number."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if not os.path.exists(p):
+        TRAFFIC_NOTES[name] = "no committed PMC summary"
         return None
     try:
         with open(p) as fh:
-            return float(json.load(fh)["hbm_bytes_per_launch"])
-    except Exception:
+            d = json.load(fh)
+        stamp = d.get("lib_sha256")
+        if stamp is None:
+            TRAFFIC_NOTES[name] = f"{os.path.relpath(p, ROOT)} carries no lib_sha256 stamp"
+            return None
+        if stamp != lib_sha256():
+            TRAFFIC_NOTES[name] = (f"{os.path.relpath(p, ROOT)} was measured on libsblas.so {stamp[:12]}, "
+                                   f"this run loaded {lib_sha256()[:12]}: not reported")
+            return None
+        TRAFFIC_NOTES[name] = f"{os.path.relpath(p, ROOT)} (libsblas.so {stamp[:12]}, the loaded build)"
+        return float(d["hbm_bytes_per_launch"])
+    except Exception as e:  # noqa: BLE001
+        TRAFFIC_NOTES[name] = f"unreadable PMC summary: {e}"
         return None
+
+
+def pmc_traffic(algo_name: str):
+    """HBM bytes per launch of the SpMV kernel `algo_name` (_stamped_traffic)."""
+    return _stamped_traffic(algo_name)
 
 
 CONFIG3 = ("BASELINE configs[2]: the same matrix, CSR5 segmented-sum kernel, rows split by nnz "
@@ -323,6 +459,247 @@ def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us, pro
         dev_bytes, [float(np.mean(st[:, 3 + 3 * d])) for d in range(N)], check,
         "cold steps (1 GiB read sweep before each), sblas_ctx_spmv_ex per-device spans, max over devices",
         exchange="allreduce", traffic=pmc_traffic("csr5") if profiled else None, nnz_per_device=[int(z) for _, z, _ in info])
+
+
+CONFIG4 = ("BASELINE configs[3]: C = -0.7*A*B + 0.8*C (dspmm_baseline_test.cu:518-519), B dense of width 64 "
+           "resident row-major, on a rail4284-shaped stand-in (m 4,284, k 1,092,610, nnz 11,279,748, uniform-random "
+           "distinct sorted columns, seed 44; rail4284 itself is not in the container)")
+CONFIG5 = ("BASELINE configs[4]: sync-free SpTRSV, forward solve of a unit-lower circuit5M-class stand-in "
+           "(n 5,558,326, 5 off-diagonals per column in a band of 80,000, ~985 level sets; circuit5M is not in the "
+           "container), integer known-answer system (off-diagonals 1..10, x_ref in 1..10, b = L x_ref exact)")
+
+
+def _hold_events(torch, stream, fn):
+    """One cold step's device time: a device-side hold queued ahead of the
+    start event (so the host has enqueued the step before the stream reaches
+    it), then HIP events on the launch stream around fn's two phases.
+    fn(ev) records ev[1] between its phases; returns (phase 1, phase 2) ms."""
+    ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(500_000)
+        ev[0].record(stream)
+        fn(ev)
+        ev[2].record(stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+
+
+def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier):
+    """configs[3] on every line: the SpMM, rows of A split
+    by nnz over the ranks (B replicated, C row slices all-gathered; the
+    reference's dspmm_mgpu_baseline.cu:147-150 splits B/C columns instead),
+    timed with the SpMV leg's cold protocol (1 GiB sweep, barrier, device-side
+    hold, HIP events on the launch stream around kernel and all-gather), max
+    over ranks; then one fresh product from C0 whose EVERY entry rank 0
+    checks against the oracle's csrmm restatement under the per-entry fp64
+    bound (dspmm_baseline_test.cu:544-549 checks every entry too)."""
+    sys.path.insert(0, os.path.join(ROOT, "s-blas_amd", "tools"))
+    from bench_spmm import rail_like
+    m, k, n, nnz = 4284, 1_092_610, 64, 11_279_748
+    alpha, beta = -0.7, 0.8
+    t0 = time.perf_counter()
+    rp, col = rail_like(m, k, nnz, 44)
+    val = np.random.default_rng(45).random(nnz)
+    gen_s = time.perf_counter() - t0
+    dev = torch.device("cuda", dev_idx)
+    B = torch.rand((k, n), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(45))
+    C0 = torch.rand((n, m), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(46))
+    stream = torch.cuda.Stream(device=dev)
+    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist)
+    sp = stream.cuda_stream
+    with torch.cuda.stream(stream):
+        op.load_c(C0)
+        t0 = time.perf_counter()
+        op.kernel(alpha, B, beta, sp)  # first call: builds the C-tile plan
+        op.exchange()
+        torch.cuda.synchronize()
+        first_s = time.perf_counter() - t0
+        for _ in range(max(1, args.warmup)):
+            op.kernel(alpha, B, beta, sp)
+            op.exchange()
+        torch.cuda.synchronize()
+
+    def step(ev):
+        op.kernel(alpha, B, beta, sp)
+        ev[1].record(stream)
+        op.exchange()
+
+    kern, xch = [], []
+    for _ in range(args.steps):
+        evict()
+        sync_barrier()
+        a, b = _hold_events(torch, stream, step)
+        kern.append(a)
+        xch.append(b)
+        sync_barrier()
+    r0, r1 = op.r0, op.r1
+    lnnz = int(rp[r1] - rp[r0])
+    lbytes = 12 * lnnz + 4 * (r1 - r0 + 1) + 8 * k * n + 16 * (r1 - r0) * n
+    mine = np.array([np.mean(kern), np.mean(xch), np.mean(np.array(kern) + np.array(xch)), lbytes, lnnz])
+    per = _gather_rows(torch, dist, dev, mine, world)
+    check = None
+    if args.check_legs:
+        with torch.cuda.stream(stream):
+            op.load_c(C0)
+            op.kernel(alpha, B, beta, sp)
+            op.exchange()
+        torch.cuda.synchronize()
+        if rank == 0:
+            got = op.result().cpu().numpy()  # (n, m): C column-major
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import orc  # oracle: checker only
+            want, bound = orc.spmm_checked(m, n, alpha, rp, col, val, B.cpu().numpy(), beta, C0.cpu().numpy().T)
+            diff = np.abs(got.T - want)
+            check = {"entries": int(diff.size), "pass": bool(np.all(diff <= bound)),
+                     "max_excess_over_bound": float(np.max(diff - bound)),
+                     "abs_1e-3": bool(np.all(diff < 1e-3 * np.maximum(1.0, np.abs(want))))}
+    op.close()
+    del B, C0
+    return config4_object(world, per, first_s, gen_s, check,
+                          _stamped_traffic("spmm_ctile") if world == 1 else None)
+
+
+def config4_object(world, per, first_s, gen_s, check, traffic):
+    """The `config4` object: per = one row per rank of
+    (kernel ms, all-gather ms, step ms, algorithmic bytes, nnz)."""
+    per = np.asarray(per, np.float64)
+    kmax, xmax, smax = (float(per[:, i].max()) for i in range(3))
+    achieved0 = float(per[0, 3]) / (per[0, 0] * 1e-3) / 1e9
+    flops = 2.0 * float(per[:, 4].sum()) * 64
+    return {
+        "what": CONFIG4,
+        "n_gpus": world, "algo": "C tile (k_spmm_ctile, column-sorted, LDS accumulators)",
+        "partition": "single GPU" if world == 1 else "whole-row blocks of A by nnz, B replicated, C all-gathered",
+        "kernel_ms_max": round(kmax, 5), "exchange_ms_max": round(xmax, 5), "step_ms": round(smax, 5),
+        "gflops": round(flops / (smax * 1e-3) / 1e9, 3),
+        "kernel_only_gflops": round(flops / (kmax * 1e-3) / 1e9, 3),
+        "algorithmic_bytes_per_rank": [int(b) for b in per[:, 3]],
+        "algorithmic_bytes_formula": "12*nnz + 4*(m+1) + 8*k*ncols + 16*m*ncols (SURVEY M1-bytes-SpMM)",
+        "roofline": {"bound": "hbm", "achieved": round(achieved0, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved0 / HBM_PEAK_GBS, 4), "traffic": traffic},
+        "kernel_ms_per_rank": [round(float(v), 5) for v in per[:, 0]],
+        "nnz_per_rank": [int(v) for v in per[:, 4]],
+        "first_call_s": round(first_s, 3), "host_gen_s": round(gen_s, 2),
+        "timing": ("cold steps (1 GiB read sweep before each, barrier, device-side hold), HIP events on the "
+                   "launch stream around the kernel and the C all-gather, max over ranks"),
+        "check": check,
+    }
+
+
+def config5_leg(args, torch, sblas, rank, world, evict, sync_barrier):
+    """configs[4] on every line: the sync-free SpTRSV.
+    Rank 0 solves the integer known-answer system (x must equal x_ref
+    exactly) with (1) the single-device pull executor (algo 4 = AUTO ticket
+    order; sptrsv_syncfree_cuda.h:545-636's solve) and (2) configs[4]'s
+    4-block partition (sblas_trsv_mgpu: nnz-balanced blocks of the solve
+    order, block d on device d % visible, producers pushing x_i into later
+    blocks' fine-grained x), each timed cold (1 GiB sweep on every device it
+    uses before each solve).  The other ranks wait at the barrier."""
+    n, offd, band = 5_558_326, 5, 80_000
+    out = {"what": CONFIG5, "n": n}
+    if rank == 0:
+        t0 = time.perf_counter()
+        cp, ri, _ = sblas.gen_lower_banded(n, offd, band, 47)
+        nnz = len(ri)
+        cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
+        vi = np.random.default_rng(5).integers(1, 11, nnz).astype(np.float64)
+        vi[cp[:-1]] = 1.0  # unit diagonal
+        xref = np.floor(sblas.gen_vector(n, 48) * 10.0) + 1.0
+        bi = np.bincount(ri, weights=vi * xref[cols], minlength=n)  # integers < 2^53: exact
+        del cols
+        gen_s = time.perf_counter() - t0
+        dev = torch.device("cuda", torch.cuda.current_device())
+        stream = torch.cuda.Stream(device=dev)
+        dcp, dri, dv, db = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (cp, ri, vi, bi))
+        dx = torch.zeros(n, dtype=torch.float64, device=dev)
+        t0 = time.perf_counter()
+        T = sblas.DeviceTRSV(dev.index, n, nnz, dcp.data_ptr(), dri.data_ptr(), dv.data_ptr(), 0)
+        setup_s = time.perf_counter() - t0
+        levels, order = T.levels(), T.pick()
+        sp = stream.cuda_stream
+        with torch.cuda.stream(stream):
+            T.solve(4, db.data_ptr(), dx.data_ptr(), sp)  # warm-up
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(args.steps):
+            evict()
+            torch.cuda.synchronize()  # the sweep runs on another stream: finish it first
+            ms.append(_hold_events(torch, stream, lambda ev: (T.solve(4, db.data_ptr(), dx.data_ptr(), sp),
+                                                              ev[1].record(stream)))[0])
+        exact = bool(np.array_equal(dx.cpu().numpy(), xref))
+        T.close()
+        del dcp, dri, dv, db, dx
+        out.update(config5_single(nnz, levels, order, float(np.mean(ms)), exact, gen_s, setup_s))
+        # configs[4]'s 4-way partition
+        ndev = torch.cuda.device_count()
+        gpus = 4 if ndev >= 4 else 2 if ndev >= 2 else 1
+        t0 = time.perf_counter()
+        H = sblas.TrsvMgpu(cp, ri, vi, n, gpus, tasks=4 // gpus)
+        build_s = time.perf_counter() - t0
+        H.run(bi)  # warm-up
+        scr = [torch.zeros(args.scrub_gib << 30, dtype=torch.uint8, device=torch.device("cuda", d))
+               for d in range(1, gpus)]
+        mms, ok = [], True
+        for _ in range(args.steps):
+            evict()
+            torch.cuda.synchronize()
+            for sc in scr:
+                sc.sum(dtype=torch.int64)
+            for d in range(gpus):
+                torch.cuda.synchronize(d)
+            x, t4 = H.run(bi)
+            mms.append(t4)
+            ok = ok and bool(np.array_equal(x, xref))
+        H.close()
+        del scr
+        out["blocks4"] = config5_blocks(nnz, gpus, float(np.mean(mms)), ok, build_s)
+    sync_barrier()
+    return out
+
+
+def config5_single(nnz, levels, order, t, exact, gen_s, setup_s):
+    """configs[4]'s single-device figures, t in ms."""
+    n = 5_558_326
+    abytes = 12 * nnz + 4 * (n + 1) + 16 * n
+    ach = abytes / (t * 1e-3) / 1e9
+    return {
+        "nnz": nnz, "levels": levels,
+        "executor": "pull (CSR rows, NaN-sentinel x, ticketed waves), " +
+                    ("level-order tickets" if order == 3 else "natural-order tickets"),
+        "ms": round(t, 5), "gflops": round(2.0 * nnz / (t * 1e-3) / 1e9, 3),
+        "algorithmic_bytes": int(abytes),
+        "algorithmic_bytes_formula": "12*nnz + 4*(n+1) + 16*n (SURVEY M1-bytes-TRSV)",
+        "roofline": {"bound": "latency (level chain); hbm reported", "achieved": round(ach, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None},
+        "us_per_level": round(t * 1e3 / max(levels, 1), 3),
+        "check_exact_vs_xref": exact,
+        "timing": "cold steps (1 GiB sweep before each), device-side hold, HIP events on the launch stream",
+        "host_gen_s": round(gen_s, 2), "analyse_s": round(setup_s, 3),
+    }
+
+
+def config5_blocks(nnz, gpus, t4, ok, build_s):
+    """configs[4]'s 4-block partition figures (4 // gpus blocks per GPU), t4 in ms."""
+    return {
+        "blocks": 4, "gpus": gpus, "blocks_per_gpu": 4 // gpus, "ms": round(t4, 5), "gflops": round(2.0 * nnz / (t4 * 1e-3) / 1e9, 3),
+        "check_exact_vs_xref": ok, "build_s": round(build_s, 3),
+        "timing": ("cold steps; host wall clock from the first block's launch to the last device's "
+                   "synchronize (sblas_trsv_mgpu_run), b upload and x reset before, x download after"),
+        "note": ("blocks on distinct GPUs, x pushed over xGMI with system-scope stores" if gpus > 1 else
+                 "one GPU visible: the 4 blocks run concurrently on it (the peer-store protocol on local "
+                 "fine-grained memory)"),
+    }
+
+
+def _gather_rows(torch, dist, dev, row, world):
+    """Every rank's stats row (numpy), as a (world, len) array."""
+    if dist is None:
+        return np.asarray(row, np.float64)[None, :]
+    use_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(np.asarray(row, np.float64), device=dev if use_dev else "cpu")
+    parts = [t.clone() for _ in range(world)]
+    dist.all_gather(parts, t)
+    return np.stack([p.cpu().numpy() for p in parts])
 
 
 def _oracle_check(rowptr, col, val, x_h, y0, ys):
@@ -491,7 +868,7 @@ def run_ctx(args) -> int:
     for _ in range(args.warmup):
         ctx.spmv_ex(ALPHA, BETA)
     devs = sorted({d % ndev for d in range(N)})  # physical devices (wrapped in loopback)
-    scrubs = [torch.zeros(1 << 30, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
+    scrubs = [torch.zeros(args.scrub_gib << 30, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
 
     def sync_all():
         for d in devs:
@@ -544,6 +921,14 @@ def run_ctx(args) -> int:
     if not args.no_config3:
         config3 = ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us,
                               profiled=N == 1 and W.default)
+    config4 = config5 = None
+    if N == 1 and not args.ctx_loopback:  # one device: the same single-GPU legs as the torch driver
+        import sblas_dist
+        torch.cuda.set_device(0)
+        if not args.no_config4:
+            config4 = config4_leg(args, torch, sblas, sblas_dist, None, 0, 1, 0, evict, sync_all)
+        if not args.no_config5:
+            config5 = config5_leg(args, torch, sblas, 0, 1, evict, sync_all)
     del scrubs
     total_flops = 2.0 * nnz
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
@@ -596,7 +981,7 @@ def run_ctx(args) -> int:
                    "over devices" if args.cache == "cold"
                    else "warm: host wall clock over K back-to-back steps"),
         "cache": args.cache,
-        "scrub": args.scrub,
+        "scrub": f"{args.scrub} {args.scrub_gib} GiB",
         ("warm" if args.cache == "cold" else "cold"): (
             {"value": round(total_flops / (warm_el / args.steps) / 1e9, 3),
              "ms_per_step": round(warm_el / args.steps * 1e3, 5),
@@ -611,6 +996,11 @@ def run_ctx(args) -> int:
         out["check_vs_oracle"] = check
     if config3 is not None:
         out["config3"] = config3
+    if config4 is not None:
+        out["config4"] = config4
+    if config5 is not None:
+        out["config5"] = config5
+    out["traffic_source"] = dict(TRAFFIC_NOTES)
     if args.ctx_loopback:
         out["note"] = (f"loopback rehearsal: {N} context ranks on {ndev} GPU(s), collectives as "
                        "stream-ordered device copies (no RCCL); not a measurement")
@@ -662,6 +1052,8 @@ def main() -> int:
                     help="cold-cache eviction before each cold step: a 1 GiB read-only sweep "
                          "(default: leaves no dirty lines whose write-back the next step would "
                          "pay) or read+write (add_, round 1's method)")
+    ap.add_argument("--scrub-gib", type=int, default=1,
+                    help="size of the cold-cache sweep buffer in GiB (default 1: 4x the 256 MB Infinity Cache)")
     ap.add_argument("--no-rowsplit-beside", action="store_true",
                     help="skip the row-split kernel's figure reported beside the headline")
     ap.add_argument("--overlap", nargs="?", type=int, const=2, default=0, metavar="K",
@@ -669,10 +1061,11 @@ def main() -> int:
                          "and all-gather part p while the kernel runs part p+1 (ctx driver: "
                          "sblas_ctx_matrix_upload_parts, any K; torch driver: two halves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peak", action="store_true", help="skip the measured HBM probe ceiling (N = 1)")
     ap.add_argument("--dist-always", action="store_true",
                     help="join a process group even at WORLD_SIZE 1 (torchrun --nproc-per-node 1): "
                          "runs the N > 1 exchange and timing path, RCCL included, on one GPU")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--ctx-loopback", action="store_true",
                     help="rehearsal only: the ctx driver with its N ranks wrapped onto the visible "
                          "GPUs and the collectives done as stream-ordered device copies instead of "
@@ -685,8 +1078,16 @@ def main() -> int:
     ap.add_argument("--no-config3", action="store_true",
                     help="skip the BASELINE configs[2] leg (CSR5, nnz split, all-reduce of y) that every "
                          "line carries under `config3`")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="skip the BASELINE configs[3] leg (SpMM, rail4284-shaped x 64) every line carries")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the BASELINE configs[4] leg (sync-free SpTRSV, circuit5M-class) every line carries")
+    ap.add_argument("--no-check-legs", action="store_true",
+                    help="skip the config4 / config5 post-timing checks (every C entry under the fp64 bound; "
+                         "the SpTRSV known answer exactly)")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    args.check_legs = not args.no_check_legs
     if args.cpu_baseline_only:  # child of cpu_baseline(): host only, no torch, no GPU
         return cpu_baseline_child(args)
 
@@ -770,7 +1171,7 @@ def main() -> int:
         if ev is not None:
             ev[2].record(stream)  # after the collective and the device merge
 
-    scrub = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
+    scrub = torch.zeros(args.scrub_gib << 30, dtype=torch.uint8, device=dev)
 
     def evict():
         if args.scrub == "write":
@@ -894,27 +1295,13 @@ def main() -> int:
     if not args.no_config3:
         config3 = torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream,
                                 evict, sync_barrier)
+    config4 = config5 = None
+    if not args.no_config4:
+        config4 = config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier)
+    if not args.no_config5:
+        config5 = config5_leg(args, torch, sblas, rank, world, evict, sync_barrier)
     del scrub
-    copy_peak = None
-    if world == 1:
-        # a STREAM-copy peak measured on this box, reported
-        # beside the 8 TB/s spec (torch copy of 512 MiB -> 512 MiB: 1 GiB
-        # moved, past the 256 MB Infinity Cache; best of 5, stream events)
-        src = torch.ones(1 << 26, dtype=torch.float64, device=dev)
-        dst = torch.empty_like(src)
-        best = None
-        with torch.cuda.stream(stream):
-            dst.copy_(src)
-            for _ in range(5):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                dst.copy_(src)
-                e1.record(stream)
-                torch.cuda.synchronize()
-                t = e0.elapsed_time(e1)
-                best = t if best is None else min(best, t)
-        copy_peak = 2.0 * src.numel() * 8 / (best * 1e-3) / 1e9
-        del src, dst
+    peak = measured_peak(torch, sblas, dev, stream) if world == 1 and not args.no_peak else None
 
     check = None
     if args.check:
@@ -986,11 +1373,8 @@ def main() -> int:
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
             },
-            **({"measured_copy_peak": {
-                "GBps": round(copy_peak, 1),
-                "frac": round(achieved / copy_peak, 4),
-                "how": "torch copy 512 MiB -> 512 MiB on this GPU, best of 5 (SURVEY M1-roof)"}}
-               if copy_peak else {}),
+            **({"measured_peak": dict(peak, frac_of_read_peak=round(achieved / peak["read_GBps"], 4))}
+               if peak else {}),
             "kernel_ms": round(kern_ms, 5),
             "kernel_ms_max_over_ranks": round(kern_ms_max, 5),
             "kernel_only_gflops": round(total_flops / (kern_ms_max * 1e-3) / 1e9, 3),
@@ -1008,7 +1392,7 @@ def main() -> int:
                         "kernel to after exchange + merge, max over ranks; host wall clock beside")
                        if args.cache == "cold" else "warm: host wall clock over K back-to-back steps"),
             "cache": args.cache,
-            "scrub": args.scrub,
+            "scrub": f"{args.scrub} {args.scrub_gib} GiB",
             # cold steps are timed on the device (run_cold); the host wall
             # clock around each, barrier round trips included, for comparison
             "cold_host_wall_ms_per_step": round(cold_wall / args.steps * 1e3, 5),
@@ -1028,6 +1412,11 @@ def main() -> int:
             out["rowsplit_beside"] = rowsplit_beside
         if config3 is not None:
             out["config3"] = config3
+        if config4 is not None:
+            out["config4"] = config4
+        if config5 is not None:
+            out["config5"] = config5
+        out["traffic_source"] = dict(TRAFFIC_NOTES)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -461,6 +461,17 @@ int sblas_gen_rmat(int scale, int edge_factor, unsigned long long seed, long lon
 int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed,
                            int *colptr, int *rowidx, double *val);
 
+/* Measured memory ceiling (bench.py's `measured_peak`):
+ * hand-written HBM stream probes on the current device, enqueued on
+ * `stream`.  mode 0 = read `bytes` of src (16-B loads, 8 in flight per lane,
+ * grid-stride; dst = an 8-byte sink that is never written in practice),
+ * 1 = the same with non-temporal loads, 2 = copy src -> dst, 3 / 4 = modes
+ * 0 / 1 with each workgroup streaming one contiguous span.  `bytes` a multiple of 16;
+ * wg_per_cu 256-thread workgroups per CU (1..32).  Not part of the reference
+ * API: the probes price the SpMV kernels against what this GPU streams. */
+int sblas_hbm_probe(int mode, const void *src, void *dst, long long bytes, int wg_per_cu,
+                    void *stream);
+
 #ifdef __cplusplus
 }
 #endif

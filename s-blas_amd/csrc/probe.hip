@@ -1,0 +1,105 @@
+// probe.hip -- hand-written HBM stream probes (read, non-temporal read, copy)
+// that give bench.py a measured memory ceiling beside the 8 TB/s spec
+// (a torch copy is not a ceiling).
+//
+// Each lane moves 16 B per access (global_load_dwordx4), kUnroll accesses in
+// flight per lane before any is consumed, a grid-stride loop over a buffer
+// far larger than the 256 MB Infinity Cache, `wg_per_cu` 256-thread
+// workgroups per CU.  The read probes fold what they load into one xor per
+// lane and store it only when it equals a value no fill produces (so the
+// loads cannot be dropped and nothing is written).
+#include <algorithm>
+
+#include "sblas_internal.hpp"
+
+namespace {
+
+constexpr int kProbeThreads = 256;
+constexpr int kUnroll = 8;
+
+template <bool kNt>
+__device__ __forceinline__ ulonglong2 probe_ld(const ulonglong2 *p)
+{
+    if constexpr (kNt) {
+        ulonglong2 v;
+        v.x = __builtin_nontemporal_load(&p->x);
+        v.y = __builtin_nontemporal_load(&p->y);
+        return v;
+    } else {
+        return *p;
+    }
+}
+
+// kBlocked = false: grid-stride (every pass of the grid covers one
+// contiguous 4 KiB x grid window); true: workgroup b streams its own
+// contiguous span [b * span, (b + 1) * span) (how the SpMV kernels read their
+// chunk streams: long runs per wave, few DRAM pages open per CU).
+template <bool kNt, bool kBlocked>
+__global__ __launch_bounds__(kProbeThreads) void k_probe_read(const ulonglong2 *__restrict__ src, long long n16,
+                                                              unsigned long long *__restrict__ sink)
+{
+    long long i, end, stride;
+    if constexpr (kBlocked) {
+        const long long span = (n16 + gridDim.x - 1) / gridDim.x;
+        i = (long long)blockIdx.x * span + threadIdx.x;
+        end = std::min(n16, (long long)(blockIdx.x + 1) * span);
+        stride = kProbeThreads;
+    } else {
+        i = (long long)blockIdx.x * kProbeThreads + threadIdx.x;
+        end = n16;
+        stride = (long long)gridDim.x * kProbeThreads;
+    }
+    unsigned long long acc = 0;
+    for (; i + (kUnroll - 1) * stride < end; i += kUnroll * stride) {
+        ulonglong2 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) v[u] = probe_ld<kNt>(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) acc ^= v[u].x ^ v[u].y;
+    }
+    for (; i < end; i += stride) {
+        const ulonglong2 v = probe_ld<kNt>(src + i);
+        acc ^= v.x ^ v.y;
+    }
+    if (acc == 0x5bd1e9955bd1e995ULL) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(kProbeThreads) void k_probe_copy(const ulonglong2 *__restrict__ src, long long n16,
+                                                              ulonglong2 *__restrict__ dst)
+{
+    const long long stride = (long long)gridDim.x * kProbeThreads;
+    long long i = (long long)blockIdx.x * kProbeThreads + threadIdx.x;
+    for (; i + (kUnroll - 1) * stride < n16; i += kUnroll * stride) {
+        ulonglong2 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) dst[i + u * stride] = v[u];
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+}  // namespace
+
+extern "C" int sblas_hbm_probe(int mode, const void *src, void *dst, long long bytes, int wg_per_cu, void *stream)
+{
+    if (mode < 0 || mode > 4 || !src || bytes < 16 || (bytes & 15) || wg_per_cu < 1 || wg_per_cu > 32)
+        return SBLAS_ERR_INVALID;
+    if (!dst) return SBLAS_ERR_INVALID;  // read probes: dst = an 8-B sink
+    int dev = 0, cus = 0;
+    SBLAS_HIP(hipGetDevice(&dev));
+    SBLAS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const long long n16 = bytes / 16;
+    const unsigned grid = (unsigned)std::max(1LL, std::min<long long>((long long)cus * wg_per_cu,
+                                                                     (n16 + kProbeThreads - 1) / kProbeThreads));
+    hipStream_t s = (hipStream_t)stream;
+    const auto *sp = (const ulonglong2 *)src;
+    auto *sink = (unsigned long long *)dst;
+    if (mode == 0) hipLaunchKernelGGL((k_probe_read<false, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 1) hipLaunchKernelGGL((k_probe_read<true, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 3) hipLaunchKernelGGL((k_probe_read<false, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 4) hipLaunchKernelGGL((k_probe_read<true, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else hipLaunchKernelGGL(k_probe_copy, dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, (ulonglong2 *)dst);
+    SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}

@@ -81,6 +81,7 @@ _sig("sblas_csr_analyse", _i, _p, _i, _p)
 _sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
 _sig("sblas_spmv_timed", _i, _p, _i, C.c_double, _p, C.c_double, _p, _p, _p)
 _sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
+_sig("sblas_hbm_probe", _i, _i, _p, _p, _ll, _i, _p)
 _sig("sblas_csr_plan_bytes", _ll, _p, _i)
 _sig("sblas_csr_pick", _i, _p, _p, _p)
 _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
@@ -402,6 +403,12 @@ def csr2csc_mgpu(m: int, n: int, rowptr, col, val, ngpu: int):
     check(lib.sblas_csr2csc_mgpu(m, n, nnz, ngpu, ptr(rp), ptr(ci), ptr(v), ptr(cp), ptr(ri),
                                  ptr(cv), C.byref(t1), C.byref(t2)), "csr2csc_mgpu")
     return cp, ri[:nnz], cv[:nnz], t1.value, t2.value
+
+
+def hbm_probe(mode: int, src_ptr: int, dst_ptr: int, nbytes: int, wg_per_cu: int = 8, stream=None) -> None:
+    """Enqueue one HBM stream probe (sblas_hbm_probe): 0 read, 1 non-temporal
+    read, 2 copy."""
+    check(lib.sblas_hbm_probe(mode, src_ptr, dst_ptr, nbytes, wg_per_cu, stream), "hbm_probe")
 
 
 def gen_vector(n: int, seed: int) -> np.ndarray:

@@ -4,7 +4,12 @@
 Usage:
   pmc_traffic.py --kernel k_spmv_rowsplit --out profiles/pmc_rowsplit.json \
       --fetch <dir of the FETCH_SIZE pass> --write <dir of the WRITE_SIZE pass> \
-      [--l2 <dir of the TCC_HIT_sum/TCC_MISS_sum pass>] [--algorithmic BYTES]
+      [--l2 <dir of the TCC_HIT_sum/TCC_MISS_sum pass>] [--algorithmic BYTES] \
+      [--lib s-blas_amd/libsblas.so]
+
+The summary is stamped with the sha256 of the libsblas.so the passes ran
+(`lib_sha256`): bench.py reports `roofline.traffic` from it only while the
+loaded library has the same hash, and null (with the reason) otherwise.
 
 Corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
   * FETCH_SIZE and WRITE_SIZE are in KiB;
@@ -18,6 +23,7 @@ one TCC pass together).
 """
 import argparse
 import csv
+import hashlib
 import glob
 import json
 import os
@@ -57,6 +63,14 @@ def counter_values(d, kernel, name):
     return [sum(total)]
 
 
+def file_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", required=True)
@@ -65,6 +79,9 @@ def main():
     ap.add_argument("--l2")
     ap.add_argument("--algorithmic", type=float)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "libsblas.so"),
+                    help="the library the counter passes ran (its sha256 stamps the summary)")
     a = ap.parse_args()
     f = counter_values(a.fetch, a.kernel, "FETCH_SIZE")
     w = counter_values(a.write, a.kernel, "WRITE_SIZE")
@@ -83,6 +100,7 @@ def main():
         "write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
         "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024",
+        "lib_sha256": file_sha256(a.lib),
     }
     if a.algorithmic:
         out["algorithmic_bytes_per_launch"] = a.algorithmic

@@ -99,3 +99,49 @@ def test_config3_is_on_by_default():
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert src.count('out["config3"] = config3') == 2
     assert src.count("if not args.no_config3:") == 2
+
+
+def test_config4_config5_object_keys():
+    """Every bench line carries BASELINE configs[3] (SpMM) and configs[4]
+    (SpTRSV) under `config4` / `config5`: the objects
+    both drivers attach, built from per-rank stats rows."""
+    per = [[0.36, 0.0, 0.36, 699e6, 11_279_748]]
+    c4 = bench.config4_object(1, per, 1.5, 0.7, {"pass": True, "entries": 4284 * 64}, None)
+    for k in ("kernel_ms_max", "exchange_ms_max", "step_ms", "gflops", "kernel_only_gflops", "roofline",
+              "algorithmic_bytes_per_rank", "kernel_ms_per_rank", "nnz_per_rank", "check", "timing", "what"):
+        assert k in c4, k
+    assert abs(c4["gflops"] - 2 * 11_279_748 * 64 / 0.36e-3 / 1e9) < 1e-3
+    assert abs(c4["roofline"]["achieved"] - 699e6 / 0.36e-3 / 1e9) < 0.1
+    per8 = [[0.05 + 0.001 * r, 0.02, 0.07 + 0.001 * r, 90e6, 11_279_748 // 8] for r in range(8)]
+    c48 = bench.config4_object(8, per8, 1.0, 0.7, None, None)
+    assert c48["n_gpus"] == 8 and c48["kernel_ms_max"] == 0.057 and len(c48["kernel_ms_per_rank"]) == 8
+    c5 = bench.config5_single(33_350_000, 985, 1, 2.45, True, 1.0, 0.5)
+    for k in ("ms", "gflops", "algorithmic_bytes", "roofline", "levels", "check_exact_vs_xref", "us_per_level",
+              "executor", "timing"):
+        assert k in c5, k
+    assert c5["algorithmic_bytes"] == 12 * 33_350_000 + 4 * (5_558_326 + 1) + 16 * 5_558_326
+    b4 = bench.config5_blocks(33_350_000, 1, 2.6, True, 2.0)
+    assert b4["blocks"] == 4 and b4["blocks_per_gpu"] == 4 and b4["check_exact_vs_xref"]
+
+
+def test_config4_config5_on_by_default():
+    """Both drivers add the configs[3] / configs[4] legs unless switched off."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('out["config4"] = config4') == 2 and src.count('out["config5"] = config5') == 2
+    assert src.count("if not args.no_config4:") == 2 and src.count("if not args.no_config5:") == 2
+
+
+def test_traffic_requires_matching_library_hash(tmp_path, monkeypatch):
+    """roofline.traffic comes from a committed PMC summary only while its
+    lib_sha256 stamp equals the loaded libsblas.so's hash."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    (prof / "pmc_x.json").write_text(json.dumps({"hbm_bytes_per_launch": 7.0e8, "lib_sha256": bench.lib_sha256()}))
+    assert bench._stamped_traffic("x") == 7.0e8
+    (prof / "pmc_y.json").write_text(json.dumps({"hbm_bytes_per_launch": 7.0e8, "lib_sha256": "0" * 64}))
+    assert bench._stamped_traffic("y") is None and "not reported" in bench.TRAFFIC_NOTES["y"]
+    (prof / "pmc_z.json").write_text(json.dumps({"hbm_bytes_per_launch": 7.0e8}))
+    assert bench._stamped_traffic("z") is None
+    assert bench._stamped_traffic("absent") is None
