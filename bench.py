@@ -428,14 +428,28 @@ def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, chec
     return out
 
 
-def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us, profiled=False):
+ROW_COST = 6.0  # the cost-weighted split's per-row weight (ctx.hip kCtxRowCost)
+
+
+def cost_weighted(c3):
+    """The compact record of the cost-weighted partition's config3 leg."""
+    keep = ("kernel_ms_max", "exchange_ms_max", "step_ms", "gflops", "kernel_only_gflops", "kernel_ms_per_device",
+            "nnz_per_device", "check")
+    out = {k: c3[k] for k in keep if k in c3}
+    out["partition"] = (f"cost-weighted whole rows: contiguous ranges balancing sum(nnz_r + {ROW_COST:g}) "
+                        "(sblas_partition_cost), no split rows, same all-reduce of the zero-padded y")
+    return out
+
+
+def ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us, profiled=False, partition=1):
     """configs[2] through the C-ABI context: the matrix re-uploaded as CSR5
-    slices of the nnz split with the SBLAS_CTX_ALLREDUCE exchange, timed with
-    the default leg's cold protocol (scrub, device-side hold, aligning
-    all-reduce, per-device spans), then one fresh step checked against the
-    oracle (--check) with every device's y bit-identical."""
+    slices of the nnz split (partition 2: the cost-weighted whole-row split)
+    with the SBLAS_CTX_ALLREDUCE exchange, timed with the default leg's cold
+    protocol (scrub, device-side hold, aligning all-reduce, per-device
+    spans), then one fresh step checked against the oracle (--check) with
+    every device's y bit-identical."""
     N = ctx.ngpu
-    ctx.upload(n, n, rowptr, col, val, sblas.CSR5, 1, sblas.CTX_ALLREDUCE)
+    ctx.upload(n, n, rowptr, col, val, sblas.CSR5, partition, sblas.CTX_ALLREDUCE)
     ctx.set_x(x_h)
     ctx.set_y(np.zeros(n))
     info = [ctx.slice_info(d) for d in range(N)]
@@ -713,7 +727,7 @@ def _oracle_check(rowptr, col, val, x_h, y0, ys):
 
 
 def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream, evict,
-                  sync_barrier):
+                  sync_barrier, row_cost=None):
     """configs[2] under the launcher (one process per GPU): the nnz split's
     slice as a CSR5 handle (sblas_dist.DistSpMV, exchange "allreduce" =
     torch.distributed.all_reduce = ncclAllReduce of the zero-padded y), timed
@@ -721,7 +735,7 @@ def torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx,
     hold, HIP events on the launch stream around kernel and exchange, max
     over ranks.  At world 1 the span is sblas_spmv_timed's (no exchange)."""
     n, rowptr = W.n, W.rowptr
-    plan = sblas_dist.make_plan(rowptr, n, world)
+    plan = sblas_dist.make_plan(rowptr, n, world, row_cost=row_cost)
     r0, r1, i0, i1, _ = plan.local(rank)
     col_rows, val_rows = W.rows(r0, r1)
     off = i0 - int(rowptr[r0])
@@ -921,6 +935,9 @@ def run_ctx(args) -> int:
     if not args.no_config3:
         config3 = ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict, delay_us,
                               profiled=N == 1 and W.default)
+        if N > 1:  # beside the literal nnz split: the cost-weighted whole-row split
+            config3["cost_weighted"] = cost_weighted(ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict,
+                                                                 delay_us, partition=2))
     config4 = config5 = None
     if N == 1 and not args.ctx_loopback:  # one device: the same single-GPU legs as the torch driver
         import sblas_dist
@@ -1295,6 +1312,10 @@ def main() -> int:
     if not args.no_config3:
         config3 = torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream,
                                 evict, sync_barrier)
+        if world > 1:  # beside the literal nnz split: the cost-weighted whole-row split
+            config3["cost_weighted"] = cost_weighted(torch_config3(
+                args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream, evict, sync_barrier,
+                row_cost=ROW_COST))
     config4 = config5 = None
     if not args.no_config4:
         config4 = config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier)

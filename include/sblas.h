@@ -335,12 +335,13 @@ int sblas_ctx_ngpu(sblas_ctx ctx, int *ngpu);
 /* HOST CSR (int64 rowptr) distributed over the devices and analysed for
  * `algo` (sblas_spmv_algo).  partition 0 = cyclic row chunks (chunk j of
  * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
- * nnz-balanced split with split rows merged on the device.  Exchange
- * SBLAS_CTX_ALLGATHER. */
+ * nnz-balanced split with split rows merged on the device, 2 = the
+ * cost-weighted whole-row split (sblas_partition_cost, w =
+ * SBLAS_CTX_ROW_COST, 6 by default).  Exchange SBLAS_CTX_ALLGATHER. */
 int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr,
                             const int *col, const double *val, int algo, int partition);
 /* Same with the exchange chosen (sblas_ctx_exchange); SBLAS_CTX_ALLREDUCE
- * needs partition 1 (SBLAS_ERR_INVALID otherwise). */
+ * needs a contiguous-range partition, 1 or 2 (SBLAS_ERR_INVALID otherwise). */
 int sblas_ctx_matrix_upload_ex(sblas_ctx ctx, int m, int n, const long long *rowptr,
                                const int *col, const double *val, int algo, int partition,
                                int exchange);
@@ -433,6 +434,12 @@ int sblas_coo_sortbyrow(int m, long long nnz, int *row, int *col, double *val, i
 int sblas_partition_nnz(int m, long long nnz, const long long *rowptr, int g,
                         long long *start_idx, long long *end_idx,
                         int *start_row, int *end_row, int *start_flag);
+/* Cost-weighted whole-row split: contiguous row ranges balancing
+ * sum_r (nnz_r + w), no split rows (start_flag all 0); same outputs as
+ * sblas_partition_nnz.  w = 0 balances entries with rows kept whole. */
+int sblas_partition_cost(int m, const long long *rowptr, int g, double w,
+                         long long *start_idx, long long *end_idx,
+                         int *start_row, int *end_row, int *start_flag);
 /* row-block partition (dspmv_mgpu_baseline.cu:64-65); g+1 entries. */
 int sblas_partition_rowblock(int m, int g, int *row_start);
 
@@ -471,6 +478,10 @@ int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed,
  * API: the probes price the SpMV kernels against what this GPU streams. */
 int sblas_hbm_probe(int mode, const void *src, void *dst, long long bytes, int wg_per_cu,
                     void *stream);
+/* The same, waiting for it and returning its device span in *ms (events the
+ * runtime stamps at the kernel's start and end, as sblas_spmv_timed). */
+int sblas_hbm_probe_timed(int mode, const void *src, void *dst, long long bytes, int wg_per_cu,
+                          void *stream, float *ms);
 
 #ifdef __cplusplus
 }

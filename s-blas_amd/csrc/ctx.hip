@@ -77,6 +77,12 @@ struct sblas_ctx_s {
     std::vector<std::pair<int, int>> peers;
 };
 
+// Per-row weight of the cost-weighted partition (2): a row end costs the
+// CSR5 segmented-sum kernel about 6 entries' time -- config 2's N = 8 slices
+// at equal nnz: 552k light rows 55 us, 52k heavy rows 35.5 us
+// (profiles/r04/c5P/), i.e. ~6.73 us per M entries + ~39 us per M rows.
+constexpr double kCtxRowCost = 6.0;
+
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
 // context's size runs on it (device-resident slices for the call, x
 // broadcast, kernels, ncclAllGather, device merge) instead of the per-device
@@ -560,11 +566,11 @@ int sblas_ctx_ngpu(sblas_ctx C, int *ngpu)
 int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowptr, const int *col,
                                const double *val, int algo, int partition, int exchange)
 {
-    if (!C || m < 0 || n < 0 || !rowptr || (partition != 0 && partition != 1)) return SBLAS_ERR_INVALID;
+    if (!C || m < 0 || n < 0 || !rowptr || partition < 0 || partition > 2) return SBLAS_ERR_INVALID;
     if (algo < SBLAS_SPMV_AUTO || algo > SBLAS_SPMV_XSORT) return SBLAS_ERR_INVALID;
     if (exchange != SBLAS_CTX_ALLGATHER && exchange != SBLAS_CTX_ALLREDUCE) return SBLAS_ERR_INVALID;
-    if (exchange == SBLAS_CTX_ALLREDUCE && partition != 1) {
-        set_error("sblas_ctx_matrix_upload: the allreduce exchange needs the nnz partition (1): each "
+    if (exchange == SBLAS_CTX_ALLREDUCE && partition == 0) {
+        set_error("sblas_ctx_matrix_upload: the allreduce exchange needs a contiguous-range partition (1 or 2): each "
                   "device's rows must be one contiguous range of the zero-padded y");
         return SBLAS_ERR_INVALID;
     }
@@ -592,8 +598,14 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
     if (partition == 0) {
         SBLAS_TRY(sblas_cyclic_plan(m, g, 8, &C->chunk_rows, &C->stride));
     } else {
-        SBLAS_TRY(sblas_partition_nnz(m, C->nnz, rowptr, g, si.data(), ei.data(), sr.data(), er.data(),
-                                      sf.data()));
+        if (partition == 1) {
+            SBLAS_TRY(sblas_partition_nnz(m, C->nnz, rowptr, g, si.data(), ei.data(), sr.data(), er.data(),
+                                          sf.data()));
+        } else {  // cost-weighted whole rows: per-row weight SBLAS_CTX_ROW_COST (default 6)
+            const char *we = getenv("SBLAS_CTX_ROW_COST");
+            SBLAS_TRY(sblas_partition_cost(m, rowptr, g, we ? atof(we) : kCtxRowCost, si.data(), ei.data(),
+                                           sr.data(), er.data(), sf.data()));
+        }
         C->h_meta.assign((size_t)3 * g, 0);
         long long mx = 1;
         for (int d = 0; d < g; ++d) {
@@ -660,7 +672,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
         if (e == hipSuccess) e = hipMalloc(&C->bar[d], sizeof(double));
         if (e == hipSuccess) e = hipMemsetAsync(C->bar[d], 0, sizeof(double), C->st[d]);
         if (e == hipSuccess) e = hipMemsetAsync(C->ylocal[d], 0, sizeof(double) * C->ylen, C->st[d]);
-        if (e == hipSuccess && partition == 1) {
+        if (e == hipSuccess && partition != 0) {
             e = hipMalloc(&C->meta[d], sizeof(int) * 3 * g);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(C->meta[d], C->h_meta.data(), sizeof(int) * 3 * g, hipMemcpyHostToDevice,

@@ -573,6 +573,41 @@ int sblas_partition_nnz(int m, long long nnz, const long long *rowptr, int g,
     return SBLAS_OK;
 }
 
+// Cost-weighted row split: contiguous WHOLE-row ranges
+// whose cost sum_r (nnz_r + w) is balanced, so a rank of short rows gets
+// fewer entries than one of long rows (a row-end costs a segmented-sum kernel
+// about w entries' time).  Same outputs as sblas_partition_nnz with every
+// start_flag 0 (no row is split, no carries); an empty range has end_row =
+// start_row - 1 and end_idx = start_idx - 1.
+int sblas_partition_cost(int m, const long long *rowptr, int g, double w, long long *start_idx,
+                         long long *end_idx, int *start_row, int *end_row, int *start_flag)
+{
+    if (g <= 0 || m < 0 || !rowptr || !(w >= 0.0)) return SBLAS_ERR_INVALID;
+    auto cost = [&](long long r) { return (double)rowptr[r] + w * (double)r; };
+    const double total = cost(m);
+    for (int d = 0; d < g; ++d) {
+        int r0 = 0;
+        if (d > 0) {  // first row whose cost prefix reaches d/g of the total
+            const double target = total * d / g;
+            long long lo = 0, hi = m;
+            while (lo < hi) {
+                const long long mid = (lo + hi) / 2;
+                if (cost(mid) >= target) hi = mid;
+                else lo = mid + 1;
+            }
+            r0 = (int)std::max<long long>(lo, start_row[d - 1]);
+        }
+        start_row[d] = r0;
+        start_flag[d] = 0;
+    }
+    for (int d = 0; d < g; ++d) {
+        end_row[d] = d == g - 1 ? m - 1 : start_row[d + 1] - 1;
+        start_idx[d] = rowptr[start_row[d]];
+        end_idx[d] = rowptr[end_row[d] + 1] - 1;
+    }
+    return SBLAS_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic generator (DESIGN.md "Synthetic"): per-row SplitMix64 stream,
 // state = seed ^ (row+1)*0x9E3779B97F4A7C15; columns by 128-bit

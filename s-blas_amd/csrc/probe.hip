@@ -95,11 +95,48 @@ extern "C" int sblas_hbm_probe(int mode, const void *src, void *dst, long long b
     hipStream_t s = (hipStream_t)stream;
     const auto *sp = (const ulonglong2 *)src;
     auto *sink = (unsigned long long *)dst;
-    if (mode == 0) hipLaunchKernelGGL((k_probe_read<false, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
-    else if (mode == 1) hipLaunchKernelGGL((k_probe_read<true, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
-    else if (mode == 3) hipLaunchKernelGGL((k_probe_read<false, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
-    else if (mode == 4) hipLaunchKernelGGL((k_probe_read<true, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
-    else hipLaunchKernelGGL(k_probe_copy, dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, (ulonglong2 *)dst);
+    if (mode == 0) SBLAS_LAUNCH((k_probe_read<false, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 1) SBLAS_LAUNCH((k_probe_read<true, false>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 3) SBLAS_LAUNCH((k_probe_read<false, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else if (mode == 4) SBLAS_LAUNCH((k_probe_read<true, true>), dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, sink);
+    else SBLAS_LAUNCH(k_probe_copy, dim3(grid), dim3(kProbeThreads), 0, s, sp, n16, (ulonglong2 *)dst);
     SBLAS_HIP(hipGetLastError());
+    return SBLAS_OK;
+}
+
+// The probe's device span as sblas_spmv_timed measures a SpMV call: events
+// the runtime stamps at the kernel's start and end (no dispatch gap), so a
+// streaming floor and a kernel are timed alike.
+extern "C" int sblas_hbm_probe_timed(int mode, const void *src, void *dst, long long bytes, int wg_per_cu,
+                                     void *stream, float *ms)
+{
+    if (!ms) return SBLAS_ERR_INVALID;
+    *ms = 0.0f;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    SBLAS_HIP(hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        sblas::set_error("sblas_hbm_probe_timed: hipEventCreate failed");
+        return SBLAS_ERR_HIP;
+    }
+    sblas::LaunchTimer &lt = sblas::launch_timer();
+    lt.start = e0;
+    lt.stop = e1;
+    lt.pending_start = true;
+    const int rc = sblas_hbm_probe(mode, src, dst, bytes, wg_per_cu, stream);
+    const bool launched = !lt.pending_start;
+    lt = sblas::LaunchTimer{};
+    hipError_t e = hipSuccess;
+    if (rc == SBLAS_OK && launched) {
+        e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc != SBLAS_OK) return rc;
+    if (e != hipSuccess) {
+        sblas::set_error("sblas_hbm_probe_timed: %s", hipGetErrorString(e));
+        return SBLAS_ERR_HIP;
+    }
     return SBLAS_OK;
 }

@@ -90,6 +90,7 @@ struct Csr5Plan {
     int *head_run = nullptr;       // [ntiles] > 0: tile t starts a run of that many tiles whose heads
                                    // continue one row (calibrated together), else 0
     bool ready = false;
+    int form = 2;                  // tile form (SBLAS_C5_PF, read at plan build; spmv.hip c5_form_env)
     // XCD-affine form (spmv.hip "CSR5 over column panels"): one tile plan per
     // column panel of the panel plan, panel p's tiles dealt to the XCDs with
     // blockIdx % P == p, alpha-scaled partial y per panel, then a reduce.
@@ -162,15 +163,7 @@ struct SpmmPlan {
     int nsparse = 0;           // rows handled by the row-wave kernel
     long long sparse_nnz = 0;  // their nonzeros
     int *srows = nullptr;
-    // L2-slice form (few rows, tall B): A cut into S slices of W columns (W
-    // rows of B, <= 1 MiB per 64-column slab), slice-major CSR; slices dealt
-    // to XCDs by index (blockIdx % 8), partial C per XCD, then reduced.
-    int l2_S = 0, l2_W = 0;
-    int *l2_rp = nullptr;                // [S][m+1] offsets into l2_col/l2_val
-    unsigned short *l2_col = nullptr;    // column - s*W
-    double *l2_val = nullptr;
-    double *l2_part = nullptr;           // [8][m][64]
-    // Column-sorted C-tile form (default where the L2-slice form applies):
+    // Column-sorted C-tile form (few rows, tall B; spmm.hip build_spmm_plan):
     // columns of A cut into slabs of 2^ct_wlog columns, slab s owned by XCD
     // s % 8 and its slabs split into ct_ns contiguous sets; rows into ct_nrb
     // blocks of ct_R.  Entries of (XCD, set, row block) sorted by (column,
@@ -185,17 +178,6 @@ struct SpmmPlan {
     unsigned *ct_key = nullptr;
     double *ct_val = nullptr;
     long long *ct_off = nullptr;         // [8*ns*nrb + 1] entry offsets
-    bool ct_own = false;                 // rows owned by waves, plain LDS read-add-write
-    long long *ct_woff = nullptr;        // own: [8*ns*nrb][17] per-wave entry offsets
-    // Tall-tile form (spmm.hip "tall tile"): C tile = all m rows x 4 columns
-    // in LDS; A's entries as column-run pieces grouped 16 at a time.
-    bool tt = false;
-    int tt_nlist = 0;                    // lists = 8 XCDs x 2 halves
-    int2 *tt_gdesc = nullptr;            // per group {first slot, slots per piece column L}
-    unsigned *tt_gcol = nullptr;         // per group 16 x (column | piece length << 24)
-    unsigned *tt_key = nullptr;          // per slot: row
-    double *tt_val = nullptr;            // per slot: value
-    int *tt_loff = nullptr;              // [nlist + 1] group offsets of the lists
     double fill_thresh = 0.08;  // MFMA tile when a 16-row block fills >= 8% of its column union
     bool ready = false;
 };
@@ -229,10 +211,7 @@ struct XsArgs {
     int *qreset;            // the other parity's heads, re-armed to qstat by block 0
     int qstat[8];           // items per queue taken statically (block b: queue b%8, index b/8)
     int dynamic;            // items beyond the static share exist (claims needed)
-    int sc1part;            // experiments: agent-scope partial stores without the fused reduce
-    int ntstore;            // y and partials written with non-temporal (streaming) stores
     int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
-    int tail;               // wide ranges reduced by their last-arriving sub-item (xs_tail_reduce)
     int nrtasks;
     const int2 *rtasks;     // (range, first row) reduce tasks
     unsigned *arrive;       // per wide range: sub-items counted in, cumulative
@@ -242,7 +221,7 @@ struct XsArgs {
     int qstride;
     int G, q, Wg;
     int use_xcc;
-    int kstride, vstride;   // chunk strides in 16-B units (keys, values); K24: the chunk size
+    int kstride, vstride;   // chunk strides in 16-B units (keys, values)
     long long *trace;       // debugging aid (SBLAS_XS_TRACE), else null
 };
 
@@ -256,7 +235,6 @@ struct XsPlan {
     uint32_t *key = nullptr;     // owns the chunk storage (keys and values)
     double *val = nullptr;       // values inside it (interleaved per chunk by default)
     int kstride = 64, vstride = 128;
-    bool k24 = false;            // 24-bit keys, 320-entry chunks (xsort.hip "K24 chunks")
     int *qitems = nullptr;
     long long *xrec = nullptr;   // item records (see XsArgs)
     int *qhead = nullptr;        // [2][16]: claim heads per launch parity
@@ -266,7 +244,6 @@ struct XsPlan {
     int qstat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int dynamic = 0;
     bool fused = false;          // in-kernel reduce of the wide ranges
-    bool tail = false;           // last-arriver reduce of the wide ranges (no reduce launch)
     int nrtasks = 0;
     int2 *rtasks = nullptr;
     unsigned *arrive = nullptr;
@@ -278,7 +255,6 @@ struct XsPlan {
     bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
     bool solo = false;           // narrow ranges are items of their own (16,384 LDS rows)
     int u = 1;                   // chunks per dynamic claim (planner; SBLAS_XS_U)
-    bool batch = false;          // small static items: k_spmv_xsort_batch (xsort.hip)
     int maxc = 0;                // most chunks of one item (both sub-items)
     bool ready = false;
 };
@@ -292,6 +268,7 @@ struct RsPlan {
     int nslots = 0;
     bool ready = false;
     bool panels = false;           // run as the panel plan (XCD column panels, spmv.hip xcd_panels_pay)
+    bool seq = true;               // consecutive entries per thread (SBLAS_RS_SEQ=0: vec4 order), read at build
 };
 
 }  // namespace sblas

@@ -202,149 +202,6 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(
     }
 }
 
-// ---- L2-slice SpMM (few rows, tall B) -------------------------------------
-// With m small (rail4284: 4,284 rows) and B far larger than the chip's 32 MB
-// of L2 (559 MB), every nonzero's 512-B B row comes over the fabric: the
-// row kernels run at the ~7-8.6 TB/s random-row gather rate.  Here A is cut
-// into slices of W columns (W rows of B, 1 MiB at n = 64) and slice s is
-// worked only by the workgroups with blockIdx % 8 == s % 8, i.e. one XCD
-// under round-robin placement: each B slice is fetched into ONE L2 and
-// re-read there by all of that XCD's waves, which walk the slices in step.
-// Every XCD covers all m rows (each wave owns RW consecutive rows, partial
-// sums in LDS, a register run per row); the 8 XCD partials are reduced after.
-constexpr int kL2Xcd = 8;
-constexpr int kL2WgPerXcd = 128;  // 4 workgroups per CU: all resident at 106 VGPRs
-constexpr int kL2MaxRows = 32;    // rows per wave (LDS: 4 waves x RW x 64 f64)
-constexpr int kL2Batch = 16;      // B-row gathers in flight per lane
-
-__global__ __launch_bounds__(256) void k_spmm_l2slice(
-    const int *__restrict__ srp, const unsigned short *__restrict__ scol,
-    const double *__restrict__ sval, int S, int W, int m, int RW,
-    const double *__restrict__ B, long long ldb, int n, int slab, double *__restrict__ part)
-{
-    extern __shared__ double l2acc[];  // [4][RW][64]
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    double *acc = l2acc + (size_t)wv * RW * 64 + lane;  // acc[i * 64] = row i
-    const int xcd = blockIdx.x % kL2Xcd, wgx = blockIdx.x / kL2Xcd;
-    const int gw = wgx * 4 + wv;
-    const int rb = gw * RW, nr = min(m, rb + RW) - rb;
-    for (int i = 0; i < RW; ++i) acc[i * 64] = 0.0;
-    if (nr <= 0) return;
-    const int c = slab * 64 + lane;
-    const int cc = c < n ? c : 0;
-    double cur = 0.0;
-    int cur_row = 0;
-    // software pipeline: the next slice's row boundaries and each slice's
-    // next 64-element chunk are loaded one step ahead
-    auto load_bnd = [&](int sl) {
-        return (sl < S && lane <= nr) ? srp[(size_t)sl * (m + 1) + rb + lane] : INT_MAX;
-    };
-    int bnd_next = load_bnd(xcd);
-    for (int s = xcd; s < S; s += kL2Xcd) {
-        const int bnd = bnd_next;
-        bnd_next = load_bnd(s + kL2Xcd);
-        const int e0 = __shfl(bnd, 0, 64), e1 = __shfl(bnd, nr, 64);
-        const long long jbase = (long long)s * W;
-        int cnt_n = min(64, e1 - e0);
-        int j_n = lane < cnt_n ? (int)(jbase + scol[e0 + lane]) : 0;
-        double a_n = lane < cnt_n ? sval[e0 + lane] : 0.0;
-        for (int eb = e0; eb < e1; eb += 64) {
-            const int cnt = cnt_n;
-            const int my_j = j_n;
-            const double my_a = a_n;
-            const int ebn = eb + 64;
-            cnt_n = min(64, e1 - ebn);
-            if (cnt_n > 0) {
-                j_n = lane < cnt_n ? (int)(jbase + scol[ebn + lane]) : 0;
-                a_n = lane < cnt_n ? sval[ebn + lane] : 0.0;
-            }
-            for (int q = 0; q < cnt; q += kL2Batch) {
-                double a[kL2Batch], b[kL2Batch];
-                int row[kL2Batch];
-#pragma unroll
-                for (int u = 0; u < kL2Batch; ++u) {
-                    const int idx = q + u;
-                    const int j = __shfl(my_j, idx & 63, 64);
-                    a[u] = __shfl(my_a, idx & 63, 64);  // 0 past cnt
-                    b[u] = B[(long long)j * ldb + cc];
-                    row[u] = idx < cnt ? __popcll(__ballot(bnd <= eb + idx)) - 1 : cur_row;
-                }
-#pragma unroll
-                for (int u = 0; u < kL2Batch; ++u) {
-                    if (row[u] != cur_row) {
-                        acc[cur_row * 64] += cur;
-                        cur = 0.0;
-                        cur_row = row[u];
-                    }
-                    cur += a[u] * b[u];
-                }
-            }
-        }
-    }
-    acc[cur_row * 64] += cur;
-    double *out = part + ((size_t)xcd * m + rb) * 64 + lane;
-    for (int i = 0; i < nr; ++i) out[(size_t)i * 64] = acc[i * 64];
-}
-
-// C[:, slab] = alpha * sum_x part[x] (+ beta * C); 4 rows x 64 columns per WG
-template <bool kBeta>
-__global__ __launch_bounds__(256) void k_spmm_l2reduce(const double *__restrict__ part, int m, int n, int slab,
-                                                       double alpha, double beta, double *__restrict__ C,
-                                                       long long ldc)
-{
-    const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int c = slab * 64 + lane;
-    if (r >= m || c >= n) return;
-    double s = 0.0;
-#pragma unroll
-    for (int x = 0; x < kL2Xcd; ++x) s += part[((size_t)x * m + r) * 64 + lane];
-    double *o = C + (long long)c * ldc + r;
-    *o = kBeta ? alpha * s + beta * *o : alpha * s;
-}
-
-// host: slice-major CSR of A (columns cut every W)
-static int build_l2slice(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
-                         const std::vector<double> &hval, int W)
-{
-    SpmmPlan &P = A.mm;
-    const int m = A.m;
-    const int S = (A.n + W - 1) / W;
-    std::vector<int> off((size_t)S * (m + 1) + 1, 0);
-    for (int r = 0; r < m; ++r)
-        for (int e = rp[r]; e < rp[r + 1]; ++e) off[(size_t)(hcol[e] / W) * (m + 1) + r + 1]++;
-    // exclusive prefix over (slice, row), slice-major
-    long long run = 0;
-    for (int sl = 0; sl < S; ++sl) {
-        int *o = off.data() + (size_t)sl * (m + 1);
-        o[0] = (int)run;
-        for (int r = 0; r < m; ++r) {
-            run += o[r + 1];
-            o[r + 1] = (int)run;
-        }
-    }
-    std::vector<unsigned short> scol((size_t)std::max<long long>(A.nnz, 1));
-    std::vector<double> sval((size_t)std::max<long long>(A.nnz, 1));
-    std::vector<int> next(off.begin(), off.end());
-    for (int r = 0; r < m; ++r)
-        for (int e = rp[r]; e < rp[r + 1]; ++e) {
-            const int sl = hcol[e] / W;
-            const int o = next[(size_t)sl * (m + 1) + r]++;
-            scol[(size_t)o] = (unsigned short)(hcol[e] - sl * W);
-            sval[(size_t)o] = hval[e];
-        }
-    SBLAS_HIP(hipMalloc(&P.l2_rp, sizeof(int) * (size_t)S * (m + 1)));
-    SBLAS_HIP(hipMalloc(&P.l2_col, sizeof(unsigned short) * scol.size()));
-    SBLAS_HIP(hipMalloc(&P.l2_val, sizeof(double) * sval.size()));
-    SBLAS_HIP(hipMalloc(&P.l2_part, sizeof(double) * (size_t)kL2Xcd * m * 64));
-    SBLAS_HIP(hipMemcpy(P.l2_rp, off.data(), sizeof(int) * (size_t)S * (m + 1), hipMemcpyHostToDevice));
-    SBLAS_HIP(hipMemcpy(P.l2_col, scol.data(), sizeof(unsigned short) * scol.size(), hipMemcpyHostToDevice));
-    SBLAS_HIP(hipMemcpy(P.l2_val, sval.data(), sizeof(double) * sval.size(), hipMemcpyHostToDevice));
-    P.l2_S = S;
-    P.l2_W = W;
-    return SBLAS_OK;
-}
-
 // ---- column-sorted C-tile SpMM (few rows, tall B) -------------------------
 // The row forms move one B row (n*8 B) from L2 to the CU per NONZERO: 5.8 GB
 // per call on rail4284, at the L2/Infinity-Cache gather rate.  Here a
@@ -511,87 +368,6 @@ __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     }
 }
 
-// Owned-row form (opt-in, SBLAS_SPMM_CTOWN=1; global-column keys).  The C tile's rows are dealt to the 16 waves (balanced by entry
-// count, plan time), each wave walks only the entries of its own rows --
-// column-sorted, in steps of 8 entries with 8 distinct rows -- so no other
-// lane can touch a row between a wave's read and write: the update is a
-// plain ds_read_b128 / add / ds_write_b128 of the lane's two columns instead
-// of two ds_add_f64 (whose atomic read-modify-write costs the LDS ~12 cycles
-// per wave instruction).  Row stride 18 doubles (16-B aligned pairs); rows
-// R .. R+15 are the waves' private sinks for padding entries (value 0).
-constexpr int kCoPad = 18;
-constexpr int kCoWaves = kCtThreads / 64;
-constexpr int kCoMaxRows = 163840 / (kCoPad * 8) - kCoWaves;  // 1121 real rows
-
-template <bool kFast>
-__global__ __launch_bounds__(kCtThreads) void k_spmm_ctown(
-    const unsigned *__restrict__ key, const double *__restrict__ val, const long long *__restrict__ woff,
-    int ns, int nrb, int R, int rbits, int ncg, const double *__restrict__ B, long long ldb, int n, int m,
-    double *__restrict__ part)
-{
-    extern __shared__ double tile[];  // [R + 16][kCoPad]
-    const int x = (int)(blockIdx.x & 7);
-    int rest = (int)(blockIdx.x >> 3);
-    const int cg = rest % ncg;
-    rest /= ncg;
-    const int rb = rest % nrb, ss = rest / nrb;
-    const int slot = x * ns + ss;
-    const int r0 = rb * R, nr = min(R, m - r0);
-    for (int i = threadIdx.x; i < (R + kCoWaves) * kCoPad; i += kCtThreads) tile[i] = 0.0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long bk = (long long)slot * nrb + rb;
-    const long long w0 = woff[bk * (kCoWaves + 1) + wv], w1 = woff[bk * (kCoWaves + 1) + wv + 1];
-    const int g = lane >> 4, h = (lane >> 3) & 1, q = lane & 7;
-    const int myoff = 8 * (lane & 7) + 2 * g + h;
-    const unsigned rmask = (1u << rbits) - 1;
-    const unsigned ldb8 = (unsigned)(ldb * 8);
-    const int c0 = cg * kCtCols + 2 * q;
-    const char *Bc = reinterpret_cast<const char *>(B) + (size_t)c0 * 8;
-    typedef double v2d_t __attribute__((ext_vector_type(2)));
-    for (long long it = w0; it < w1; it += 64) {
-        const long long e = it + myoff;
-        const unsigned kk = key[e];
-        const unsigned long long vb = (unsigned long long)__double_as_longlong(val[e]);
-        const unsigned vlo = (unsigned)vb, vhi = (unsigned)(vb >> 32);
-        unsigned kt[8];
-        kt[0] = ct_bcast<0>(kk); kt[1] = ct_bcast<1>(kk); kt[2] = ct_bcast<2>(kk); kt[3] = ct_bcast<3>(kk);
-        kt[4] = ct_bcast<4>(kk); kt[5] = ct_bcast<5>(kk); kt[6] = ct_bcast<6>(kk); kt[7] = ct_bcast<7>(kk);
-        v2d_t bb[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            if constexpr (kFast) {
-                bb[t] = *reinterpret_cast<const v2d_t *>(Bc + (unsigned)(kt[t] >> rbits) * ldb8);
-            } else {  // guarded columns, 64-bit offsets
-                const double *br = B + (long long)(kt[t] >> rbits) * ldb;
-                bb[t].x = c0 < n ? br[c0] : 0.0;
-                bb[t].y = c0 + 1 < n ? br[c0 + 1] : 0.0;
-            }
-        }
-        unsigned lo[8], hi[8];
-        lo[0] = ct_bcast<0>(vlo); lo[1] = ct_bcast<1>(vlo); lo[2] = ct_bcast<2>(vlo); lo[3] = ct_bcast<3>(vlo);
-        lo[4] = ct_bcast<4>(vlo); lo[5] = ct_bcast<5>(vlo); lo[6] = ct_bcast<6>(vlo); lo[7] = ct_bcast<7>(vlo);
-        hi[0] = ct_bcast<0>(vhi); hi[1] = ct_bcast<1>(vhi); hi[2] = ct_bcast<2>(vhi); hi[3] = ct_bcast<3>(vhi);
-        hi[4] = ct_bcast<4>(vhi); hi[5] = ct_bcast<5>(vhi); hi[6] = ct_bcast<6>(vhi); hi[7] = ct_bcast<7>(vhi);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const double vt = __longlong_as_double((long long)(((unsigned long long)hi[t] << 32) | lo[t]));
-            v2d_t *cp = reinterpret_cast<v2d_t *>(&tile[(kt[t] & rmask) * kCoPad + 2 * q]);
-            v2d_t c = *cp;
-            c.x += vt * bb[t].x;
-            c.y += vt * bb[t].y;
-            *cp = c;
-        }
-    }
-    __syncthreads();
-    const int ncol = min(kCtCols, n - cg * kCtCols);
-    double *out = part + ((long long)slot * n + cg * kCtCols) * m + r0;
-    for (int i = threadIdx.x; i < nr * ncol; i += kCtThreads) {
-        const int c = i / nr, r = i - c * nr;
-        out[(long long)c * m + r] = tile[r * kCoPad + c];
-    }
-}
-
 // C = alpha * sum_slot part[slot] (+ beta * C), slots in order
 template <bool kBeta>
 __global__ __launch_bounds__(256) void k_spmm_ctreduce(const double *__restrict__ part, int nslot, int m, int n,
@@ -607,402 +383,6 @@ __global__ __launch_bounds__(256) void k_spmm_ctreduce(const double *__restrict_
     *o = kBeta ? alpha * s + beta * *o : alpha * s;
 }
 
-// ---------------------------------------------------------------------------
-// Tall-tile form (opt-in, SBLAS_SPMM_TTILE=1; m <= kTtMaxRows).  The C
-// tile of a workgroup is ALL m rows x 4 columns (m * 32 B of LDS: 137 KB for
-// rail4284's 4,284 rows), so every entry of a column j of A lands in the one
-// tile and B[j][4cg .. 4cg+3] is needed once per column run instead of once
-// per entry: the C-tile form above delivers 8 B of B to a lane per product
-// (5.8 GB per call on config 4, its TD-bound), this form 32 B per
-// (column-run piece, 4 columns) -- ~10 entries -- plus the entry itself.
-// The products land in LDS with one ds_add_f64 each, as before.
-//   Data: A's entries in CSC order, each column's run cut into near-equal
-// pieces of <= kTtPiece entries; the pieces of one slab of columns sorted by
-// length and dealt 64 to a GROUP, one per lane; a group of longest piece L
-// holds L x 64 slots, slot (t, l) = entry t of piece l (row, value; shorter
-// pieces padded), so iteration t of a wave is ONE coalesced 256-B key load
-// and ONE 512-B value load.  Lane l holds B[j_l][4cg .. 4cg+3] in registers
-// for its whole piece and adds 4 products per entry into the column-major
-// tile (one column per ds_add_f64 instruction: 64 random rows over 32 bank
-// pairs).  A wave loads all L slots of its group at once and the next
-// group's column words and B segment one group ahead.
-//   Work: slab s (2^wlog columns) belongs to list (s % 8) * 2 + (s / 8) % 2;
-// list (x, h) is walked by the column-group workgroups (x, h, cg) of XCD x
-// in the same order, so its entries and B lines (128 B = 4 column groups)
-// come into that XCD's L2 once and are shared.  Each workgroup writes its
-// alpha-free partial (slot = list); k_spmm_ctreduce adds the 16 in order.
-constexpr int kTtCols = 4;
-constexpr int kTtThreads = 1024;
-constexpr int kTtMaxRows = 4800;   // 150 KB of LDS tile
-// tile column stride (one instruction adds one column for all lanes, so the
-// stride does not affect its banks)
-__host__ __device__ constexpr int tt_stride(int m) { return m; }
-constexpr int kTtLists = 16;       // 8 XCDs x 2 halves
-constexpr int kTtPiece = 16;       // max entries per piece
-constexpr int kTtBlk = 8;          // slots per register block of the kernel
-constexpr int kTtGroup = 64;       // pieces per group: one per lane
-constexpr unsigned kTtNone = 0xffffffffu;  // key of an unused slot
-
-template <bool kFast>
-__global__ __launch_bounds__(kTtThreads) void k_spmm_ttile(
-    const int2 *__restrict__ gdesc, const unsigned *__restrict__ gcol, const unsigned *__restrict__ key,
-    const double *__restrict__ val, const int *__restrict__ loff, int m, int ms, int n, int ncg,
-    const double *__restrict__ B, long long ldb, double *__restrict__ part)
-{
-    extern __shared__ double tile[];  // [kTtCols][ms], column-major (ms = column stride)
-    const int x = (int)(blockIdx.x & 7);
-    const int rest = (int)(blockIdx.x >> 3);
-    const int cg = rest % ncg, hh = rest / ncg;
-    const int list = x * 2 + hh;
-    for (int i = threadIdx.x; i < ms * kTtCols; i += kTtThreads) tile[i] = 0.0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int c0 = cg * kTtCols;
-    typedef double v2d_t __attribute__((ext_vector_type(2)));
-    auto loadb = [&](unsigned gc, double *b) {
-        const long long j = (long long)(gc & 0xffffffu);
-        const double *br = B + j * ldb + c0;
-        if constexpr (kFast) {  // n % 4 == 0, 16-B aligned rows
-            const v2d_t u = *reinterpret_cast<const v2d_t *>(br);
-            const v2d_t w = *reinterpret_cast<const v2d_t *>(br + 2);
-            b[0] = u.x; b[1] = u.y; b[2] = w.x; b[3] = w.y;
-        } else {
-#pragma unroll
-            for (int c = 0; c < kTtCols; ++c) b[c] = c0 + c < n ? br[c] : 0.0;
-        }
-    };
-    const int gend = loff[list + 1];
-    constexpr int S = kTtThreads / 64;
-    int g = loff[list] + wv;
-    if (g >= gend) g = gend;  // wave-uniform
-    // stage: this group's {desc, column word, B}; next group's desc and
-    // column word (its B is issued at the top of this group)
-    int2 d = g < gend ? gdesc[g] : make_int2(0, 0);
-    unsigned gc = g < gend ? gcol[(long long)g * kTtGroup + lane] : 0u;
-    double b[kTtCols];
-    loadb(gc, b);
-    int2 dn = g + S < gend ? gdesc[g + S] : make_int2(0, 0);
-    unsigned gcn = g + S < gend ? gcol[(long long)(g + S) * kTtGroup + lane] : 0u;
-    for (; g < gend; g += S) {
-        double bn[kTtCols];
-        loadb(gcn, bn);  // next group's B (column word 0 for none: row 0, unused)
-        const int2 dnn = g + 2 * S < gend ? gdesc[g + 2 * S] : make_int2(0, 0);
-        const unsigned gcnn = g + 2 * S < gend ? gcol[(long long)(g + 2 * S) * kTtGroup + lane] : 0u;
-        const int L = d.y;  // wave-uniform
-        // slots in blocks of kTtBlk, the next block's loads in flight while
-        // this one is added
-        const unsigned *kp = key + d.x + lane;
-        const double *vp = val + d.x + lane;
-        unsigned ka[kTtBlk], kb[kTtBlk];
-        double va[kTtBlk], vb[kTtBlk];
-        auto ld = [&](int t0, unsigned *kk, double *vv) {
-#pragma unroll
-            for (int t = 0; t < kTtBlk; ++t)
-                if (t0 + t < L) {  // uniform
-                    kk[t] = kp[(long long)(t0 + t) * kTtGroup];
-                    vv[t] = vp[(long long)(t0 + t) * kTtGroup];
-                }
-        };
-        auto add = [&](int t0, const unsigned *kk, const double *vv) {
-#pragma unroll
-            for (int t = 0; t < kTtBlk; ++t)
-                if (t0 + t < L && kk[t] != kTtNone) {
-                    double *cp = tile + kk[t];
-#pragma unroll
-                    for (int c = 0; c < kTtCols; ++c)
-                        if (kFast || c0 + c < n) atomicAdd(cp + c * ms, vv[t] * b[c]);
-                }
-        };
-        ld(0, ka, va);
-        for (int t0 = 0; t0 < L; t0 += 2 * kTtBlk) {
-            ld(t0 + kTtBlk, kb, vb);
-            add(t0, ka, va);
-            if (t0 + kTtBlk >= L) break;  // uniform
-            ld(t0 + 2 * kTtBlk, ka, va);
-            add(t0 + kTtBlk, kb, vb);
-        }
-        d = dn;
-        gc = gcn;
-        dn = dnn;
-        gcn = gcnn;
-#pragma unroll
-        for (int c = 0; c < kTtCols; ++c) b[c] = bn[c];
-    }
-    __syncthreads();
-    // alpha-free partial [list][column][row] (column-major, as k_spmm_ctreduce reads)
-    const int ncol = min(kTtCols, n - c0);
-    double *out = part + ((long long)list * n + c0) * m;
-    for (int i = threadIdx.x; i < m * ncol; i += kTtThreads) {
-        const int cc = i / m, rr = i - cc * m;
-        out[i] = tile[cc * ms + rr];
-    }
-}
-
-// host: the tall-tile layout.  SBLAS_ERR_UNSUPPORTED when it does not apply
-// (too many rows for the tile, columns >= 2^24, or > 2^31 slots).
-//   LDS banks: a ds_add_f64 is serviced in 16-lane groups, and the 16
-// doubles of a group are conflict-free when their tile indices differ mod 16
-// (tools/exp_lds_atomic.hip: 11.3-13 LDS cycles per wave-instruction so,
-// 22.4 with random rows -- what a plain piece-per-lane layout gets).  With
-// the column-major tile (index c*ms + row, one column per instruction) that
-// means distinct rows mod 16 among a lane group's 16 entries in each slot.
-// So (1) the 16 pieces of a lane group are chosen, among the
-// next kTtWindow pieces in length order, to keep the group's residue
-// histogram flat (greedy), and (2) each lane group's entries are placed in
-// slots by a bipartite edge colouring (pieces x residues, every piece and
-// every residue at most once per slot), which needs max(longest piece,
-// busiest residue) slots (Konig).  Unused slots hold the sentinel key.
-constexpr int kTtWindow = 96;
-constexpr int kTtLg = 16;                  // pieces per 16-lane LDS group (= residues mod 16)
-constexpr int kTtLgPerWave = kTtGroup / kTtLg;
-
-// Edge colouring of a bipartite multigraph with max degree <= S colours:
-// edges (u, v), u < kTtLg (piece), v < kTtLg (residue); writes col[e] in [0, S).
-static void tt_colour(int ne, const unsigned char *eu, const unsigned char *ev, int S, std::vector<int> &col)
-{
-    constexpr int N = kTtLg;
-    std::vector<int> L((size_t)N * S, -1), R((size_t)N * S, -1);  // [node][colour] -> edge
-    col.assign((size_t)ne, -1);
-    for (int e = 0; e < ne; ++e) {
-        const int u = eu[e], v = ev[e];
-        int a = 0, b = 0;
-        while (L[(size_t)u * S + a] >= 0) ++a;  // free at u (exists: deg(u) <= S)
-        while (R[(size_t)v * S + b] >= 0) ++b;  // free at v
-        if (R[(size_t)v * S + a] >= 0) {
-            // a is taken at v, b free at v: flip the a/b path from v (it
-            // cannot reach u, whose a is free), after which a is free at v
-            std::vector<int> path;
-            int node = v, side = 1, cur = a;  // side 1: node on the right
-            for (;;) {
-                const int f = side ? R[(size_t)node * S + cur] : L[(size_t)node * S + cur];
-                if (f < 0) break;
-                path.push_back(f);
-                node = side ? eu[f] : ev[f];
-                side ^= 1;
-                cur = cur == a ? b : a;
-            }
-            for (int f : path) {  // clear, then recolour with the other colour
-                L[(size_t)eu[f] * S + col[(size_t)f]] = -1;
-                R[(size_t)ev[f] * S + col[(size_t)f]] = -1;
-            }
-            for (int f : path) {
-                col[(size_t)f] = col[(size_t)f] == a ? b : a;
-                L[(size_t)eu[f] * S + col[(size_t)f]] = f;
-                R[(size_t)ev[f] * S + col[(size_t)f]] = f;
-            }
-        }
-        col[(size_t)e] = a;
-        L[(size_t)u * S + a] = e;
-        R[(size_t)v * S + a] = e;
-    }
-}
-
-static int build_ttile(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
-                       const std::vector<double> &hval)
-{
-    SpmmPlan &P = A.mm;
-    const int m = A.m, k = A.n;
-    if (m <= 0 || m > kTtMaxRows || k >= (1 << 24)) return SBLAS_ERR_UNSUPPORTED;
-    int wlog = 11;  // slab: 2048 columns = 1 MiB of B at n = 64 per list in flight
-    if (const char *e = getenv("SBLAS_SPMM_TTW")) wlog = std::max(4, std::min(20, atoi(e)));
-    int pmax = kTtPiece;
-    if (const char *e = getenv("SBLAS_SPMM_TTPIECE")) pmax = std::max(1, std::min(kTtPiece, atoi(e)));
-    int win = kTtWindow;  // SBLAS_SPMM_TTWIN=1: consecutive pieces, no balancing
-    if (const char *e = getenv("SBLAS_SPMM_TTWIN")) win = std::max(1, atoi(e));
-    const long long nnz = A.nnz;
-    // CSC order: columns ascending, rows ascending inside a column
-    std::vector<long long> cp((size_t)k + 1, 0);
-    for (long long e = 0; e < nnz; ++e) cp[(size_t)hcol[(size_t)e] + 1]++;
-    for (int j = 0; j < k; ++j) cp[(size_t)j + 1] += cp[(size_t)j];
-    std::vector<unsigned> crow((size_t)std::max<long long>(nnz, 1));
-    std::vector<double> cval((size_t)std::max<long long>(nnz, 1));
-    {
-        std::vector<long long> nx(cp.begin(), cp.end() - 1);
-        for (int r = 0; r < m; ++r)
-            for (int e = rp[r]; e < rp[r + 1]; ++e) {
-                const long long o = nx[(size_t)hcol[(size_t)e]]++;
-                crow[(size_t)o] = (unsigned)r;
-                cval[(size_t)o] = hval[(size_t)e];
-            }
-    }
-    const long long nslab = ((long long)k + (1LL << wlog) - 1) >> wlog;
-    struct Piece {
-        int col;
-        long long e0;
-        int len;
-    };
-    // per slab: its waves (64 pieces = 4 lane groups), each as (slots S, the
-    // 64 pieces' column words, and slot-major entry indices (-1 = none))
-    struct Wave {
-        int S;
-        unsigned gcol[kTtGroup];
-        std::vector<long long> ent;  // [S][64] CSC entry index or -1
-    };
-    std::vector<std::vector<Wave>> sw((size_t)nslab);
-#pragma omp parallel for schedule(dynamic, 4)
-    for (long long s = 0; s < nslab; ++s) {
-        const int j0 = (int)(s << wlog), j1 = (int)std::min<long long>(k, (s + 1) << wlog);
-        std::vector<Piece> v;
-        for (int j = j0; j < j1; ++j) {
-            const long long cnt = cp[(size_t)j + 1] - cp[(size_t)j];
-            if (!cnt) continue;
-            const long long np = (cnt + pmax - 1) / pmax;
-            long long e = cp[(size_t)j];
-            for (long long p = 0; p < np; ++p) {  // near-equal pieces
-                const int L = (int)((cnt * (p + 1)) / np - (cnt * p) / np);
-                v.push_back({j, e, L});
-                e += L;
-            }
-        }
-        std::stable_sort(v.begin(), v.end(), [](const Piece &a, const Piece &b) { return a.len > b.len; });
-        const size_t np = v.size();
-        std::vector<std::array<unsigned char, kTtLg>> hist(np);
-        for (size_t i = 0; i < np; ++i) {
-            hist[i].fill(0);
-            for (int t = 0; t < v[i].len; ++t) hist[i][crow[(size_t)(v[i].e0 + t)] % kTtLg]++;
-        }
-        // (1) lane groups of kTtLg pieces with flat residue histograms
-        std::vector<char> used(np, 0);
-        std::vector<std::vector<int>> groups;
-        size_t head = 0;
-        while (true) {
-            while (head < np && used[head]) ++head;
-            if (head >= np) break;
-            std::vector<int> g;
-            int h[kTtLg] = {0};
-            for (int q = 0; q < kTtLg; ++q) {
-                int best = -1;
-                long long bv = 0;
-                int seen = 0;
-                for (size_t i = head; i < np && seen < win; ++i) {
-                    if (used[i]) continue;
-                    ++seen;
-                    int mx = 0;
-                    for (int r = 0; r < kTtLg; ++r) mx = std::max(mx, h[r] + hist[i][r]);
-                    const long long val = (long long)mx * 1000 - v[i].len;
-                    if (best < 0 || val < bv) {
-                        best = (int)i;
-                        bv = val;
-                    }
-                    if (q == 0) break;  // the group starts with the longest piece
-                }
-                if (best < 0) break;
-                used[(size_t)best] = 1;
-                g.push_back(best);
-                for (int r = 0; r < kTtLg; ++r) h[r] += hist[(size_t)best][r];
-            }
-            groups.push_back(std::move(g));
-        }
-        // (2) waves of kTtLgPerWave lane groups, each edge-coloured into slots
-        std::vector<Wave> &out = sw[(size_t)s];
-        for (size_t w0 = 0; w0 < groups.size(); w0 += kTtLgPerWave) {
-            Wave W{};
-            std::fill(W.gcol, W.gcol + kTtGroup, 0u);
-            std::vector<std::vector<int>> colour(kTtLgPerWave);
-            std::vector<std::vector<long long>> eidx(kTtLgPerWave);
-            std::vector<std::vector<unsigned char>> elane(kTtLgPerWave);
-            int Sw = 0;
-            for (int gi = 0; gi < kTtLgPerWave && w0 + gi < groups.size(); ++gi) {
-                const std::vector<int> &g = groups[w0 + gi];
-                int deg[kTtLg] = {0}, Lg = 0;
-                std::vector<unsigned char> eu, ev;
-                for (int q = 0; q < (int)g.size(); ++q) {
-                    const Piece &pc = v[(size_t)g[q]];
-                    W.gcol[gi * kTtLg + q] = (unsigned)pc.col | ((unsigned)pc.len << 24);
-                    Lg = std::max(Lg, pc.len);
-                    for (int t = 0; t < pc.len; ++t) {
-                        const unsigned rr = crow[(size_t)(pc.e0 + t)] % kTtLg;
-                        eu.push_back((unsigned char)q);
-                        ev.push_back((unsigned char)rr);
-                        eidx[gi].push_back(pc.e0 + t);
-                        deg[rr]++;
-                    }
-                }
-                int Sg = Lg;
-                for (int r = 0; r < kTtLg; ++r) Sg = std::max(Sg, deg[r]);
-                tt_colour((int)eu.size(), eu.data(), ev.data(), std::max(Sg, 1), colour[gi]);
-                elane[gi] = eu;
-                Sw = std::max(Sw, Sg);
-            }
-            W.S = Sw;
-            W.ent.assign((size_t)Sw * kTtGroup, -1);
-            for (int gi = 0; gi < kTtLgPerWave; ++gi)
-                for (size_t e = 0; e < eidx[gi].size(); ++e)
-                    W.ent[(size_t)colour[gi][e] * kTtGroup + gi * kTtLg + elane[gi][e]] = eidx[gi][e];
-            out.push_back(std::move(W));
-        }
-    }
-    // lists: slab s -> (s % 8) * 2 + (s / 8) % 2, slabs in order inside a list
-    std::vector<std::vector<long long>> lslabs(kTtLists);
-    for (long long s = 0; s < nslab; ++s) lslabs[(size_t)((s & 7) * 2 + ((s >> 3) & 1))].push_back(s);
-    std::vector<int> loff(kTtLists + 1, 0);
-    std::vector<long long> gbase((size_t)nslab), ebase((size_t)nslab);
-    long long G = 0, S = 0;
-    for (int l = 0; l < kTtLists; ++l) {
-        loff[(size_t)l] = (int)G;
-        for (long long s : lslabs[(size_t)l]) {
-            gbase[(size_t)s] = G;
-            ebase[(size_t)s] = S;
-            for (const Wave &W : sw[(size_t)s]) S += (long long)W.S * kTtGroup;
-            G += (long long)sw[(size_t)s].size();
-        }
-    }
-    loff[kTtLists] = (int)G;
-    if (S >= (1LL << 31) || G >= (1LL << 31) / kTtGroup) return SBLAS_ERR_UNSUPPORTED;
-    std::vector<int2> gdesc((size_t)std::max<long long>(G, 1));
-    std::vector<unsigned> gcol((size_t)std::max<long long>(G, 1) * kTtGroup, 0u);
-    std::vector<unsigned> key((size_t)std::max<long long>(S, 1), kTtNone);
-    std::vector<double> val((size_t)std::max<long long>(S, 1), 0.0);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (long long s = 0; s < nslab; ++s) {
-        long long g = gbase[(size_t)s], e = ebase[(size_t)s];
-        for (const Wave &W : sw[(size_t)s]) {
-            gdesc[(size_t)g] = make_int2((int)e, W.S);
-            std::copy(W.gcol, W.gcol + kTtGroup, gcol.begin() + (size_t)g * kTtGroup);
-            for (size_t i = 0; i < W.ent.size(); ++i)
-                if (W.ent[i] >= 0) {
-                    key[(size_t)(e + (long long)i)] = crow[(size_t)W.ent[i]];
-                    val[(size_t)(e + (long long)i)] = cval[(size_t)W.ent[i]];
-                }
-            e += (long long)W.S * kTtGroup;
-            ++g;
-        }
-    }
-    if (getenv("SBLAS_SPMM_TTSTAT")) {  // plan statistics: slot use, residue clashes per slot group
-        long long used = 0, clash = 0, groups = 0;
-        for (long long g = 0; g < G; ++g)
-            for (int t = 0; t < gdesc[(size_t)g].y; ++t)
-                for (int q = 0; q < kTtLgPerWave; ++q) {
-                    int seen[kTtLg] = {0}, any = 0;
-                    for (int l = 0; l < kTtLg; ++l) {
-                        const unsigned kk = key[(size_t)gdesc[(size_t)g].x + (size_t)t * kTtGroup + q * kTtLg + l];
-                        if (kk == kTtNone) continue;
-                        ++used;
-                        any = 1;
-                        clash += seen[kk % kTtLg]++ > 0;
-                    }
-                    groups += any;
-                }
-        fprintf(stderr, "tt plan: nnz %lld, slots %lld (%.3f per entry), lane-group slots %lld (%.2f entries each), "
-                        "residue clashes %lld\n", nnz, S, (double)S / std::max<long long>(nnz, 1), groups,
-                (double)used / std::max<long long>(groups, 1), clash);
-    }
-    auto up = [&](auto **dst, const auto &vv) -> int {
-        using T = typename std::decay_t<decltype(vv)>::value_type;
-        SBLAS_HIP(hipMalloc(dst, sizeof(T) * std::max<size_t>(vv.size(), 1)));
-        if (!vv.empty()) SBLAS_HIP(hipMemcpy(*dst, vv.data(), sizeof(T) * vv.size(), hipMemcpyHostToDevice));
-        return SBLAS_OK;
-    };
-    SBLAS_TRY(up(&P.tt_gdesc, gdesc));
-    SBLAS_TRY(up(&P.tt_gcol, gcol));
-    SBLAS_TRY(up(&P.tt_key, key));
-    SBLAS_TRY(up(&P.tt_val, val));
-    SBLAS_TRY(up(&P.tt_loff, loff));
-    P.tt_nlist = kTtLists;
-    P.tt = true;
-    return SBLAS_OK;
-}
-
 // host: the C-tile layout.  Returns SBLAS_ERR_UNSUPPORTED (caller keeps the
 // other forms) when the packed key cannot hold XCD-local column and row.
 static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
@@ -1012,19 +392,13 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     const int m = A.m, k = A.n;
     int wlog = 11;  // 2048 B rows = 1 MiB of B per slab at n = 64
     if (const char *e = getenv("SBLAS_SPMM_CTW")) wlog = std::max(4, std::min(20, atoi(e)));
-    // owned-row form (k_spmm_ctown, opt-in SBLAS_SPMM_CTOWN=1: bitwise
-    // repeatable, but measured 0.468 vs 0.370 ms on config 4 -- on gfx950 a
-    // ds_write_b128 costs ~13 LDS cycles of transfer, so read + write of two
-    // columns outweighs two ds_add_f64, and the b128 read groups conflict)
-    bool own = getenv("SBLAS_SPMM_CTOWN") && atoi(getenv("SBLAS_SPMM_CTOWN")) == 1 &&
-               !(getenv("SBLAS_SPMM_CTSLOT") && atoi(getenv("SBLAS_SPMM_CTSLOT")) != 0);
-    const int rcap = own ? kCoMaxRows : kCtMaxRows;
+    const int rcap = kCtMaxRows;
     int rmax = rcap;  // experiments: SBLAS_SPMM_CTR caps the tile rows
     if (const char *e = getenv("SBLAS_SPMM_CTR")) rmax = std::max(16, std::min(rcap, atoi(e)));
     const int nrb = (m + rmax - 1) / rmax;
     const int R = (m + nrb - 1) / nrb;
     int rbits = 1;
-    while ((1 << rbits) < R + (own ? kCoWaves : 0)) ++rbits;  // own: the waves' sink rows too
+    while ((1 << rbits) < R) ++rbits;
     const long long nslab = ((long long)k + (1LL << wlog) - 1) >> wlog;
     const long long jc_max = ((nslab + 7) / 8) << wlog;  // XCD-local columns
     if (rbits + 1 > 32 || jc_max > (1LL << (32 - rbits))) return SBLAS_ERR_UNSUPPORTED;
@@ -1057,7 +431,6 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // kernel then needs no slab arithmetic; sorting is the same order
     const bool direct = (long long)k <= (1LL << (32 - rbits)) && !(getenv("SBLAS_SPMM_CTDIRECT") &&
                                                                      atoi(getenv("SBLAS_SPMM_CTDIRECT")) == 0);
-    own = own && direct;
     std::vector<unsigned long long> kv((size_t)std::max<long long>(A.nnz, 1));  // key << 32 | entry index
     {
         std::vector<long long> next(off.begin(), off.end() - 1);
@@ -1076,7 +449,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // in parity.  So inside each aligned 8-entry step, odd rows go to the even
     // slots and even rows to the odd slots as far as the step allows (the
     // order inside a step does not change which products are summed).
-    const bool pair_rows = !own && !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
+    const bool pair_rows = !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int b = 0; b < nbk; ++b) {
         std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
@@ -1117,106 +490,6 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     }
     bool slots = false;
     if (const char *e = getenv("SBLAS_SPMM_CTSLOT")) slots = atoi(e) != 0 && A.nnz > 0;
-    if (own) {
-        // per bucket: rows dealt to the 16 waves by entry count (longest
-        // first to the least loaded), each wave's entries kept in column
-        // order and cut into steps of 8 entries with 8 distinct rows (an
-        // entry whose row is already in the step waits for the next one;
-        // look-ahead 32), short steps and the list's end padded to whole
-        // 64-entry iterations with value-0 entries on the wave's sink row
-        constexpr int W = kCoWaves;
-        constexpr unsigned kPadIdx = 0xffffffffu;
-        std::vector<std::vector<unsigned long long>> bl((size_t)nbk);
-        std::vector<long long> blen((size_t)nbk * W, 0);  // padded entries per (bucket, wave)
-#pragma omp parallel for schedule(dynamic, 1)
-        for (int b = 0; b < nbk; ++b) {
-            const long long e0 = off[(size_t)b], e1 = off[(size_t)b + 1];
-            const unsigned rm = (1u << rbits) - 1;
-            std::vector<long long> cnt((size_t)R, 0);
-            for (long long e = e0; e < e1; ++e) cnt[(size_t)((unsigned)(kv[(size_t)e] >> 32) & rm)]++;
-            std::vector<int> order((size_t)R);
-            for (int r = 0; r < R; ++r) order[(size_t)r] = r;
-            std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return cnt[(size_t)a] > cnt[(size_t)c]; });
-            std::vector<int> owner((size_t)R, 0);
-            long long load[W] = {0};
-            for (int r : order) {
-                int best = 0;
-                for (int w = 1; w < W; ++w)
-                    if (load[w] < load[best]) best = w;
-                owner[(size_t)r] = best;
-                load[best] += cnt[(size_t)r];
-            }
-            std::vector<std::vector<unsigned long long>> lists(W);
-            for (long long e = e0; e < e1; ++e)
-                lists[(size_t)owner[(size_t)((unsigned)(kv[(size_t)e] >> 32) & rm)]].push_back(kv[(size_t)e]);
-            std::vector<unsigned long long> &out = bl[(size_t)b];
-            for (int w = 0; w < W; ++w) {
-                std::vector<unsigned long long> &L = lists[(size_t)w];
-                const unsigned sink = (unsigned)(R + w);
-                std::vector<char> used(L.size(), 0);
-                size_t head = 0;
-                std::vector<unsigned long long> wl;
-                wl.reserve(L.size() + 64);
-                unsigned lastcol = 0;
-                auto pad = [&]() { wl.push_back(((unsigned long long)((lastcol << rbits) | sink) << 32) | kPadIdx); };
-                while (head < L.size()) {
-                    unsigned rows[8];
-                    int nr8 = 0;
-                    for (size_t i = head; i < L.size() && i < head + 32 && nr8 < 8; ++i) {
-                        if (used[i]) continue;
-                        const unsigned r = (unsigned)(L[i] >> 32) & rm;
-                        bool clash = false;
-                        for (int j = 0; j < nr8; ++j) clash |= rows[j] == r;
-                        if (clash) continue;
-                        rows[nr8++] = r;
-                        used[i] = 1;
-                        wl.push_back(L[i]);
-                        lastcol = (unsigned)(L[i] >> 32) >> rbits;
-                    }
-                    for (int j = nr8; j < 8; ++j) pad();
-                    while (head < L.size() && used[head]) ++head;
-                }
-                while (wl.size() % 64) pad();
-                out.insert(out.end(), wl.begin(), wl.end());
-                blen[(size_t)b * W + w] = (long long)wl.size();
-            }
-        }
-        std::vector<long long> woff((size_t)nbk * (W + 1));
-        long long tot = 0;
-        for (int b = 0; b < nbk; ++b)
-            for (int w = 0; w <= W; ++w) {
-                woff[(size_t)b * (W + 1) + w] = tot;
-                if (w < W) tot += blen[(size_t)b * W + w];
-            }
-        std::vector<unsigned> okey((size_t)std::max<long long>(tot, 1));
-        std::vector<double> oval((size_t)std::max<long long>(tot, 1));
-#pragma omp parallel for schedule(dynamic, 1)
-        for (int b = 0; b < nbk; ++b) {
-            const std::vector<unsigned long long> &v = bl[(size_t)b];
-            long long o = woff[(size_t)b * (W + 1)];
-            for (unsigned long long e : v) {
-                okey[(size_t)o] = (unsigned)(e >> 32);
-                const unsigned idx = (unsigned)(e & 0xffffffffu);
-                oval[(size_t)o] = idx == kPadIdx ? 0.0 : hval[(size_t)idx];
-                ++o;
-            }
-        }
-        SBLAS_HIP(hipMalloc(&P.ct_key, sizeof(unsigned) * okey.size()));
-        SBLAS_HIP(hipMalloc(&P.ct_val, sizeof(double) * oval.size()));
-        SBLAS_HIP(hipMalloc(&P.ct_woff, sizeof(long long) * woff.size()));
-        SBLAS_HIP(hipMemcpy(P.ct_key, okey.data(), sizeof(unsigned) * okey.size(), hipMemcpyHostToDevice));
-        SBLAS_HIP(hipMemcpy(P.ct_val, oval.data(), sizeof(double) * oval.size(), hipMemcpyHostToDevice));
-        SBLAS_HIP(hipMemcpy(P.ct_woff, woff.data(), sizeof(long long) * woff.size(), hipMemcpyHostToDevice));
-        P.ct_own = true;
-        P.ct_slots = false;
-        P.ct_ns = ns;
-        P.ct_nrb = nrb;
-        P.ct_R = R;
-        P.ct_rbits = rbits;
-        P.ct_wlog = wlog;
-        P.ct_direct = direct;
-        return SBLAS_OK;
-    }
     const long long nunits = slots ? soff.back() : A.nnz;
     std::vector<unsigned> hkey((size_t)std::max<long long>(nunits, 1)), hkey2;
     std::vector<double> hv((size_t)std::max<long long>(nunits, 1)), hv2;
@@ -1368,35 +641,16 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     SBLAS_TRY(up(&P.ucol, ucol));
     SBLAS_TRY(up(&P.atile, atile));
     SBLAS_TRY(up(&P.srows, srows));
-    // L2-slice form: few rows (every XCD holds all m partial rows), B much
-    // taller than the L2s (k >= 2^17: >= 64 MiB at n = 64), no MFMA blocks.
-    // SBLAS_SPMM_L2SLICE=0/1 overrides the size rule; SBLAS_SPMM_L2W sets W.
-    const int rw = (m + kL2WgPerXcd * 4 - 1) / (kL2WgPerXcd * 4);
-    bool l2 = P.nmfma == 0 && m > 0 && rw <= kL2MaxRows && A.n >= (1 << 17);
-    if (const char *e = getenv("SBLAS_SPMM_L2SLICE")) l2 = atoi(e) != 0 && P.nmfma == 0 && m > 0 && rw <= kL2MaxRows;
-    int W = 8192;
-    if (const char *e = getenv("SBLAS_SPMM_L2W")) W = std::max(1, std::min(65536, atoi(e)));
-    // the C-tile form replaces the L2-slice form where that one applies
-    // (SBLAS_SPMM_CTILE=0 keeps the L2-slice form, =1 forces C tiles)
-    bool ct = l2;
+    // C-tile form: few rows (m <= 16,384: a tile of <= 1,204 rows per CU
+    // covers them in <= 14 row blocks), B much taller than the L2s (k >=
+    // 2^17: >= 64 MiB at n = 64), no MFMA blocks.  SBLAS_SPMM_CTILE=0/1
+    // overrides the size rule (0: the row-wave kernels).
+    bool ct = P.nmfma == 0 && m > 0 && m <= 16384 && A.n >= (1 << 17);
     if (const char *e = getenv("SBLAS_SPMM_CTILE")) ct = atoi(e) != 0 && P.nmfma == 0 && m > 0;
-    // the tall-tile form is opt-in (SBLAS_SPMM_TTILE=1, wherever m fits the
-    // tile): on config 4 it runs 0.43 ms against the C tile's 0.36 ms -- its
-    // per-lane B fetches double the L1->L2 requests and L2 is the bound of
-    // both forms
-    bool tt = false;
-    if (const char *e = getenv("SBLAS_SPMM_TTILE")) tt = atoi(e) != 0 && P.nmfma == 0 && m > 0;
-    if (tt) {
-        const int rc = build_ttile(A, rp, hcol, hval);
-        if (rc == SBLAS_OK) ct = l2 = false;
-        else if (rc != SBLAS_ERR_UNSUPPORTED) return rc;
-    }
     if (ct) {
         const int rc = build_ctile(A, rp, hcol, hval);
-        if (rc == SBLAS_OK) l2 = false;
-        else if (rc != SBLAS_ERR_UNSUPPORTED) return rc;
+        if (rc != SBLAS_OK && rc != SBLAS_ERR_UNSUPPORTED) return rc;
     }
-    if (l2) SBLAS_TRY(build_l2slice(A, rp, hcol, hval, W));
     (void)s;
     P.ready = true;
     return SBLAS_OK;
@@ -1410,21 +664,11 @@ void free_spmm_plan(sblas_csr_s &A)
     (void)hipFree(P.ucol);
     (void)hipFree(P.atile);
     (void)hipFree(P.srows);
-    (void)hipFree(P.l2_rp);
-    (void)hipFree(P.l2_col);
-    (void)hipFree(P.l2_val);
-    (void)hipFree(P.l2_part);
     (void)hipFree(P.ct_key);
     (void)hipFree(P.ct_val);
     (void)hipFree(P.ct_off);
     (void)hipFree(P.ct_key2);
     (void)hipFree(P.ct_val2);
-    (void)hipFree(P.ct_woff);
-    (void)hipFree(P.tt_gdesc);
-    (void)hipFree(P.tt_gcol);
-    (void)hipFree(P.tt_key);
-    (void)hipFree(P.tt_val);
-    (void)hipFree(P.tt_loff);
     A.mm = SpmmPlan{};
 }
 
@@ -1475,35 +719,6 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     }
     const SpmmPlan &P = A.mm;
     const int nslab = (n + 63) / 64;
-    if (P.ready && P.tt) {
-        const int ncg = (n + kTtCols - 1) / kTtCols;
-        const int nslot = P.tt_nlist;
-        SBLAS_TRY(grow_scratch(A.spmm_part, A.spmm_part_bytes,
-                               sizeof(double) * (size_t)nslot * (size_t)n * (size_t)A.m));
-        static thread_local bool tt_attr[64] = {};
-        if (!tt_attr[A.device & 63]) {  // > 64 KiB of dynamic LDS
-            for (const void *kf : {(const void *)k_spmm_ttile<true>, (const void *)k_spmm_ttile<false>})
-                SBLAS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)(sizeof(double) * tt_stride(kTtMaxRows) * kTtCols)));
-            tt_attr[A.device & 63] = true;
-        }
-        const bool fast = n % kTtCols == 0 && ldr % 2 == 0 && ((uintptr_t)Brow & 15) == 0;
-        const int ms = tt_stride(A.m);
-        const size_t lds = sizeof(double) * (size_t)ms * kTtCols;
-        const unsigned nwg = (unsigned)(8 * 2 * ncg);
-        hipLaunchKernelGGL(fast ? k_spmm_ttile<true> : k_spmm_ttile<false>, dim3(nwg), dim3(kTtThreads), lds, s,
-                           P.tt_gdesc, P.tt_gcol, P.tt_key, P.tt_val, P.tt_loff, A.m, ms, n, ncg, Brow, ldr,
-                           A.spmm_part);
-        const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
-        if (beta != 0.0)
-            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, A.spmm_part, nslot, A.m, n, alpha,
-                               beta, C, (long long)ldc);
-        else
-            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, A.spmm_part, nslot, A.m, n,
-                               alpha, beta, C, (long long)ldc);
-        SBLAS_HIP(hipGetLastError());
-        return SBLAS_OK;
-    }
     if (P.ready && P.ct_nrb > 0) {
         const int ncg = (n + kCtCols - 1) / kCtCols;
         const int nslot = 8 * P.ct_ns;
@@ -1526,19 +741,6 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         }
         const bool fast = (ldr % 2 == 0) && (n % kCtCols == 0) && (((uintptr_t)Brow & 15) == 0) &&
                           (unsigned long long)A.n * (unsigned long long)ldr * 8ULL < (1ULL << 32);
-        if (P.ct_own) {
-            static thread_local bool own_attr[64] = {};
-            if (!own_attr[A.device & 63]) {
-                for (const void *kf : {(const void *)k_spmm_ctown<true>, (const void *)k_spmm_ctown<false>})
-                    SBLAS_HIP(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  (int)(sizeof(double) * (kCoMaxRows + kCoWaves) * kCoPad)));
-                own_attr[A.device & 63] = true;
-            }
-            const size_t lds_o = sizeof(double) * (size_t)(P.ct_R + kCoWaves) * kCoPad;
-            hipLaunchKernelGGL(fast ? k_spmm_ctown<true> : k_spmm_ctown<false>, dim3((unsigned)nwg),
-                               dim3(kCtThreads), lds_o, s, P.ct_key, P.ct_val, P.ct_woff, P.ct_ns, P.ct_nrb,
-                               P.ct_R, P.ct_rbits, ncg, Brow, ldr, n, A.m, part);
-        } else {
         using K = void (*)(const unsigned *, const double *, const unsigned *, const double *, const long long *,
                            int, int, int, int, int, int, const double *, long long, int, int, double *);
         K kern;
@@ -1551,7 +753,6 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_key2,
                            P.ct_val2, P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr,
                            n, A.m, part);
-        }
         const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
         if (beta != 0.0)
             hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
@@ -1559,23 +760,6 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         else
             hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
                                beta, C, (long long)ldc);
-        SBLAS_HIP(hipGetLastError());
-        return SBLAS_OK;
-    }
-    if (P.ready && P.l2_S > 0) {
-        const int rw = (A.m + kL2WgPerXcd * 4 - 1) / (kL2WgPerXcd * 4);
-        for (int sl = 0; sl < nslab; ++sl) {
-            hipLaunchKernelGGL(k_spmm_l2slice, dim3(kL2Xcd * kL2WgPerXcd), dim3(256),
-                               sizeof(double) * 4 * 64 * (size_t)rw, s, P.l2_rp, P.l2_col,
-                               P.l2_val, P.l2_S, P.l2_W, A.m, rw, Brow, ldr, n, sl, P.l2_part);
-            const unsigned nb = (unsigned)((A.m + 3) / 4);
-            if (beta != 0.0)
-                hipLaunchKernelGGL(k_spmm_l2reduce<true>, dim3(nb), dim3(256), 0, s, P.l2_part, A.m, n, sl, alpha,
-                                   beta, C, (long long)ldc);
-            else
-                hipLaunchKernelGGL(k_spmm_l2reduce<false>, dim3(nb), dim3(256), 0, s, P.l2_part, A.m, n, sl, alpha,
-                                   beta, C, (long long)ldc);
-        }
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;
     }

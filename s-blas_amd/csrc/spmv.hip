@@ -266,6 +266,24 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.rs.ready) return SBLAS_OK;
     DeviceGuard g(A.device);
+    // SBLAS_RS_SEQ=0: the vec4 entry order (A/B timing; read once per plan)
+    const char *seq_env = getenv("SBLAS_RS_SEQ");
+    A.rs.seq = !seq_env || atoi(seq_env) != 0;
+    // the same row blocks per XCD column panel on large scattered matrices
+    // (the panel plan, algo 4's layout; SBLAS_RS_PANEL=1 / 0 forces): decided
+    // first, so a panel plan never keeps a second, unused set of row blocks
+    if (!A.pn.degenerate) {
+        bool use = false;
+        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", 4000000LL, &use));
+        if (use) {
+            SBLAS_TRY(build_panel_plan(A, s));
+            if (!A.pn.degenerate) {
+                A.rs.panels = true;
+                A.rs.ready = true;
+                return SBLAS_OK;
+            }
+        }
+    }
     std::vector<RowBlock> blocks;
     std::vector<int4> longs;
     blocks.reserve(A.nnz / kRsBlockNnz + A.m / kRsMaxRows + 16);
@@ -286,17 +304,7 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
         SBLAS_HIP(hipMalloc(&A.rs.partial, sizeof(double) * nslots));
     }
     SBLAS_HIP(hipStreamSynchronize(s));
-    A.rs.ready = true;
-    // the same row blocks per XCD column panel on large scattered matrices
-    // (the panel plan, algo 4's layout); SBLAS_RS_PANEL=1 / 0 forces
-    if (!A.pn.degenerate) {
-        bool use = false;
-        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", 4000000LL, &use));
-        if (use) {
-            SBLAS_TRY(build_panel_plan(A, s));
-            A.rs.panels = !A.pn.degenerate;
-        }
-    }
+    A.rs.ready = true;  // only once every step above has succeeded
     return SBLAS_OK;
 }
 
@@ -330,8 +338,7 @@ int launch_spmv_rowsplit(const sblas_csr_s &A, double alpha, const double *x,
     if (!A.rs.ready) return SBLAS_ERR_INVALID;
     if (A.rs.panels) return launch_spmv_panel(A, alpha, x, beta, y, s);
     if (A.rs.nblocks == 0) return SBLAS_OK;
-    const char *seq_env = getenv("SBLAS_RS_SEQ");  // read per launch (tests switch it)
-    const int seq = seq_env ? atoi(seq_env) : 1;
+    const bool seq = A.rs.seq;
     if (beta != 0.0) {
         auto kern = seq ? k_spmv_rowsplit<true, true> : k_spmv_rowsplit<true, false>;
         SBLAS_LAUNCH(kern, dim3(A.rs.nblocks), dim3(kRsThreads), 0, s,
@@ -782,12 +789,13 @@ __device__ __forceinline__ void csr5_tile_st(
     }
 }
 
-// SBLAS_C5_PF selects the tile form (A/B timing; read once): 0 plain,
-// 1 phased loads + prefetched row ends, 2 (default) staged y with
-// non-temporal y accesses, 3 staged y with plain accesses
-static int c5_form()
+// SBLAS_C5_PF selects the tile form (A/B timing; read once per plan, at
+// build_csr5_plan): 0 plain, 1 phased loads + prefetched row ends,
+// 2 (default) staged y with non-temporal y accesses, 3 staged y with plain
+// accesses
+static int c5_form_env()
 {
-    const char *e = getenv("SBLAS_C5_PF");  // read per launch (tests switch it within one process)
+    const char *e = getenv("SBLAS_C5_PF");
     return e ? std::max(0, std::min(3, atoi(e))) : 2;
 }
 
@@ -1107,6 +1115,7 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     if (A.c5.ready) return SBLAS_OK;
     DeviceGuard g(A.device);
     Csr5Plan &P = A.c5;
+    P.form = c5_form_env();
     const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
     const char *pe = getenv("SBLAS_CSR5_PANEL");
     // Tiles per XCD column panel (each XCD's gathers in a slice of x) when x
@@ -1219,9 +1228,9 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
         if (A.m == 0) return SBLAS_OK;
         const long long grid = (P.maxtiles + 3) / 4 * P.P;
         if (grid > 0)
-            SBLAS_LAUNCH((c5_form() == 2   ? k_spmv_csr5_panel<2>
-                          : c5_form() == 3 ? k_spmv_csr5_panel<3>
-                                           : k_spmv_csr5_panel<0>),
+            SBLAS_LAUNCH((P.form == 2   ? k_spmv_csr5_panel<2>
+                          : P.form == 3 ? k_spmv_csr5_panel<3>
+                                        : k_spmv_csr5_panel<0>),
                          dim3((unsigned)grid), dim3(256), 0, s, P.desc, P.P, x, alpha);
         const long long mc = P.maxtiles;
         if (mc > 0)
@@ -1237,7 +1246,7 @@ int launch_spmv_csr5(const sblas_csr_s &A, double alpha, const double *x,
     }
     if (P.ntiles) {
         const unsigned nb = (unsigned)((P.ntiles + 3) / 4);
-        const int form = c5_form();
+        const int form = P.form;
         if (beta != 0.0)
             SBLAS_LAUNCH((form == 2   ? k_spmv_csr5<true, 2>
                           : form == 3 ? k_spmv_csr5<true, 3>

@@ -70,20 +70,6 @@ constexpr int kXsChunk = 256;      // entries per chunk: one wave, 4 per lane
 constexpr int kXsUnroll = 2;       // chunks per wave per pipeline stage
 constexpr uint32_t kXsPad = ((1u << kXsColBits) - 1) << kXsRowBits;  // column all ones, row 0
 constexpr int kXsTrace = 6;        // longs per trace row
-// K24 chunks (opt-in, SBLAS_XS_K24; measured slower, see the planner): 320 entries = 5 sub-chunks of
-// 64; a key is 24 bits, (column - sub-chunk base) << 13 | local row, the base
-// being the group-local column of the sub-chunk's first entry; a sub-chunk
-// ends early rather than span more than kK24Span columns.  Lane l's 16-B key
-// load holds the keys of entries l, 64+l, ..., 256+l (5 x 24 bits); values
-// {l, 64+l} and {128+l, 192+l} as two 16-B loads and 256+l as one 8-B load;
-// the 5 bases sit in a 32-B header read with scalar loads.  11.1 B per entry
-// on config 2's narrow blocks against 12 for the 32-bit keys.
-constexpr int kK24RowBits = 13;
-constexpr uint32_t kK24Mask = (1u << 24) - 1;
-constexpr uint32_t kK24Pad = kK24Mask;  // column offset all ones, row all ones
-constexpr int kK24Span = (1 << (24 - kK24RowBits)) - 2;  // largest column offset (2046)
-constexpr int kK24Bytes = 1024 + 2560 + 32;              // keys | values | header
-static_assert(kK24Bytes % 16 == 0, "16-B aligned chunks");
 static_assert(kXsRowBits + kXsColBits == 32, "packed key is 32 bits");
 static_assert(kXsHalfRows <= (1 << kXsRowBits), "a team's local row must fit the key");
 // a range's rows: a team's half, or (unpaired / solo items) the whole
@@ -141,8 +127,7 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 // bit 0 = plain LDS stores instead of ds_add_f64, bit 1 = gathers read x[0],
 // bit 3 (xs_stream_dyn only) = no gather at all (a key-derived constant),
 // bit 4 (xs_stream_dyn only) = gathers folded into x[0, 65536) (same lane
-// pattern, an L2-resident 512 KiB: separates L2 fills from L2 requests),
-// bit 5 (xs_stream_dyn only) = gathers as sc1 loads (L1 bypassed, L2-served).
+// pattern, an L2-resident 512 KiB: separates L2 fills from L2 requests).
 template <int kMode, int S>
 __device__ __forceinline__ void xs_stream(const v4u *__restrict__ key4,
                                           const v2d *__restrict__ val2, int ks, int vs, long long c0,
@@ -266,10 +251,7 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
             for (int j = 0; j < 4; ++j) {
                 const uint32_t k = kk[u][j];
                 const int idx = k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits);
-                if constexpr ((kMode & 32) != 0)  // experiment: L1-bypassing (sc1) gathers, L2-served
-                    xx[u][j] = __hip_atomic_load(x + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    xx[u][j] = (kMode & 8) ? (double)(k & 1) : x[(kMode & 2) ? 0 : (kMode & 16) ? (idx & 0xffff) : idx];
+                xx[u][j] = (kMode & 8) ? (double)(k & 1) : x[(kMode & 2) ? 0 : (kMode & 16) ? (idx & 0xffff) : idx];
             }
     };
     auto accumulate = [&](long long cb, const v4u *kk, const v2d *va, const v2d *vb,
@@ -310,111 +292,6 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4,
         load(ca, ka, vaa, vab, oa);
         __builtin_amdgcn_sched_barrier(0);
         accumulate(cb, kb, vba, vbb, xb);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ca >= c1) break;
-    }
-}
-
-// K24 form of xs_stream_dyn (same claims, same pipeline): per chunk one 16-B
-// key load, two 16-B and one 8-B value loads, a 32-B scalar header.
-template <int kMode, int U = kXsUnroll>
-__device__ __forceinline__ void xs_stream_dyn24(const unsigned char *__restrict__ base, int *ctr, long long c0,
-                                                long long c1, const long long *bnd, int gb, int Wg,
-                                                const double *__restrict__ x, double *acc)
-{
-    if (c1 <= c0) return;  // uniform
-    if (__builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= c1 - c0)
-        return;
-    const int lane = threadIdx.x & 63;
-    int gi = 0;
-    long long nb = bnd[1];
-    auto claim = [&]() -> long long {
-        int v = 0;
-        if (lane == 0) v = atomicAdd(ctr, U);
-        return c0 + __builtin_amdgcn_readfirstlane(v);
-    };
-    struct Ch {
-        v4u k;
-        v2d va, vb;
-        double vc;
-        uint32_t b[5];
-        int xo;
-    };
-    auto load = [&](long long cb, Ch *ch) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const long long c = cb + u;
-            const bool live = c < c1;
-            const long long ci = live ? c : c1 - 1;
-            const unsigned char *cp = base + ci * kK24Bytes;
-            const int l = live ? lane : 0;
-            ch[u].k = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(cp) + l);
-            ch[u].va = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cp + 1024) + l);
-            ch[u].vb = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(cp + 2048) + l);
-            ch[u].vc = __builtin_nontemporal_load(reinterpret_cast<const double *>(cp + 3072) + l);
-            const uint32_t *h = reinterpret_cast<const uint32_t *>(cp + 3584);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) ch[u].b[j] = __builtin_amdgcn_readfirstlane(h[j]);
-            while (ci >= nb) nb = bnd[++gi + 1];
-            ch[u].xo = (gb + gi) * Wg;
-        }
-    };
-    auto keys = [&](const v4u &k, uint32_t *e) {
-        e[0] = k.x & kK24Mask;
-        e[1] = __builtin_amdgcn_alignbit(k.y, k.x, 24) & kK24Mask;
-        e[2] = __builtin_amdgcn_alignbit(k.z, k.y, 16) & kK24Mask;
-        e[3] = k.z >> 8;
-        e[4] = k.w & kK24Mask;
-    };
-    auto gather = [&](const Ch *ch, double (*xx)[5]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint32_t e[5];
-            keys(ch[u].k, e);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const int idx = e[j] == kK24Pad ? ch[u].xo : ch[u].xo + (int)ch[u].b[j] + (int)(e[j] >> kK24RowBits);
-                xx[u][j] = x[(kMode & 2) ? 0 : idx];
-            }
-        }
-    };
-    auto accumulate = [&](long long cb, const Ch *ch, double (*xx)[5]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool live = cb + u < c1;
-            uint32_t e[5];
-            keys(ch[u].k, e);
-            const double v[5] = {ch[u].va.x, ch[u].va.y, ch[u].vb.x, ch[u].vb.y, ch[u].vc};
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const double p = (live && e[j] != kK24Pad) ? v[j] * xx[u][j] : 0.0;
-                double *slot = &acc[e[j] & ((1u << kK24RowBits) - 1)];
-                if (kMode & 1) *slot = p;
-                else atomicAdd(slot, p);
-            }
-        }
-    };
-    Ch a[U], b[U];
-    double xa[U][5], xb[U][5];
-    long long ca = claim();
-    if (ca >= c1) return;
-    load(ca, a);
-    for (;;) {
-        gather(a, xa);
-        __builtin_amdgcn_sched_barrier(0);
-        const long long cb = claim();
-        load(cb, b);
-        __builtin_amdgcn_sched_barrier(0);
-        accumulate(ca, a, xa);
-        __builtin_amdgcn_sched_barrier(0);
-        if (cb >= c1) break;
-        gather(b, xb);
-        __builtin_amdgcn_sched_barrier(0);
-        ca = claim();
-        load(ca, a);
-        __builtin_amdgcn_sched_barrier(0);
-        accumulate(cb, b, xb);
         __builtin_amdgcn_sched_barrier(0);
         if (ca >= c1) break;
     }
@@ -465,49 +342,6 @@ __device__ void xs_reduce_phase(const XsArgs &a, double alpha, double beta, doub
     }
 }
 
-// Last-arriver reduce of a wide range (a.tail; replaces k_xsort_reduce): the
-// team whose sub-item counted in 8th for this launch writes the range's y.
-// Hand-off (MI355X_MICROARCH.md "visibility", first row of the sc1 table):
-// every partial is stored sc1 (8 B) by its team, every storing wave drains
-// (vmcnt(0)) before a workgroup barrier, ONE lane per team adds to the
-// range's unsharded arrival counter, and the team told by its add's return
-// value that it came last loads the other seven partials with sc1 loads only
-// (its own sit in its LDS rows).  Same sum as k_xsort_reduce: slots in XCD
-// order, then alpha * s + beta * y.
-template <bool kBeta, int kEp>
-__device__ __forceinline__ void xs_tail_reduce(const XsArgs &a, const XsRange &R, int k1, const double *acc,
-                                               int ht, int NT, double alpha, double beta,
-                                               double *__restrict__ y)
-{
-    const double *p = a.partial + R.pbase;
-    const int own = k1 - 1;
-    constexpr int B = 2;  // rows per thread in flight: 14 sc1 loads + 2 y loads
-#pragma unroll 1
-    for (int e0 = 0; e0 < kEp; e0 += B) {
-        double v[B][8], y0[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const int r = ht + (e0 + u) * NT;
-            const int rr = r < R.nrows ? r : 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                v[u][k] = k == own ? 0.0
-                                   : __hip_atomic_load(p + (long long)k * R.nrows + rr, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            y0[u] = kBeta ? y[R.row0 + rr] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const int r = ht + (e0 + u) * NT;
-            if (r >= R.nrows) continue;
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += k == own ? acc[r] : v[u][k];
-            y[R.row0 + r] = kBeta ? alpha * s + beta * y0[u] : alpha * s;
-        }
-    }
-}
-
 // kWG threads per workgroup: 1024 (16384 LDS rows, one workgroup per CU) or
 // 512 (8192 rows, two independent workgroups per CU).  kPair (1024 only): the
 // two halves of the workgroup ("teams", 8 waves and 8192 LDS rows each) run
@@ -515,7 +349,7 @@ __device__ __forceinline__ void xs_tail_reduce(const XsArgs &a, const XsRange &R
 // kDyn (pairs only): the chunks of both sub-items are claimed dynamically
 // (xs_stream_dyn); a team drains its own streams, then its partner's.
 template <bool kBeta, int kMode, int kWG, bool kPair, int kWA = 8, bool kTrace = false,
-          bool kDyn = false, int kU = kXsUnroll, bool kK24 = false>
+          bool kDyn = false, int kU = kXsUnroll>
 __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     const double *__restrict__ x,
                                                     double alpha, double beta,
@@ -529,7 +363,6 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
     __shared__ int s_item;
     __shared__ int s_ctr[2][2];  // kDyn: claimed chunks per (team, segment)
     __shared__ int s_par[2][4];  // kDyn: per team {sub valid, k1, g0, n1}
-    __shared__ int s_last[2];    // a.tail: this team's wide sub-item counted in last
     static_assert(!kDyn || kPair, "dynamic claims pair two sub-items");
     // waves per team: team 0 (the pair's first, normally narrow, sub-item)
     // gets kWA waves, team 1 the rest
@@ -647,11 +480,7 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                 if (hs < 0 || (seg && (hk1 || hg0 == 0))) continue;  // uniform
                 const long long *hb = s_bnd_all[h] + (seg ? 128 : 0);
                 const int hn = seg ? hg0 : hn1;
-                if constexpr (kK24)
-                    xs_stream_dyn24<kMode, kU>(reinterpret_cast<const unsigned char *>(a.key), &s_ctr[h][seg], hb[0],
-                                               hb[hn], hb, seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
-                else
-                    xs_stream_dyn<kMode, kU>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], hb[0], hb[hn], hb,
+                xs_stream_dyn<kMode, kU>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], hb[0], hb[hn], hb,
                                              seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
             }
         } else if (sub >= 0) {
@@ -702,18 +531,12 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             // agent-scope (sc1) stores when the fused reduce may read them
             // on another XCD (whose L2 is not coherent with this one);
             // plain stores otherwise: the kernel boundary before
-            // k_xsort_reduce publishes them (SBLAS_XS_SC1PART=1 keeps sc1)
-            if (a.fused || a.tail || a.sc1part) {
+            // k_xsort_reduce publishes them
+            if (a.fused) {
 #pragma unroll
                 for (int e = 0; e < kEp; ++e) {
                     const int r = ht + e * NT;
                     if (r < R.nrows) __hip_atomic_store(out + r, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else if (a.ntstore) {
-#pragma unroll
-                for (int e = 0; e < kEp; ++e) {
-                    const int r = ht + e * NT;
-                    if (r < R.nrows) __builtin_nontemporal_store(acc[r], out + r);
                 }
             } else {
 #pragma unroll
@@ -743,199 +566,23 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                     y0[e] = r < nrows ? yr[r] : 0.0;
                 }
             }
-            if (a.ntstore) {
 #pragma unroll
-                for (int e = 0; e < kEp; ++e) {
-                    const int r = et + e * eNT;
-                    if (r < nrows)
-                        __builtin_nontemporal_store(kBeta ? alpha * eacc[r] + beta * y0[e] : alpha * eacc[r], yr + r);
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < kEp; ++e) {
-                    const int r = et + e * eNT;
-                    if (r < nrows) yr[r] = kBeta ? alpha * eacc[r] + beta * y0[e] : alpha * eacc[r];
-                }
+            for (int e = 0; e < kEp; ++e) {
+                const int r = et + e * eNT;
+                if (r < nrows) yr[r] = kBeta ? alpha * eacc[r] + beta * y0[e] : alpha * eacc[r];
             }
         }
-        if (a.fused || a.tail) {
+        if (a.fused) {
             // count this team's wide sub-item in once every wave's partial
             // stores have drained (vmcnt(0), then the barrier)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (sub >= 0 && k1 && ht == 0) {
-                // acq_rel: releases this team's partials to the last
-                // arriver and makes every other team's visible to it before
-                // its reduce reads them (the HIP memory model's hand-off)
-                const unsigned old =
-                    __hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                s_last[half] = old + 1u == 8u * a.epoch;
-            }
-            if (a.tail) {
-                __syncthreads();
-                if (sub >= 0 && k1 && s_last[half]) {  // team-uniform
-                    constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
-                    constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
-                    xs_tail_reduce<kBeta, kEp>(a, R, k1, acc, ht, NT, alpha, beta, y);
-                }
-            }
+            if (sub >= 0 && k1 && ht == 0)
+                // release: this team's partials before its arrival
+                (void)__hip_atomic_fetch_add(&a.arrive[R.widx], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         // (the barrier at the loop top orders these reads of acc before the
         // next item's zeroing, and s_bnd's reuse)
-    }
-}
-
-// Batch form for small items (a rank's slice at N = 8: ~5 chunks per wave).
-// The persistent kernel's per-wave chain -- claim, key/value load, dependent
-// x gather, LDS add, with two chunks in flight -- is repeated only a few
-// times per wave there, so its fill and drain dominate.  Here every item is
-// static (one per workgroup, the plan has no dynamic claims), the item's
-// chunks of both sub-items are listed once in LDS (chunk id, x offset of its
-// column group, team), and wave w takes entries w, w+16, ... in batches of
-// KB: all KB chunks' key/value loads are issued together, then all their
-// gathers, then the adds (into the owning team's LDS rows).  Same products
-// and epilogue as k_spmv_xsort.
-constexpr int kXsBatchKB = 4;       // chunks per batch and wave
-constexpr int kXsBatchMax = 16 * kXsBatchKB * 3;  // at most 3 batches per wave
-template <bool kBeta>
-__global__ __launch_bounds__(kXsThreads) void k_spmv_xsort_batch(const XsArgs a, const double *__restrict__ x,
-                                                                 double alpha, double beta,
-                                                                 double *__restrict__ y)
-{
-    constexpr int KB = kXsBatchKB;
-    constexpr int NT = kXsThreads / 2;  // threads of a team (epilogue)
-    __shared__ double acc_all[kXsRows];
-    __shared__ long long s_rec_all[2][128 + 5];
-    __shared__ int4 s_tab[kXsBatchMax];  // chunk id, x offset, team
-    __shared__ int s_seg[4][4];          // per segment: team, first group, groups, prefix
-    __shared__ int s_nc;
-    const int qb = (int)(blockIdx.x & 7), ib = (int)(blockIdx.x >> 3);
-    if (ib >= a.qstat[qb]) return;  // workgroup-uniform
-    const int slot = qb * a.qstride + ib;
-    const int xcc = a.use_xcc ? xs_xcc_id() : qb;
-    const int RL = a.G + 5;
-    for (int j = threadIdx.x; j < 2 * RL; j += kXsThreads) {
-        const int h = j / RL;
-        s_rec_all[h][j - h * RL] = a.xrec[(long long)(2 * slot + h) * RL + (j - h * RL)];
-    }
-    __syncthreads();
-    // zero the teams' rows; segments of the two sub-items (thread 0)
-    for (int h = 0; h < 2; ++h) {
-        const int sub = (int)s_rec_all[h][0];
-        const int nr = sub >= 0 ? (int)(s_rec_all[h][1] >> 32) : 0;
-        for (int r = threadIdx.x; r < nr; r += kXsThreads) acc_all[h * kXsHalfRows + r] = 0.0;
-    }
-    if (threadIdx.x == 0) {
-        int ns = 0, tot = 0;
-        for (int h = 0; h < 2; ++h) {
-            const int sub = (int)s_rec_all[h][0];
-            if (sub < 0) continue;
-            const int k1 = sub & 255;
-            const long long *bo = s_rec_all[h] + 4;
-            const int g0 = k1 ? (k1 - 1) * a.q : xcc * a.q;
-            const int n1 = k1 ? a.q : a.G - g0;
-            // segment 1: groups [g0, g0 + n1); a narrow sub-item's segment 2: [0, g0)
-            const int sg[2][2] = {{g0, n1}, {0, k1 ? 0 : g0}};
-            for (int q = 0; q < 2; ++q) {
-                const int c = (int)(bo[sg[q][0] + sg[q][1]] - bo[sg[q][0]]);
-                if (sg[q][1] == 0 || c == 0) continue;
-                s_seg[ns][0] = h;
-                s_seg[ns][1] = sg[q][0];
-                s_seg[ns][2] = sg[q][1];
-                s_seg[ns][3] = tot;
-                tot += c;
-                ++ns;
-            }
-        }
-        for (int q = ns; q < 4; ++q) s_seg[q][3] = tot;
-        s_nc = tot;
-    }
-    __syncthreads();
-    const int C = s_nc;  // <= kXsBatchMax (planner)
-    for (int i = threadIdx.x; i < C; i += kXsThreads) {
-        int q = 0;
-        while (q < 3 && s_seg[q + 1][3] <= i) ++q;
-        const int h = s_seg[q][0], gs = s_seg[q][1], ng = s_seg[q][2];
-        const long long *bo = s_rec_all[h] + 4;
-        const long long cid = bo[gs] + (i - s_seg[q][3]);
-        int g = gs;
-        while (g + 1 < gs + ng && bo[g + 1] <= cid) ++g;
-        s_tab[i] = make_int4((int)cid, g * a.Wg, h, 0);
-    }
-    __syncthreads();
-    const v4u *key4 = reinterpret_cast<const v4u *>(a.key);
-    const v2d *val2 = reinterpret_cast<const v2d *>(a.val);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int b0 = wave; b0 < C; b0 += 16 * KB) {  // wave-uniform
-        v4u kk[KB];
-        v2d va[KB], vb[KB];
-        int xo[KB], tm[KB];
-        bool live[KB];
-#pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const int idx = b0 + 16 * u;
-            live[u] = idx < C;
-            const int4 t = s_tab[live[u] ? idx : b0];
-            const long long ci = t.x;
-            kk[u] = __builtin_nontemporal_load(key4 + ci * a.kstride + lane);
-            va[u] = __builtin_nontemporal_load(val2 + ci * a.vstride + lane);
-            vb[u] = __builtin_nontemporal_load(val2 + ci * a.vstride + 64 + lane);
-            xo[u] = t.y;
-            tm[u] = t.z;
-        }
-        double xx[KB][4];
-#pragma unroll
-        for (int u = 0; u < KB; ++u)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = kk[u][j];
-                xx[u][j] = x[k == kXsPad ? xo[u] : xo[u] + (int)(k >> kXsRowBits)];
-            }
-#pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const double v[4] = {va[u].x, va[u].y, vb[u].x, vb[u].y};
-            double *acc = acc_all + tm[u] * kXsHalfRows;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = kk[u][j];
-                const double p = (live[u] && k != kXsPad) ? v[j] * xx[u][j] : 0.0;
-                atomicAdd(&acc[k & ((1u << kXsRowBits) - 1)], p);
-            }
-        }
-    }
-    __syncthreads();
-    // epilogue: team h's rows by the threads of half h (as k_spmv_xsort)
-    const int h = (int)(threadIdx.x >= (unsigned)NT);
-    const int ht = (int)threadIdx.x - h * NT;
-    const long long *rec = s_rec_all[h];
-    const int sub = (int)rec[0];
-    if (sub < 0) return;
-    const int k1 = sub & 255;
-    const int row0 = (int)(rec[1] & 0xffffffffLL), nrows = (int)(rec[1] >> 32);
-    const double *acc = acc_all + h * kXsHalfRows;
-    constexpr int kEp = kXsHalfRows / NT;
-    if (k1) {
-        double *out = a.partial + rec[2] + (long long)(k1 - 1) * nrows;
-#pragma unroll
-        for (int e = 0; e < kEp; ++e) {
-            const int r = ht + e * NT;
-            if (r < nrows) out[r] = acc[r];
-        }
-    } else {
-        double *yr = y + row0;
-        double y0[kEp];
-        if constexpr (kBeta) {
-#pragma unroll
-            for (int e = 0; e < kEp; ++e) {
-                const int r = ht + e * NT;
-                y0[e] = r < nrows ? yr[r] : 0.0;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < kEp; ++e) {
-            const int r = ht + e * NT;
-            if (r < nrows) yr[r] = kBeta ? alpha * acc[r] + beta * y0[e] : alpha * acc[r];
-        }
     }
 }
 
@@ -1213,50 +860,17 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         set_error("xsort: column index out of [0, n) or key overflow");
         return SBLAS_ERR_INVALID;
     }
-    // K24 sub-chunks of a block: <= 64 entries spanning <= kK24Span columns
-    auto k24_subs = [&](const std::vector<std::pair<uint32_t, double>> &bb, std::vector<int> *starts) {
-        long long subs = 0;
-        for (size_t i0 = 0; i0 < bb.size();) {
-            const uint32_t base = bb[i0].first >> kXsRowBits;
-            size_t j = i0;
-            while (j < bb.size() && j - i0 < 64 && (bb[j].first >> kXsRowBits) - base <= (uint32_t)kK24Span) ++j;
-            if (starts) starts->push_back((int)i0);
-            ++subs;
-            i0 = j;
-        }
-        return subs;
-    };
-    // format: K24 needs the paired dynamic kernel (8192-row teams) and wins
-    // when its chunks hold fewer bytes (dense-enough blocks); SBLAS_XS_K24=0/1
-    std::vector<long long> n32(nblk), n24(nblk);
-    long long b32 = 0, b24 = 0;
-#pragma omp parallel for schedule(dynamic, 64) reduction(+ : b32, b24)
-    for (long long k = 0; k < (long long)nblk; ++k) {
-        n32[(size_t)k] = ((long long)bk[(size_t)k].size() + kXsChunk - 1) / kXsChunk;
-        n24[(size_t)k] = (k24_subs(bk[(size_t)k], nullptr) + 4) / 5;
-        b32 += n32[(size_t)k] * (long long)kXsChunk * 12;
-        b24 += n24[(size_t)k] * (long long)kK24Bytes;
-    }
-    // opt-in: on config 2 K24 moves 7% fewer bytes but runs 144 us against
-    // 137.7 us (the header's scalar load sits on every claim's dependency
-    // chain, and one 320-entry chunk per claim -- two spill -- keeps fewer
-    // loads in flight than two 256-entry chunks); SBLAS_XS_K24=1 selects it
-    // (only where its chunks are smaller, unless forced with =2)
-    bool k24 = false;
-    if (const char *e = getenv("SBLAS_XS_K24"))
-        k24 = P.dyn && !P.solo && rows_cap <= (1 << kK24RowBits) && (atoi(e) == 2 || (atoi(e) == 1 && b24 < b32));
-    P.k24 = k24;
     std::vector<long long> blk(nblk + 1, 0);  // chunk offsets
-    for (size_t k = 0; k < nblk; ++k) blk[k + 1] = blk[k] + (k24 ? n24[k] : n32[k]);
+    for (size_t k = 0; k < nblk; ++k)
+        blk[k + 1] = blk[k] + ((long long)bk[k].size() + kXsChunk - 1) / kXsChunk;
     const long long nchunks = blk.back();
 
     mark("pass1");
-    // pass 2: fill every chunk (lane-transposed, header comment / K24 notes)
-    // 32-bit keys, interleaved (default): per chunk 1 KiB of keys then 2 KiB
-    // of values, ONE 3-KiB run in HBM; split (SBLAS_XS_KV=0): all keys, then
-    // all values.  K24: 3616-B chunks, keys | values | header.
+    // pass 2: fill every chunk (lane-transposed, header comment)
+    // interleaved (default): per chunk 1 KiB of keys then 2 KiB of values,
+    // ONE 3-KiB run in HBM; split (SBLAS_XS_KV=0): all keys, then all values
     const bool kv = !(getenv("SBLAS_XS_KV") && atoi(getenv("SBLAS_XS_KV")) == 0);
-    const size_t cbytes = k24 ? (size_t)kK24Bytes : (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
+    const size_t cbytes = (size_t)kXsChunk * (sizeof(uint32_t) + sizeof(double));
     // every byte of every chunk is written by the fill below: no zeroing pass
     struct HostBuf {
         std::unique_ptr<unsigned char[]> p;
@@ -1267,72 +881,28 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     const size_t hb_n = (size_t)std::max<long long>(nchunks, 1) * cbytes;
     const HostBuf hbuf{std::unique_ptr<unsigned char[]>(new unsigned char[hb_n]), hb_n};
     auto chunk_keys = [&](long long c) {
-        return (uint32_t *)(hbuf.data() + ((kv || k24) ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
+        return (uint32_t *)(hbuf.data() + (kv ? (size_t)c * cbytes : (size_t)c * kXsChunk * sizeof(uint32_t)));
     };
     auto chunk_vals = [&](long long c) {
-        return (double *)(hbuf.data() + ((kv || k24) ? (size_t)c * cbytes + (k24 ? 1024 : kXsChunk * sizeof(uint32_t))
-                                                     : (size_t)std::max<long long>(nchunks, 1) * kXsChunk * sizeof(uint32_t) +
-                                                           (size_t)c * kXsChunk * sizeof(double)));
+        return (double *)(hbuf.data() + (kv ? (size_t)c * cbytes + kXsChunk * sizeof(uint32_t)
+                                            : (size_t)std::max<long long>(nchunks, 1) * kXsChunk * sizeof(uint32_t) +
+                                                  (size_t)c * kXsChunk * sizeof(double)));
     };
-    P.kstride = k24 ? kK24Bytes / 16 : kv ? (int)(cbytes / 16) : kXsChunk * 4 / 16;
-    P.vstride = k24 ? kK24Bytes / 16 : kv ? (int)(cbytes / 16) : kXsChunk * 8 / 16;
+    P.kstride = kv ? (int)(cbytes / 16) : kXsChunk * 4 / 16;
+    P.vstride = kv ? (int)(cbytes / 16) : kXsChunk * 8 / 16;
 #pragma omp parallel for schedule(dynamic, 64)
     for (long long k = 0; k < (long long)nblk; ++k) {
         const auto &bb = bk[(size_t)k];
         const long long c0 = blk[(size_t)k], c1 = blk[(size_t)k + 1];
-        if (!k24) {
-            for (long long c = c0; c < c1; ++c) {
-                uint32_t *kc = chunk_keys(c);
-                double *vc = chunk_vals(c);
-                for (int p = 0; p < kXsChunk; ++p) {
-                    const long long src = (c - c0) * kXsChunk + p;
-                    const bool in = src < (long long)bb.size();
-                    const int l = p & 63, j = p >> 6;
-                    kc[4 * l + j] = in ? bb[src].first : kXsPad;
-                    vc[(j < 2 ? 0 : 128) + 2 * l + (j & 1)] = in ? bb[src].second : 0.0;
-                }
-            }
-            continue;
-        }
-        std::vector<int> starts;
-        k24_subs(bb, &starts);
-        starts.push_back((int)bb.size());
-        const long long nsub = (long long)starts.size() - 1;
         for (long long c = c0; c < c1; ++c) {
-            unsigned char *cp = hbuf.data() + (size_t)c * cbytes;
-            uint32_t *kw = (uint32_t *)cp;          // 64 lanes x 4 words
-            double *vw = (double *)(cp + 1024);     // 320 values
-            uint32_t *hd = (uint32_t *)(cp + 3584); // 8 words
-            std::memset(cp, 0, cbytes);
-            for (int sb = 0; sb < 5; ++sb) {
-                const long long si = (c - c0) * 5 + sb;
-                uint32_t base = 0;
-                int a0 = 0, a1 = 0;
-                if (si < nsub) {
-                    a0 = starts[(size_t)si];
-                    a1 = starts[(size_t)si + 1];
-                    base = bb[(size_t)a0].first >> kXsRowBits;
-                }
-                hd[sb] = base;
-                for (int l = 0; l < 64; ++l) {
-                    const int src = a0 + l;
-                    uint32_t key = kK24Pad;
-                    double v = 0.0;
-                    if (src < a1) {
-                        const uint32_t col = bb[(size_t)src].first >> kXsRowBits;
-                        const uint32_t row = bb[(size_t)src].first & ((1u << kXsRowBits) - 1);
-                        key = ((col - base) << kK24RowBits) | row;
-                        v = bb[(size_t)src].second;
-                    }
-                    // lane l's 120 key bits: slot sb at bit 24*sb
-                    const int bit = 24 * sb, w = bit >> 5, o = bit & 31;
-                    kw[4 * l + w] |= key << o;
-                    if (o > 8) kw[4 * l + w + 1] |= key >> (32 - o);
-                    // values: slots 0,1 -> {l, 64+l} pair, 2,3 -> second pair, 4 -> single
-                    if (sb < 2) vw[2 * l + sb] = v;
-                    else if (sb < 4) vw[128 + 2 * l + (sb - 2)] = v;
-                    else vw[256 + l] = v;
-                }
+            uint32_t *kc = chunk_keys(c);
+            double *vc = chunk_vals(c);
+            for (int p = 0; p < kXsChunk; ++p) {
+                const long long src = (c - c0) * kXsChunk + p;
+                const bool in = src < (long long)bb.size();
+                const int l = p & 63, j = p >> 6;
+                kc[4 * l + j] = in ? bb[src].first : kXsPad;
+                vc[(j < 2 ? 0 : 128) + 2 * l + (j & 1)] = in ? bb[src].second : 0.0;
             }
         }
     }
@@ -1449,12 +1019,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         nstat += P.qstat[k];
     }
     P.dynamic = nstat < P.nitems ? 1 : 0;
-    // batch form (k_spmv_xsort_batch, opt-in SBLAS_XS_BATCH=1) when every
-    // item is static and small.  Not the default: on rank 0's cyclic slice of
-    // config 2 it is slower than the persistent kernel (cold span N = 4: 54.8
-    // vs 50.4 us, N = 8: 39.0 vs 34.9; profiles/r03/xsort/slice_batch*.jsonl):
-    // issuing a wave's loads together leaves HBM idle during the gathers.
-    {
+    {  // most chunks of one item (both sub-items), for the plan's statistics
         auto nch = [&](int sub) -> long long {
             if (sub < 0) return 0;
             const size_t i = (size_t)(sub >> 8) * G;
@@ -1465,9 +1030,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         for (int k = 0; k < 8; ++k)
             for (const auto &it : q[k]) mc = std::max(mc, nch(it.first) + nch(it.second));
         P.maxc = (int)std::min<long long>(mc, 1 << 30);
-        const char *be = getenv("SBLAS_XS_BATCH");
-        P.batch = be && atoi(be) != 0 && P.pair && !P.solo && P.nt == kXsThreads && !P.k24 && !P.dynamic &&
-                  mc <= kXsBatchMax;
     }
     std::vector<int> qflat((size_t)16 * P.qstride, -1);
     for (int k = 0; k < 8; ++k)
@@ -1497,9 +1059,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // against 6 us for the separate k_xsort_reduce launch.
     P.fused = P.nt == kXsThreads && !wide.empty() && getenv("SBLAS_XS_FUSE") &&
               atoi(getenv("SBLAS_XS_FUSE")) != 0;
-    // last-arriver reduce (SBLAS_XS_TAIL=1): no reduce launch, no waiting;
-    // the 8th sub-item of a wide range to finish writes its y (xs_tail_reduce)
-    P.tail = !P.fused && !wide.empty() && getenv("SBLAS_XS_TAIL") && atoi(getenv("SBLAS_XS_TAIL")) != 0;
     P.nrtasks = (int)rtasks.size();
     SBLAS_HIP(hipMalloc(&P.rtasks, sizeof(int2) * std::max<size_t>(rtasks.size(), 1)));
     SBLAS_HIP(hipMalloc(&P.arrive, sizeof(unsigned) * std::max<size_t>(wide.size(), 1)));
@@ -1580,24 +1139,12 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     a.rtasks = P.rtasks;
     a.nrtasks = P.nrtasks;
     a.arrive = P.arrive;
-    const bool tail = P.tail && !P.batch;  // the batch form has no in-kernel reduce
-    a.tail = tail ? 1 : 0;
-    a.epoch = (unsigned)(P.epoch + ((P.fused || tail) ? 1 : 0));
+    a.epoch = (unsigned)(P.epoch + (P.fused ? 1 : 0));
     a.qstride = P.qstride;
     a.G = P.G;
     a.q = P.q;
     a.Wg = P.Wg;
     a.use_xcc = use_xcc;
-    static const int sc1part = [] {
-        const char *e = getenv("SBLAS_XS_SC1PART");
-        return e ? atoi(e) : 0;
-    }();
-    a.sc1part = sc1part;
-    static const int ntstore = [] {
-        const char *e = getenv("SBLAS_XS_NTSTORE");
-        return e ? atoi(e) : 0;
-    }();
-    a.ntstore = ntstore;
     using K = void (*)(const XsArgs, const double *, double, double, double *);
     K kern;
     const bool b = beta != 0.0;
@@ -1631,35 +1178,17 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         else kern = mm == 4 ? XS_DYN(4, 2) : XS_DYN(6, 2);
         if ((mode & ~1) == 8 && xu == 1) kern = (mode & 1) ? XS_DYN(9, 1) : XS_DYN(8, 1);  // experiment: no gathers
         if (mode == 16 && xu == 1) kern = XS_DYN(16, 1);  // experiment: L2-resident gathers
-        if (mode == 32 && xu == 1) kern = XS_DYN(32, 1);  // experiment: sc1 (L1-bypassing) gathers
 #undef XS_DYN
-    }
-    if (P.k24) {  // 24-bit keys: the paired dynamic kernel only (planner)
-#define XS_K24(M, U) k_spmv_xsort<true, M, W, true, 8, false, true, U, true>
-        const int mm = mode & 2;
-        // one 320-entry chunk per claim by default (U = 2 spills at the
-        // 128-VGPR cap of 16 waves per CU); SBLAS_XS_U=2 for experiments
-        const char *ue = getenv("SBLAS_XS_U");
-        const int u24 = ue ? atoi(ue) : 1;
-        if (!b) kern = k_spmv_xsort<false, 0, W, true, 8, false, true, 1, true>;
-        else if (u24 == 2) kern = mm ? XS_K24(2, 2) : XS_K24(0, 2);
-        else kern = mm ? XS_K24(2, 1) : XS_K24(0, 1);
-#undef XS_K24
     }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
     if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
         if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
-        else if (P.pair && P.dyn && P.k24)
-            kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1, true>
-                     : k_spmv_xsort<false, 0, W, true, 8, true, true, 1, true>;
         else if (P.pair && P.dyn && xu == 1)
             kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1> : k_spmv_xsort<false, 0, W, true, 8, true, true, 1>;
         else if (P.pair && P.dyn) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true> : k_spmv_xsort<false, 0, W, true, 8, true, true>;
         else if (P.pair) kern = b ? k_spmv_xsort<true, 0, W, true, 8, true> : k_spmv_xsort<false, 0, W, true, 8, true>;
         else kern = b ? k_spmv_xsort<true, 0, W, false, 8, true> : k_spmv_xsort<false, 0, W, false, 8, true>;
     }
-    if (P.batch && !P.fused && mode == 0 && !trace_path)
-        kern = b ? k_spmv_xsort_batch<true> : k_spmv_xsort_batch<false>;
     std::vector<long long> htrace;
     if (trace_path) {
         const size_t len = 1 + (size_t)kXsTrace * (P.nitems + P.grid);
@@ -1670,7 +1199,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     SBLAS_LAUNCH(kern, dim3(P.grid), dim3(P.nt), 0, s, a, x, alpha, beta, y);
     SBLAS_HIP(hipGetLastError());
     P.parity ^= 1;
-    if (P.fused || tail) ++P.epoch;
+    if (P.fused) ++P.epoch;
     if (trace_path) {  // debugging aid: rows {subA, subB, block<<4|xcc, t0, endA, endB}
         SBLAS_HIP(hipMemcpyAsync(htrace.data(), a.trace, sizeof(long long) * htrace.size(),
                                  hipMemcpyDeviceToHost, s));
@@ -1685,7 +1214,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
             fclose(f);
         }
     }
-    if (P.nwide && !P.fused && !tail) {
+    if (P.nwide && !P.fused) {
         const dim3 grid((kXsHalfRows + 255) / 256, (unsigned)P.nwide);
         if (b)
             SBLAS_LAUNCH(k_xsort_reduce<true>, grid, dim3(256), 0, s, P.wranges, P.partial, alpha, beta,

@@ -82,6 +82,7 @@ _sig("sblas_spmv", _i, _p, _i, _d, _p, _d, _p, _p)
 _sig("sblas_spmv_timed", _i, _p, _i, C.c_double, _p, C.c_double, _p, _p, _p)
 _sig("sblas_spmv_algorithmic_bytes", _ll, _p, _i)
 _sig("sblas_hbm_probe", _i, _i, _p, _p, _ll, _i, _p)
+_sig("sblas_hbm_probe_timed", _i, _i, _p, _p, _ll, _i, _p, _p)
 _sig("sblas_csr_plan_bytes", _ll, _p, _i)
 _sig("sblas_csr_pick", _i, _p, _p, _p)
 _sig("sblas_spmm", _i, _p, _i, _d, _p, _i, _i, _d, _p, _i, _p)
@@ -105,6 +106,7 @@ _sig("sblas_mm_read", _i, C.c_char_p, _i, _p, _p, _p, _p, _p, _p)
 _sig("sblas_csrbin_write", _i, C.c_char_p, _i, _i, _ll, _p, _p, _p)
 _sig("sblas_csrbin_read", _i, C.c_char_p, _p, _p, _p, _p, _p, _p)
 _sig("sblas_partition_nnz", _i, _i, _ll, _p, _i, _p, _p, _p, _p, _p)
+_sig("sblas_partition_cost", _i, _i, _p, _i, C.c_double, _p, _p, _p, _p, _p)
 _sig("sblas_partition_rowblock", _i, _i, _i, _p)
 _sig("sblas_coo_sortbyrow", _i, _i, _ll, _p, _p, _p, _p)
 _sig("sblas_trsv_mgpu_create", _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i)
@@ -205,6 +207,18 @@ def partition_nnz(rowptr: np.ndarray, g: int):
     rp = np.ascontiguousarray(rowptr, np.int64)
     check(lib.sblas_partition_nnz(m, nnz, ptr(rp), g, ptr(si), ptr(ei), ptr(sr), ptr(er), ptr(sf)),
           "partition_nnz")
+    return si, ei, sr, er, sf
+
+
+def partition_cost(rowptr: np.ndarray, g: int, w: float = 6.0):
+    """Cost-weighted whole-row split (sblas_partition_cost): contiguous row
+    ranges balancing sum(nnz_r + w); same outputs as partition_nnz."""
+    m = len(rowptr) - 1
+    si = np.zeros(g, np.int64); ei = np.zeros(g, np.int64)
+    sr = np.zeros(g, np.int32); er = np.zeros(g, np.int32); sf = np.zeros(g, np.int32)
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    check(lib.sblas_partition_cost(m, ptr(rp), g, float(w), ptr(si), ptr(ei), ptr(sr), ptr(er), ptr(sf)),
+          "partition_cost")
     return si, ei, sr, er, sf
 
 
@@ -409,6 +423,15 @@ def hbm_probe(mode: int, src_ptr: int, dst_ptr: int, nbytes: int, wg_per_cu: int
     """Enqueue one HBM stream probe (sblas_hbm_probe): 0 read, 1 non-temporal
     read, 2 copy."""
     check(lib.sblas_hbm_probe(mode, src_ptr, dst_ptr, nbytes, wg_per_cu, stream), "hbm_probe")
+
+
+def hbm_probe_timed(mode: int, src_ptr: int, dst_ptr: int, nbytes: int, wg_per_cu: int = 8, stream=None) -> float:
+    """One HBM stream probe, waited for; returns its device span in ms
+    (sblas_hbm_probe_timed: runtime-stamped kernel start / end events)."""
+    ms = C.c_float(0.0)
+    check(lib.sblas_hbm_probe_timed(mode, src_ptr, dst_ptr, nbytes, wg_per_cu, stream, C.byref(ms)),
+          "hbm_probe_timed")
+    return ms.value
 
 
 def gen_vector(n: int, seed: int) -> np.ndarray:

@@ -57,8 +57,14 @@ class Plan:
                 bool(self.start_flag[rank]))
 
 
-def make_plan(rowptr: np.ndarray, n: int, world: int) -> Plan:
-    si, ei, sr, er, sf = sblas.partition_nnz(rowptr, world)
+def make_plan(rowptr: np.ndarray, n: int, world: int, row_cost=None) -> Plan:
+    """spMV_mgpu_v1's nnz split (dspmv_mgpu_v1.cu:60-94), or with row_cost =
+    w the cost-weighted whole-row split (sblas_partition_cost: ranges
+    balancing sum(nnz_r + w), no split rows)."""
+    if row_cost is None:
+        si, ei, sr, er, sf = sblas.partition_nnz(rowptr, world)
+    else:
+        si, ei, sr, er, sf = sblas.partition_cost(rowptr, world, row_cost)
     return Plan(world, len(rowptr) - 1, n, int(rowptr[-1]), si, ei, sr, er, sf)
 
 

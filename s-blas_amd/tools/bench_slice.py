@@ -32,12 +32,15 @@ def main():
                     help="also time the slice cut into K parts of consecutive local chunks (the "
                          "overlapped exchange's kernels, sblas_ctx_matrix_upload_parts): the K "
                          "launches back to back after a cold sweep, events between them")
-    ap.add_argument("--partition", choices=["cyclic", "nnz"], default="cyclic",
-                    help="cyclic (bench.py's default leg) or nnz (configs[2]'s spMV_mgpu_v1 split, the "
-                         "config3 leg: ranks hold different row classes, so --ranks all)")
+    ap.add_argument("--partition", choices=["cyclic", "nnz", "cost"], default="cyclic",
+                    help="cyclic (bench.py's default leg), nnz (configs[2]'s spMV_mgpu_v1 split, the "
+                         "config3 leg: ranks hold different row classes, so --ranks all) or cost (the "
+                         "cost-weighted whole-row split, config3's cost_weighted leg)")
+    ap.add_argument("--row-cost", type=float, default=6.0, help="per-row weight of --partition cost")
     ap.add_argument("--ranks", default="0", help="ranks whose slices to time: a list or 'all'")
     ap.add_argument("--floor", action="store_true",
-                    help="also time a cold streaming read of the slice's byte count")
+                    help="also time the slice's streaming floor (slice_floor: one cold read-stream "
+                         "kernel over the bytes xsort moves for the slice)")
     args = ap.parse_args()
 
     import torch
@@ -60,8 +63,10 @@ def main():
         if args.partition == "cyclic":
             plan = sblas_dist.make_cyclic_plan(rowptr, n, world)
             lrp, col, val = sblas_dist.cyclic_local_csr(rowptr, plan, rank, rows_fn)
-        else:  # whole rows of the nnz split (its split rows' shares rounded to whole rows)
-            _, _, sr, er, _ = sblas.partition_nnz(rowptr, world)
+        else:  # whole rows of the nnz split (its split rows' shares rounded to whole rows),
+               # or of the cost-weighted whole-row split (sblas_partition_cost)
+            _, _, sr, er, _ = (sblas.partition_nnz(rowptr, world) if args.partition == "nnz"
+                               else sblas.partition_cost(rowptr, world, args.row_cost))
             a, b = int(sr[rank]), int(er[rank]) + 1
             lrp = np.asarray(rowptr[a:b + 1], np.int64) - int(rowptr[a])
             col, val = rows_fn(a, b)
@@ -107,27 +112,44 @@ def main():
                               "algo": name, "local_rows": int(len(lrp) - 1),
                               "local_nnz": int(lrp[-1]), **out}), flush=True)
         if args.floor:
-            # streaming floor for the slice's bytes: a cold torch sum over a
-            # buffer of the slice's algorithmic size (stream events)
-            nbytes = 12 * int(lrp[-1]) + 4 * len(lrp) + 8 * n + 16 * (len(lrp) - 1)
-            buf = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
-            ts = []
-            with torch.cuda.stream(stream):
+            print(json.dumps(slice_floor(args, lrp, col, val, n, x, scrub, stream, torch, sblas, world)), flush=True)
+
+
+def slice_floor(args, lrp, col, val, n, x, scrub, stream, torch, sblas, world):
+    """the streaming floor of a rank's slice -- ONE
+    hand-written read-stream kernel (sblas_hbm_probe: 16-B loads, 8 in flight
+    per lane) over exactly the bytes the column-sorted kernel must move for
+    the slice (its chunk layout incl. padding and wide-range partials, x
+    once, y read and written), cold (1 GiB read sweep before each), timed as
+    the SpMV spans are (runtime-stamped kernel start / end events), over
+    launch shapes (grid-stride or one span per workgroup, plain or
+    non-temporal loads, 1-16 workgroups per CU); the best shape is the
+    floor."""
+    m = len(lrp) - 1
+    A = sblas.DeviceCSR.upload(0, n, lrp, col, val)
+    A.analyse(sblas.XSORT)
+    layout = int(A.plan_bytes(sblas.XSORT))
+    A.close()
+    nbytes = (layout + 8 * n + 16 * m + 15) // 16 * 16
+    buf = torch.ones(nbytes // 8, dtype=torch.float64, device=x.device)
+    sink = torch.zeros(2, dtype=torch.float64, device=x.device)
+    shapes = {}
+    with torch.cuda.stream(stream):
+        for mode, name in ((0, "grid"), (1, "grid_nt"), (3, "span"), (4, "span_nt")):
+            for wg in (1, 2, 4, 8, 16):
+                ts = []
                 for k in range(args.reps + 2):
                     scrub.sum(dtype=torch.int64)
                     torch.cuda.synchronize()
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record(stream)
-                    buf.sum()
-                    e1.record(stream)
-                    torch.cuda.synchronize()
-                    ts.append(e0.elapsed_time(e1))
-            us = float(np.median(ts[2:])) * 1e3
-            print(json.dumps({"world": world, "floor": "torch sum over the slice's bytes, cold",
-                              "bytes": nbytes, "us": round(us, 1),
-                              "gbps": round(nbytes / us / 1e3, 1)}), flush=True)
-            del buf
+                    ts.append(sblas.hbm_probe_timed(mode, buf.data_ptr(), sink.data_ptr(), nbytes, wg,
+                                                    stream.cuda_stream))
+                shapes[f"{name}_wg{wg}"] = round(float(np.median(ts[2:])) * 1e3, 2)
+    del buf
+    best = min(shapes, key=shapes.get)
+    us = shapes[best]
+    return {"world": world, "floor": "cold read stream of the slice's xsort bytes (sblas_hbm_probe_timed)",
+            "layout_bytes": layout, "x_bytes": 8 * n, "y_bytes": 16 * m, "bytes": nbytes,
+            "best_shape": best, "us": us, "gbps": round(nbytes / us / 1e3, 1), "shapes_us": shapes}
 
 
 def time_parts(args, plan, lrp, col, val, n, algo, resolved, x, scrub, stream, torch, sblas):

@@ -76,18 +76,16 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
     (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (2, {"SBLAS_CSR5_PANEL": "0"}),
     (2, {"SBLAS_C5_PF": "0"}), (2, {"SBLAS_C5_PF": "1"}), (2, {"SBLAS_C5_PF": "3", "SBLAS_CSR5_PANEL": "0"}),
     (1, {"SBLAS_RS_PANEL": "0"}), (1, {"SBLAS_RS_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
-    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_K24": "0"}),
-    (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2"}), (5, {"SBLAS_XS_TAIL": "1"}),
-    (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (1, {"SBLAS_RS_SEQ": "0"})],
+    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_U": "2"}),
+    (5, {"SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (1, {"SBLAS_RS_SEQ": "0"})],
     ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "csr5_plain", "csr5_form0", "csr5_form1",
          "csr5_form3_plain", "rowsplit_plain", "rowsplit_panels", "panel", "xsort", "xsort_static", "xsort_q3",
-         "xsort_fused",
-         "xsort_k32", "xsort_k24_u2", "xsort_tail", "xsort_tail_allwide", "xsort_solo", "rowsplit_vec4"])
+         "xsort_fused", "xsort_u2", "xsort_allwide", "xsort_solo", "rowsplit_vec4"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    launches = 25 if (algo == 5 and (not env or env in ({"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}))
+    launches = 25 if (algo == 5 and (not env or env == {"SBLAS_XS_SOLO": "1"})
                       and not cfg2["prefix"]) else 1
     _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
 
@@ -167,12 +165,10 @@ def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
 
 
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_TAIL": "1"}, {"SBLAS_XS_SOLO": "1"}],
-                         ids=["default", "batch", "tail", "solo"])
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_SOLO": "1"}], ids=["default", "solo"])
 def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world, rank, env):
     """A rank's cyclic slice of config 2 (bench.py's N > 1 share) with the
-    persistent column-sorted kernel and its opt-in batch form (SBLAS_XS_BATCH=1,
-    taken where every item is static and small: N >= 4 here), three launches
+    persistent column-sorted kernel (and its solo-item layout), three launches
     on one plan against the oracle, and the beta = 0 form on a NaN-filled y."""
     import sblas_dist
     torch = torch_cuda
@@ -277,28 +273,17 @@ def cfg4(orc):
                 want=want, bound=bound)
 
 
-@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ttile"), ("col", "ttile"),
-                                         ("row", "ttpiece4"), ("row", "ttwin1"), ("row", "ctown"),
-                                         ("row", "ctslot"), ("row", "l2slice")])
+@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ctslot"), ("row", "rowwave")])
 def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form):
     """BASELINE configs[3]: C = -0.7 A B + 0.8 C on the rail4284-shaped matrix,
     all 4284 x 64 entries of C checked (B row-major as resident in HBM, and
     the reference's column-major host layout), with the default column-sorted
-    C-tile form, the tall-tile form (opt-in: all rows x 4 columns per tile,
-    column-run pieces in bank-scheduled slots) and the L2-slice form."""
+    C-tile form, its column-run slot variant and the row kernels."""
     torch = torch_cuda
-    if form.startswith("tt"):
-        monkeypatch.setenv("SBLAS_SPMM_TTILE", "1")
-    if form == "ttpiece4":
-        monkeypatch.setenv("SBLAS_SPMM_TTPIECE", "4")
-    if form == "ttwin1":  # consecutive pieces, no residue balancing
-        monkeypatch.setenv("SBLAS_SPMM_TTWIN", "1")
-    if form == "l2slice":
-        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     if form == "ctslot":
         monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
-    if form == "ctown":  # owned rows (opt-in, bitwise repeatable)
-        monkeypatch.setenv("SBLAS_SPMM_CTOWN", "1")
+    if form == "rowwave":
+        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     c = cfg4
     m, k, n = c["m"], c["k"], c["n"]
     A = sb.DeviceCSR.upload(0, k, c["rp"], c["col"], c["val"])

@@ -36,7 +36,7 @@ def rand_csr(rng, m, n, maxlen, long_rows=()):
 
 
 @pytest.mark.parametrize("algo", [0, 1, 2, 4, 5])
-@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1), (2, 1)])
 def test_ctx_spmv_chain(torch_cuda, sb, orc, algo, partition, exchange):
     """Two chained steps (the second's beta input is the first's y, kept on
     the devices by the context) against the oracle; exchange 1 is the
@@ -117,7 +117,7 @@ def test_ctx_timed_steps_and_slice_info(torch_cuda, sb, orc):
     ctx.close()
 
 
-def test_ctx_allreduce_needs_nnz_partition(torch_cuda, sb):
+def test_ctx_allreduce_needs_contiguous_partition(torch_cuda, sb):
     rng = np.random.default_rng(8)
     rp, col, val = rand_csr(rng, 100, 100, 5)
     ctx = sb.DeviceCtx(1)
@@ -176,7 +176,7 @@ def test_cli_spmv_ctx(algo, partition, exchange, parts):
 
 @pytest.mark.parametrize("g", [2, 3, 5])
 @pytest.mark.parametrize("algo", [1, 2, 5])
-@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("partition,exchange", [(0, 0), (1, 0), (1, 1), (2, 0), (2, 1)])
 def test_ctx_loopback_multi_rank(torch_cuda, sb, orc, monkeypatch, g, algo, partition, exchange):
     """g > 1 context ranks on the one GPU (SBLAS_CTX_LOOPBACK=1: no RCCL, the
     collectives are stream-ordered device copies): three chained steps, long
@@ -346,4 +346,31 @@ def test_ctx_reupload_fewer_parts(torch_cuda, sb, orc, monkeypatch, g):
         assert np.all(np.abs(got[0] - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y)), parts
         for d in range(1, g):
             assert np.array_equal(got[0], got[d])
+    ctx.close()
+
+
+def test_ctx_loopback_cost_partition_config2_g8(torch_cuda, sb, orc, monkeypatch):
+    """configs[2]'s dataflow at full size over 8 loopback ranks with the
+    cost-weighted whole-row split (partition 2) and the all-reduce of the
+    zero-padded y: every rank's y within the bound and bit-identical; the
+    light ranks hold fewer entries than the heavy ones."""
+    monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    n = 2_000_000
+    rp = sb.gen_synth_rowptr(n)
+    col, val = sb.gen_synth_rows(n, rp, 0, n)
+    x = sb.gen_vector(n, 43)
+    y0 = sb.gen_vector(n, 44)
+    alpha, beta = orc.alpha_beta()
+    ctx = sb.DeviceCtx(8)
+    ctx.upload(n, n, rp, col, val, sb.CSR5, 2, sb.CTX_ALLREDUCE)
+    nnz = [ctx.slice_info(d)[1] for d in range(8)]
+    assert sum(nnz) == int(rp[-1]) and nnz[-1] < nnz[0]
+    ctx.set_x(x)
+    ctx.set_y(y0)
+    ctx.spmv_ex(alpha, beta)
+    want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
+    got = [ctx.get_y(d) for d in range(8)]
+    assert np.all(np.abs(got[0] - want) <= orc.spmv_bound(rp, col, val, x, alpha, beta, y0))
+    for d in range(1, 8):
+        assert np.array_equal(got[0], got[d])
     ctx.close()

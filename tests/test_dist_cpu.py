@@ -37,7 +37,7 @@ def merge(gathered, meta, stride, m):
     return y
 
 
-def _worker(rank, world, port, n, result_q):
+def _worker(rank, world, port, n, result_q, row_cost=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import orc
@@ -46,7 +46,7 @@ def _worker(rank, world, port, n, result_q):
     x = orc.gen_vector(n, 43)
     y0 = orc.gen_vector(n, 44)
     a, b = orc.alpha_beta()
-    plan = sblas_dist.make_plan(rp, n, world)
+    plan = sblas_dist.make_plan(rp, n, world, row_cost=row_cost)
     r0, r1, i0, i1, cont = plan.local(rank)
     # local slice exactly as the GPU path uploads it (dspmv_mgpu_v1.cu:125-133)
     dm = r1 - r0
@@ -58,23 +58,32 @@ def _worker(rank, world, port, n, result_q):
     if cont and dm:
         yl[0] = 0.0
     part = orc.csr_spmv(lrp, col[i0:i1], val[i0:i1], x, a, b, yl)
-    buf = torch.zeros(plan.stride, dtype=torch.float64)
-    buf[:dm] = torch.from_numpy(part)
-    out = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf)
-    y = merge(torch.cat(out).numpy(), plan.meta(), plan.stride, plan.m)
+    if row_cost is not None:
+        # cost-weighted whole rows + configs[2]'s exchange: the rank writes
+        # its rows into a zero-padded full y, one all-reduce sums them
+        yfull = torch.zeros(plan.m, dtype=torch.float64)
+        yfull[r0:r1] = torch.from_numpy(part)
+        dist.all_reduce(yfull)
+        y = yfull.numpy()
+    else:
+        buf = torch.zeros(plan.stride, dtype=torch.float64)
+        buf[:dm] = torch.from_numpy(part)
+        out = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        y = merge(torch.cat(out).numpy(), plan.meta(), plan.stride, plan.m)
     want = orc.csr_spmv(rp, col, val, x, a, b, y0)
     ok = bool(np.all(np.abs(y - want) <= orc.spmv_bound(rp, col, val, x, a, b, y0)))
     result_q.put((rank, ok, int(cont)))
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("row_cost", [None, 6.0], ids=["nnz_split_allgather", "cost_rows_allreduce"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_protocol(world):
+def test_gloo_protocol(world, row_cost):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 997, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 997, q, row_cost)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -82,7 +91,10 @@ def test_gloo_protocol(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res)
-    assert any(c for _, _, c in res)  # the split actually crossed a row
+    if row_cost is None:
+        assert any(c for _, _, c in res)  # the split actually crossed a row
+    else:
+        assert not any(c for _, _, c in res)  # whole rows: no carries
 
 
 def assemble_cyclic(gathered, world, stride, R, m):

@@ -80,6 +80,39 @@ def test_partition_nnz_matches_oracle(sb, orc, seed):
         assert covered == list(range(m))
 
 
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("w", [0.0, 6.0, 100.0])
+def test_partition_cost_whole_rows_balanced(sb, seed, w):
+    """The cost-weighted split (sblas_partition_cost): contiguous whole-row
+    ranges covering every row once, no carries, index ranges matching the
+    rows, and each range's cost sum(nnz_r + w) within one row's cost of the
+    ideal share."""
+    rng = np.random.default_rng(seed)
+    m = int(rng.integers(1, 600))
+    rp = _rand_rowptr(rng, m, int(rng.integers(1, 50)), [0.0, 0.3, 0.9][seed % 3])
+    cost = rp[1:] - rp[:-1] + w
+    for g in (1, 2, 3, 5, 8, 13):
+        si, ei, sr, er, sf = sb.partition_cost(rp, g, w)
+        assert not sf.any() and sr[0] == 0 and er[-1] == m - 1
+        assert np.all(sr[1:] == er[:-1] + 1)
+        assert np.array_equal(si, rp[sr]) and np.array_equal(ei, rp[er + 1] - 1)
+        share = cost.sum() / g
+        for d in range(g):
+            c = cost[sr[d]:er[d] + 1].sum()
+            assert c <= share + cost.max() + 1e-9, (g, d, c, share)
+
+
+def test_partition_cost_config2_shape(sb):
+    """On config 2's shape (rows < n/8: 96 entries, others 9) the cost split
+    gives the light ranks fewer entries than the nnz split does."""
+    rp = sb.gen_synth_rowptr(2_000_000)
+    si, ei, sr, er, _ = sb.partition_cost(rp, 8, 6.0)
+    nnz = ei - si + 1
+    assert nnz[-1] < rp[-1] / 8 < nnz[0]
+    costs = [(rp[er[d] + 1] - rp[sr[d]]) + 6.0 * (er[d] - sr[d] + 1) for d in range(8)]
+    assert max(costs) / min(costs) < 1.001
+
+
 def test_partition_rowblock(sb, orc):
     for m, g in [(10, 3), (2000000, 8), (5, 8), (0, 2)]:
         rs = sb.partition_rowblock(m, g)

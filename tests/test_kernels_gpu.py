@@ -33,50 +33,30 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1", "l2", "l2w", "ct", "ctw", "ctrows", "ctslab", "ctslot",
-                                    "ctown", "ctownrows", "ctownw", "tt", "ttrows", "ttpiece3", "ttw"])
+@pytest.mark.parametrize("splitk", ["auto", "0", "1", "ct", "ctw", "ctrows", "ctslab", "ctslot"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     """Both row kernels: wave per row and workgroup per row (split over its
-    nonzeros; picked automatically for long rows), the L2-slice form
-    (forced: "l2" = 3 slices of 2048 columns, "l2w" = 79 slices of 64) and
-    the column-sorted C-tile form (forced: "ct" = 3 slabs of 2048 columns,
-    one slab set; "ctw" = 313 slabs of 16 columns in 3 sets per XCD;
-    "ctrows" = 2,500 rows, i.e. 3 row blocks of 834), in its LDS-atomic form
-    (default) and its owned-row form ("ctown*", opt-in), and the tall-tile
-    form ("tt*": all rows x 4 columns per tile, column-run pieces; "ttpiece3"
-    cuts runs into pieces of <= 3 entries, "ttw" uses slabs of 64 columns)."""
+    nonzeros; picked automatically for long rows) and the column-sorted
+    C-tile form (forced: "ct" = 3 slabs of 2048 columns, one slab set; "ctw"
+    = 313 slabs of 16 columns in 3 sets per XCD; "ctrows" = 2,500 rows, i.e.
+    3 row blocks of 834; "ctslab" XCD-local slab keys; "ctslot" column-run
+    slots of two entries)."""
     torch = torch_cuda
-    if splitk.startswith("tt"):
-        monkeypatch.setenv("SBLAS_SPMM_TTILE", "1")
-        if splitk == "ttpiece3":
-            monkeypatch.setenv("SBLAS_SPMM_TTPIECE", "3")
-        if splitk == "ttw":
-            monkeypatch.setenv("SBLAS_SPMM_TTW", "6")
     if splitk in ("0", "1"):
         monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
-    if splitk.startswith("l2"):
-        monkeypatch.setenv("SBLAS_SPMM_L2SLICE", "1")
-        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
-        if splitk == "l2w":
-            monkeypatch.setenv("SBLAS_SPMM_L2W", "64")
     if splitk.startswith("ct"):
         monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
         if splitk == "ctslab":  # XCD-local slab keys instead of global columns
             monkeypatch.setenv("SBLAS_SPMM_CTDIRECT", "0")
         if splitk == "ctslot":  # column-run slots of two entries (opt-in form)
             monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
-        if splitk.startswith("ctown"):  # owned rows, plain LDS read-add-write
-            monkeypatch.setenv("SBLAS_SPMM_CTOWN", "1")
-        if splitk == "ctownw":
-            monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
-            monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
         if splitk == "ctw":
             monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
             monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
     rng = np.random.default_rng(ncols + 10 * layout)
-    m, k = (2500 if splitk in ("ctrows", "ctownrows") else 4700 if splitk == "ttrows" else 700), 5000
+    m, k = (2500 if splitk == "ctrows" else 700), 5000
     rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
     B = rng.standard_normal((k, ncols))
     C0 = rng.standard_normal((m, ncols))
@@ -97,14 +77,14 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
     A.close()
 
 
-@pytest.mark.parametrize("form", ["ctile", "ttile"])
+@pytest.mark.parametrize("form", ["ctile"])
 @pytest.mark.parametrize("layout", [0, 1])
 def test_spmm_two_handles_two_streams(torch_cuda, sb, orc, monkeypatch, layout, form):
     """Two handles of different matrices on two streams of one device, launched
     back to back without synchronising: each keeps its own scratch (B copy,
     C-tile partials: sblas_csr_s::spmm_*), so both C match the oracle."""
     torch = torch_cuda
-    monkeypatch.setenv("SBLAS_SPMM_CTILE" if form == "ctile" else "SBLAS_SPMM_TTILE", "1")
+    monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
     ncols, k = 64, 6000
     outs = []
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]

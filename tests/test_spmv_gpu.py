@@ -34,22 +34,14 @@ ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (5, {"SBLAS_XS_Q": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_Q": "3"}),
          (5, {"SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_FUSE": "1", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_K24": "2"}), (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_K24": "2", "SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K24": "0"}),
-         (5, {"SBLAS_XS_BATCH": "1"}), (5, {"SBLAS_XS_BATCH": "1", "SBLAS_XS_ALLWIDE": "1"}),
-         (5, {"SBLAS_XS_TAIL": "1"}), (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_ALLWIDE": "1", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_TAIL": "1", "SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_SOLO": "1"}), (5, {"SBLAS_XS_SOLO": "1", "SBLAS_XS_WSTAR": "50"}),
          (1, {"SBLAS_RS_SEQ": "0"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "2"}),
          (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"})]
 ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
-            "xsort_k24", "xsort_k24_w50", "xsort_k24_q3_w50", "xsort_k24_u2_w50", "xsort_k32",
-            "xsort_batch", "xsort_batch_allwide", "xsort_tail", "xsort_tail_w50", "xsort_tail_allwide_w50",
-            "xsort_tail_unpaired_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
+            "xsort_u2_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
             "rowsplit_panel3"]
 
 
@@ -221,9 +213,8 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
     assert np.array_equal(outs[4], outs[5])
 
 
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_BATCH": "1"}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"},
-                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"},
-                                 {"SBLAS_XS_K24": "2", "SBLAS_XS_WSTAR": "50"}])
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"},
+                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}])
 def test_xsort_relaunch(torch_cuda, sb, orc, monkeypatch, env):
     """The column-sorted kernel's work queues re-arm themselves at the end of
     each launch (no memset): five launches on one plan, each checked."""
