@@ -26,3 +26,5 @@ for f in [f"{O}/c3_nnz.jsonl"] + sorted(glob.glob(f"{O}/c3_cost*.jsonl")):
         r = [x for x in rows if x["world"] == w]
         print(f.split("/")[-1], w, "max", max(x["cold_span_us"] for x in r), [x["cold_span_us"] for x in r], [x["local_nnz"] for x in r])
 PY
+$T 300 python s-blas_amd/tools/bench_spmm_slices.py --worlds 1,2,4,8 > $O/spmm_slices.jsonl 2> $O/spmm_slices.err || { tail -20 $O/spmm_slices.err; exit 1; }
+grep summary $O/spmm_slices.jsonl
