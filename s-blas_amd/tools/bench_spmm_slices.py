@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--ncols", type=int, default=64)
+    ap.add_argument("--split", choices=["rows", "cols"], default="rows",
+                    help="rows (north star; DistSpMM split='rows') or cols (the reference's column split)")
     args = ap.parse_args()
     import torch
     import sblas
@@ -53,6 +55,10 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     c_bytes = 8 * m * n
     for world in [int(w) for w in args.worlds.split(",")]:
+        if args.split == "cols":
+            per = cols_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch, sblas)
+            summary(world, per, c_bytes)
+            continue
         rb = sblas_dist.row_blocks_by_nnz(rp, world)
         per = []
         for d in range(world):
@@ -80,14 +86,56 @@ def main():
                               "algorithmic_bytes": abytes,
                               "roofline_frac": round(abytes / (us * 1e-6) / 8e12, 4)}), flush=True)
             A.close()
-        kmax = max(per)
-        proj = {}
-        for link in (64.0, 153.0):
-            ag = 0.0 if world == 1 else (c_bytes / world) / (link * 1e9) * 1e6
-            step = kmax + (ag + 3.0 if world > 1 else 0.0)
-            proj[f"{int(link)}GBps"] = {"allgather_us": round(ag, 1), "step_us": round(step, 1)}
-        print(json.dumps({"world": world, "summary": True, "kernel_max_us": round(kmax, 1),
-                          "kernel_min_us": round(min(per), 1), "c_bytes": c_bytes, "projection": proj}), flush=True)
+        summary(world, per, c_bytes)
+
+
+def timed_cold(args, torch, stream, scrub, fn):
+    ts = []
+    with torch.cuda.stream(stream):
+        for it in range(args.reps + 2):
+            scrub.sum(dtype=torch.int64)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(500_000)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts[2:])) * 1e3
+
+
+def cols_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch, sblas):
+    """The reference's own split (dspmm_mgpu_baseline.cu:147-150): A
+    replicated, rank d owns B/C columns [d*n/g, (d+1)*n/g) -- its kernel reads
+    all of A and its columns' share of every touched B row."""
+    A = sblas.DeviceCSR.upload(0, k, rp, col, val)
+    per = []
+    for d in range(world):
+        c0, c1 = d * n // world, (d + 1) * n // world
+        Cl = C0[c0:c1].contiguous()
+        us = timed_cold(args, torch, stream, scrub,
+                        lambda: A.spmm(c1 - c0, -0.7, B.data_ptr() + 8 * c0, n, 1, 0.8, Cl.data_ptr(), m,
+                                       stream.cuda_stream))
+        nnz = int(rp[-1])
+        abytes = 12 * nnz + 4 * (m + 1) + 8 * k * (c1 - c0) + 16 * m * (c1 - c0)
+        per.append(us)
+        print(json.dumps({"world": world, "rank": d, "split": "cols", "cols": c1 - c0, "kernel_cold_us": round(us, 1),
+                          "algorithmic_bytes": abytes,
+                          "roofline_frac": round(abytes / (us * 1e-6) / 8e12, 4)}), flush=True)
+    A.close()
+    return per
+
+
+def summary(world, per, c_bytes):
+    kmax = max(per)
+    proj = {}
+    for link in (64.0, 153.0):
+        ag = 0.0 if world == 1 else (c_bytes / world) / (link * 1e9) * 1e6
+        step = kmax + (ag + 3.0 if world > 1 else 0.0)
+        proj[f"{int(link)}GBps"] = {"allgather_us": round(ag, 1), "step_us": round(step, 1)}
+    print(json.dumps({"world": world, "summary": True, "kernel_max_us": round(kmax, 1),
+                      "kernel_min_us": round(min(per), 1), "c_bytes": c_bytes, "projection": proj}), flush=True)
 
 
 if __name__ == "__main__":

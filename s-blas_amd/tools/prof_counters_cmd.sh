@@ -22,4 +22,4 @@ TD_TD_BUSY_sum TD_TC_STALL_sum
 TCC_HIT_sum TCC_MISS_sum TCC_BUSY_avr TCC_TAG_STALL_sum
 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum
 GROUPS
-python3 s-blas_amd/tools/pmc_summary.py --kernel $K --json $O/summary.json $O/p*
+python3 s-blas_amd/tools/pmc_summary.py --kernel "$K" --json $O/summary.json $O/p*
