@@ -363,16 +363,17 @@ void orc_gen_ref(int n, int *coo_row, int *coo_col, double *coo_val)
 }
 
 /* Synthetic generator (our own definition; DESIGN.md "Synthetic").  One
- * SplitMix64 stream per row, state = seed ^ (row+1)*golden.  Columns drawn by
- * 128-bit multiply-high into [0,n), redrawn on a duplicate within the row,
- * then sorted; values drawn afterwards, one per sorted column. */
-static unsigned long long sm64(unsigned long long *s)
+ * SplitMix64 stream per row, started at mix(seed ^ mix((row+1)*golden)) so
+ * that rows draw independent columns.  Columns drawn by 128-bit multiply-high
+ * into [0,n), redrawn on a duplicate within the row, then sorted; values
+ * drawn afterwards, one per sorted column. */
+static unsigned long long mix64(unsigned long long z)
 {
-    unsigned long long z = (*s += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+static unsigned long long sm64(unsigned long long *s) { return mix64(*s += 0x9E3779B97F4A7C15ULL); }
 static double u01(unsigned long long r) { return (double)(r >> 11) * (1.0 / 9007199254740992.0); }
 
 static int cmp_int(const void *a, const void *b)
@@ -396,7 +397,7 @@ void orc_gen_synth(int n, int heavy, int light, int prefix_cols,
     for (int i = 0; i < n; ++i) {
         long long b = rowptr[i];
         int d = (int)(rowptr[i + 1] - b);
-        unsigned long long s = seed ^ ((unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ULL);
+        unsigned long long s = mix64(seed ^ mix64((unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ULL));
         int *c = col + b;
         if (prefix_cols) {
             for (int k = 0; k < d; ++k) c[k] = k;

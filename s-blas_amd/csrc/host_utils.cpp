@@ -609,17 +609,28 @@ int sblas_partition_cost(int m, const long long *rowptr, int g, double w, long l
 }
 
 // ---------------------------------------------------------------------------
-// Synthetic generator (DESIGN.md "Synthetic"): per-row SplitMix64 stream,
-// state = seed ^ (row+1)*0x9E3779B97F4A7C15; columns by 128-bit
-// multiply-high into [0,n), redrawn on duplicates, sorted; then one U[0,1)
-// value per sorted column.
+// Synthetic generator (DESIGN.md "Synthetic"): per-row SplitMix64 stream
+// started at stream_state(seed, row); columns by 128-bit multiply-high into
+// [0,n), redrawn on duplicates, sorted; then one U[0,1) value per sorted
+// column.
 // ---------------------------------------------------------------------------
-static inline unsigned long long splitmix(unsigned long long &s)
+static inline unsigned long long mix64(unsigned long long z)
 {
-    unsigned long long z = (s += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
+}
+static inline unsigned long long splitmix(unsigned long long &s) { return mix64(s += 0x9E3779B97F4A7C15ULL); }
+// Start of row (or column) i's stream.  Rounds 1-4 used seed ^ (i+1)*golden:
+// row i+1's start then often equalled row i's state after one draw (the xor
+// with a small seed commutes with the +golden step unless it meets a carry),
+// so ~1 pair in 8 of consecutive rows shared all but one column and runs of
+// rows repeated one column set (config 2's first 20k heavy rows: 8% distinct
+// columns instead of 64%; round 5, profiles/r05/gen/).  Hashing the index
+// and the seed puts every stream at an independent point of the sequence.
+static inline unsigned long long stream_state(unsigned long long seed, unsigned long long i)
+{
+    return mix64(seed ^ mix64((i + 1) * 0x9E3779B97F4A7C15ULL));
 }
 static inline double to_u01(unsigned long long r) { return (double)(r >> 11) * 0x1.0p-53; }
 
@@ -644,7 +655,7 @@ int sblas_gen_synth_rows(int n, int heavy, int light, int prefix_cols,
     for (int i = row_begin; i < row_end; ++i) {
         const long long b = rowptr[i] - base;
         const int d = (int)(rowptr[i + 1] - rowptr[i]);
-        unsigned long long s = seed ^ ((unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ULL);
+        unsigned long long s = stream_state(seed, (unsigned long long)i);
         int *c = col + b;
         if (prefix_cols) {
             for (int k = 0; k < d; ++k) c[k] = k;
@@ -693,7 +704,7 @@ int sblas_gen_lower_banded(int n, int offd, int band, unsigned long long seed, i
     std::vector<unsigned char> draw((size_t)colptr[n]);
 #pragma omp parallel for schedule(dynamic, 4096)
     for (int j = 0; j < n; ++j) {
-        unsigned long long st = seed ^ ((unsigned long long)(j + 1) * 0x9E3779B97F4A7C15ULL);
+        unsigned long long st = stream_state(seed, (unsigned long long)j);
         const int a = colptr[j], b = colptr[j + 1];
         rowidx[a] = j;
         const long long room = std::min<long long>((long long)n - 1 - j, band);
@@ -811,7 +822,7 @@ int sblas_gen_rmat(int scale, int edge_factor, unsigned long long seed, long lon
     std::vector<double> ev((size_t)E);
 #pragma omp parallel for schedule(static)
     for (long long e = 0; e < E; ++e) {
-        unsigned long long st = seed ^ ((unsigned long long)(e + 1) * 0x9E3779B97F4A7C15ULL);
+        unsigned long long st = stream_state(seed, (unsigned long long)e);
         long long r = 0, c = 0;
         for (int l = 0; l < scale; ++l) {
             const double u = to_u01(splitmix(st));
