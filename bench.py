@@ -428,7 +428,7 @@ def config3_object(N, kern_max, xch_max, step_ms, nnz, dev_bytes, dev_kern, chec
     return out
 
 
-ROW_COST = 6.0  # the cost-weighted split's per-row weight (ctx.hip kCtxRowCost)
+ROW_COST = 3.0  # the cost-weighted split's per-row weight (ctx.hip kCtxRowCost)
 
 
 def cost_weighted(c3):

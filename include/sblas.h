@@ -337,7 +337,7 @@ int sblas_ctx_ngpu(sblas_ctx ctx, int *ngpu);
  * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
  * nnz-balanced split with split rows merged on the device, 2 = the
  * cost-weighted whole-row split (sblas_partition_cost, w =
- * SBLAS_CTX_ROW_COST, 6 by default).  Exchange SBLAS_CTX_ALLGATHER. */
+ * SBLAS_CTX_ROW_COST, 3 by default).  Exchange SBLAS_CTX_ALLGATHER. */
 int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr,
                             const int *col, const double *val, int algo, int partition);
 /* Same with the exchange chosen (sblas_ctx_exchange); SBLAS_CTX_ALLREDUCE

@@ -78,10 +78,11 @@ struct sblas_ctx_s {
 };
 
 // Per-row weight of the cost-weighted partition (2): a row end costs the
-// CSR5 segmented-sum kernel about 6 entries' time -- config 2's N = 8 slices
-// at equal nnz: 552k light rows 55 us, 52k heavy rows 35.5 us
-// (profiles/r04/c5P/), i.e. ~6.73 us per M entries + ~39 us per M rows.
-constexpr double kCtxRowCost = 6.0;
+// CSR5 segmented-sum kernel (over 4 XCD panels) about 3 entries' time --
+// configs[2]'s N = 8 ranks of the uniform config 2 at equal nnz: 552k light
+// rows 60 us, 52k heavy rows 46 us (profiles/r05/c5P/), i.e. ~9 us per M
+// entries + ~28 us per M rows.
+constexpr double kCtxRowCost = 3.0;
 
 // Bound context for the reference API: spMV_mgpu_v1 with ngpu == the bound
 // context's size runs on it (device-resident slices for the call, x
@@ -601,7 +602,7 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
         if (partition == 1) {
             SBLAS_TRY(sblas_partition_nnz(m, C->nnz, rowptr, g, si.data(), ei.data(), sr.data(), er.data(),
                                           sf.data()));
-        } else {  // cost-weighted whole rows: per-row weight SBLAS_CTX_ROW_COST (default 6)
+        } else {  // cost-weighted whole rows: per-row weight SBLAS_CTX_ROW_COST (default 3)
             const char *we = getenv("SBLAS_CTX_ROW_COST");
             SBLAS_TRY(sblas_partition_cost(m, rowptr, g, we ? atof(we) : kCtxRowCost, si.data(), ei.data(),
                                            sr.data(), er.data(), sf.data()));

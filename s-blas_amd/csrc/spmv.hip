@@ -243,12 +243,16 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
 // panels (~4 MiB of x each, P = 4 partials added after): x outgrows an XCD's
 // L2, the rows' columns are scattered (the column probe: most sampled rows
 // span > n/4 of the columns, spread over the eighths) and the matrix is large
-// enough to amortise the partial-y pass (`min_nnz`).  Measured on config 2
-// and its rank-0 slices (cold spans, profiles/r04/slicepanels/): CSR5 286 ->
-// 238 us, N = 4 slice (9.9M nnz) 81 -> 74 us, N = 8 (5M) 47 -> 49 us (so
-// CSR5 from 8M entries, from 4M on short rows: build_csr5_plan); row split
-// 307 -> 244 us, N = 4 84 -> 71 us, N = 8 46 -> 43 us (from 4M entries).
+// enough to amortise the partial-y pass (`min_nnz`).  Measured on the uniform
+// config 2 and its rank slices (cold spans, profiles/r05/sweep/, c5P/; plain
+// / 4 panels): CSR5 567 / 287 us at N = 1, 77 / 46 (heavy) and 80 / 60
+// (light rows) on configs[2]'s N = 8 ranks (5M entries), 45 / 38 on a 2.5M
+// cyclic slice, 29.6 / 30.4 on 1.2M; the row split alike (573 / 310, 76 / 47,
+// 79 / 58, 42 / 32, 24 / 25).  So both take panels from 2M entries.
+// (Rounds 1-4 set 8M / 4M thresholds and 2 panels on short rows on the
+// correlated generator, profiles/r05/gen/, whose heavy rows shared x lines.)
 // `env` = 1 / 0 forces either form.
+constexpr long long kPanelMinNnz = 2000000LL;
 static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, long long min_nnz, bool *use)
 {
     *use = false;
@@ -274,7 +278,7 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
     // first, so a panel plan never keeps a second, unused set of row blocks
     if (!A.pn.degenerate) {
         bool use = false;
-        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", 4000000LL, &use));
+        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", kPanelMinNnz, &use));
         if (use) {
             SBLAS_TRY(build_panel_plan(A, s));
             if (!A.pn.degenerate) {
@@ -1122,21 +1126,15 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     // outgrows an XCD's L2, the rows' columns are scattered (the probe: most
     // sampled rows span > n/4 of the columns, spread over the eighths) and
     // the matrix is large enough to amortise the panels' partial-y pass.
-    // Short rows (< 12 entries on average) take 2 panels from 4M entries:
-    // a 9-entry row cut 4 ways ends ~4 rows per lane and tile; others 4
-    // panels from 8M.  Measured per slice of configs[2]'s nnz split (cold
-    // spans, profiles/r04/c5P/; plain / 2 / 4 panels): full 286 / 251 / 241,
-    // N = 2 heavy 110 / 112 / 95 and light 192 / 161 / 165, N = 4 light
-    // 114 / 95 / 100, N = 8 heavy (5M) 36 / 42 / 38 and light (5M) 62 / 55
-    // / 60 us; R-MAT (15.5 per row) 315 / 248 / 234.  Banded / stencil /
-    // prefix-column matrices keep the plain tiles, whose gathers share lines.
-    // SBLAS_CSR5_PANEL=1 / 0 forces either form, SBLAS_PANELS the count.
+    // P = default_panels (4 on config 2) whatever the row length: on the
+    // uniform config 2 4 panels beat 2 and 8 on short rows (N = 8 light rank
+    // 60 vs 68 / 67 us) and are within 4-8% of 8 on 96-entry rows
+    // (profiles/r05/c5P/).  SBLAS_CSR5_PANEL=1 / 0 forces either form,
+    // SBLAS_PANELS the count.
     (void)pe;
-    const bool short_rows = A.m > 0 && A.nnz < 12LL * A.m;
-    int npanels = short_rows ? std::min(2, default_panels(A)) : default_panels(A);
-    if (getenv("SBLAS_PANELS")) npanels = default_panels(A);
+    const int npanels = default_panels(A);
     bool panels = false;
-    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", short_rows ? 4000000LL : 8000000LL, &panels));
+    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", kPanelMinNnz, &panels));
     if (panels && npanels >= 2 && !(hp && atoi(hp) == 1)) {
         const int rc = build_csr5_panels(A, npanels, s);
         if (rc == SBLAS_OK) return SBLAS_OK;

@@ -210,7 +210,7 @@ def partition_nnz(rowptr: np.ndarray, g: int):
     return si, ei, sr, er, sf
 
 
-def partition_cost(rowptr: np.ndarray, g: int, w: float = 6.0):
+def partition_cost(rowptr: np.ndarray, g: int, w: float = 3.0):
     """Cost-weighted whole-row split (sblas_partition_cost): contiguous row
     ranges balancing sum(nnz_r + w); same outputs as partition_nnz."""
     m = len(rowptr) - 1

@@ -36,7 +36,7 @@ def main():
                     help="cyclic (bench.py's default leg), nnz (configs[2]'s spMV_mgpu_v1 split, the "
                          "config3 leg: ranks hold different row classes, so --ranks all) or cost (the "
                          "cost-weighted whole-row split, config3's cost_weighted leg)")
-    ap.add_argument("--row-cost", type=float, default=6.0, help="per-row weight of --partition cost")
+    ap.add_argument("--row-cost", type=float, default=3.0, help="per-row weight of --partition cost")
     ap.add_argument("--ranks", default="0", help="ranks whose slices to time: a list or 'all'")
     ap.add_argument("--floor", action="store_true",
                     help="also time the slice's streaming floor (slice_floor: one cold read-stream "

@@ -109,8 +109,8 @@ def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
 @pytest.mark.parametrize("world", [4, 8])
 def test_config2_slice_xcd_panel_choice(torch_cuda, sb, orc, cfg2, world):
     """Rank 0's cyclic slice at N = 4 (9.9M nnz) and N = 8 (5M): the row split
-    takes panels from 4M entries, CSR5 from 8M (profiles/r04/slicepanels/);
-    both stay within the bound against the oracle on the slice."""
+    and CSR5 take 4 panels from 2M entries (profiles/r05/c5P/); both stay
+    within the bound against the oracle on the slice."""
     import sblas_dist
     rp = cfg2["rp"]
     plan = sblas_dist.make_cyclic_plan(rp, N2, world)
@@ -123,7 +123,7 @@ def test_config2_slice_xcd_panel_choice(torch_cuda, sb, orc, cfg2, world):
     bound = orc.spmv_bound(lrp, col, val, x.cpu().numpy(), cfg2["alpha"], cfg2["beta"], y0)
     A = sb.DeviceCSR.upload(0, N2, lrp, col, val)
     try:
-        for algo, thr in ((sb.ROWSPLIT, 4_000_000), (sb.CSR5, 8_000_000)):
+        for algo, thr in ((sb.ROWSPLIT, 2_000_000), (sb.CSR5, 2_000_000)):
             A.analyse(algo)
             want_p = 0 if cfg2["prefix"] or int(lrp[-1]) < thr else 4
             assert A.panels(algo) == want_p, (world, algo)
@@ -138,8 +138,8 @@ def test_config2_slice_xcd_panel_choice(torch_cuda, sb, orc, cfg2, world):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
     """configs[2]'s nnz split puts the light rows on the last rank (9-entry
-    rows): CSR5 takes 2 XCD panels there from 4M entries (4 panels from 8M on
-    longer rows), within the bound against the oracle on that slice."""
+    rows): CSR5 takes 4 XCD panels there, as on longer rows, from 2M entries;
+    within the bound against the oracle on that slice."""
     rp = cfg2["rp"]
     _, _, sr, er, _ = sb.partition_nnz(rp, world)
     a, b = int(sr[world - 1]), int(er[world - 1]) + 1
@@ -155,7 +155,7 @@ def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
     A = sb.DeviceCSR.upload(0, N2, lrp, col, val)
     try:
         A.analyse(sb.CSR5)
-        assert A.panels(sb.CSR5) == (0 if cfg2["prefix"] else 2)
+        assert A.panels(sb.CSR5) == (0 if cfg2["prefix"] else 4)
         y = torch_cuda.from_numpy(y0.copy()).cuda()
         A.spmv(sb.CSR5, cfg2["alpha"], x.data_ptr(), cfg2["beta"], y.data_ptr(), 0)
         torch_cuda.cuda.synchronize()
