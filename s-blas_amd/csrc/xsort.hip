@@ -55,6 +55,7 @@
 namespace sblas {
 
 constexpr int kXsThreads = 1024;
+constexpr long long kXsAllWideMaxNnz = 6000000;  // all ranges wide up to this many entries (planner)
 // LDS row accumulators per workgroup: 16384 = 128 KiB (default); an
 // experiment build may raise it towards the 160 KiB of a gfx950 CU
 // (SBLAS_XS_LDS_ROWS=19456: 152 KiB of rows + ~6 KiB of bookkeeping)
@@ -685,7 +686,13 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     int kper = 1;
     if (const char *e = getenv("SBLAS_XS_K")) kper = std::max(1, atoi(e));
     const long long slots = (long long)resident * kper * (P.pair ? 2 : 1);  // sub-items
-    const bool all_wide = getenv("SBLAS_XS_ALLWIDE") && atoi(getenv("SBLAS_XS_ALLWIDE")) != 0;
+    // every range wide (8 XCD-local sub-items + partials per row) on small
+    // matrices: a rank's slice of the uniform config 2 at N = 8 (5.0M
+    // entries) 47.0 -> 41.8 us, N = 16 (2.5M) 33.8 -> 29.9, but N = 4 (9.9M)
+    // 66.8 -> 104 (profiles/r05/sweep2/): the partials (16 B per row and XCD)
+    // outweigh XCD-local gathers beyond ~6M entries.  SBLAS_XS_ALLWIDE=0/1 forces.
+    const char *awe = getenv("SBLAS_XS_ALLWIDE");
+    const bool all_wide = awe ? atoi(awe) != 0 : nnz <= kXsAllWideMaxNnz;
     const bool no_wide = getenv("SBLAS_XS_NOWIDE") && atoi(getenv("SBLAS_XS_NOWIDE")) != 0;
     const bool nosort = getenv("SBLAS_XS_NOSORT") && atoi(getenv("SBLAS_XS_NOSORT")) != 0;
     int rows_cap = (P.pair || P.nt == 512) ? kXsHalfRows : kXsItemRows;
@@ -1004,13 +1011,17 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         P.nitems += P.qlen[k];
     }
     P.grid = std::min(P.nitems, resident);
-    // chunks per dynamic claim: one (finer claims balance the waves and
-    // shorten the last stage; rank 0's cyclic slice of config 2, cold span,
-    // U = 1 vs 2: N = 1 130.4 vs 134.3 us, N = 2 77.2 vs 82.7, N = 4 51.3 vs
-    // 57.0, N = 8 35.6 vs 41.3; profiles/r02/slice/).  SBLAS_XS_U forces it.
+    // Chunks per dynamic claim (SBLAS_XS_U forces it).  Finer claims balance
+    // the waves and shorten the last stage (rounds 2-4, correlated generator:
+    // U = 1 won at every N, profiles/r02/slice/); on the uniform matrix two
+    // chunks per claim win where waves stream many chunks: the uniform
+    // config 2 (~38 chunks per wave) 159.2 -> 156.2 us (three alternating
+    // A/B pairs, profiles/r05/sweep2/); one on small plans (N = 8 slice, ~5
+    // per wave: 46.9 vs 51.5, profiles/r05/sweep/).
     {
         const char *ue = getenv("SBLAS_XS_U");
-        P.u = ue ? std::max(1, std::min(4, atoi(ue))) : 1;
+        const double per_wave = (double)nchunks / ((double)std::max(P.nitems, 1) * (P.nt / 64));
+        P.u = ue ? std::max(1, std::min(4, atoi(ue))) : (per_wave >= 24.0 ? 2 : 1);
     }
     int nstat = 0;
     for (int k = 0; k < 8; ++k) {

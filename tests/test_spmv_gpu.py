@@ -17,17 +17,19 @@ pytestmark = pytest.mark.gpu
 # (algorithm, plan environment).  The panel algorithm (4) picks ~4 MiB of x
 # per panel, i.e. one panel for these small matrices; 3 and 8 panels are
 # forced too so the multi-panel path (interleaved grid + partial reduce) runs.
-# The column-sorted algorithm (5) makes few, narrow ranges for small
-# matrices; a tiny work target forces many ranges, most of them wide (one
-# sub-item per XCD + the partial reduce) and paired with narrow ones, ALLWIDE
-# forces every range with entries through the wide path (wide sub-items paired
-# with each other), and PAIR=0 runs one sub-item per workgroup.  Q = 2 / 3
+# The column-sorted algorithm (5) makes every range wide (one sub-item per
+# XCD + the partial reduce) on matrices of <= 6M entries, so these small
+# cases run the all-wide layout by default; ALLWIDE=0 restores the planner's
+# narrow ranges (few, for small matrices; a tiny work target forces many,
+# most of them wide and paired with narrow ones), and PAIR=0 runs one
+# sub-item per workgroup.  Q = 2 / 3
 # column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
 # cover the wide sub-items' group ranges and the narrow wrap at q > 1.
 ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "3"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "8"}),
          (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
+         (5, {"SBLAS_XS_ALLWIDE": "0"}), (5, {"SBLAS_XS_ALLWIDE": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"}),
@@ -39,7 +41,7 @@ ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (1, {"SBLAS_RS_SEQ": "0"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "2"}),
          (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"})]
 ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
+            "xsort_allwide", "xsort_narrow", "xsort_narrow_w50", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_u2_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
             "rowsplit_panel3"]
@@ -214,7 +216,8 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
 
 
 @pytest.mark.parametrize("env", [{}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"},
-                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}])
+                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_ALLWIDE": "0"},
+                                 {"SBLAS_XS_ALLWIDE": "0", "SBLAS_XS_U": "2"}])
 def test_xsort_relaunch(torch_cuda, sb, orc, monkeypatch, env):
     """The column-sorted kernel's work queues re-arm themselves at the end of
     each launch (no memset): five launches on one plan, each checked."""
