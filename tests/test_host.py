@@ -136,6 +136,27 @@ def test_generator_bit_exact(sb, orc, prefix):
             assert np.all(np.diff(seg) > 0) and seg.min() >= 0 and seg.max() < n
 
 
+def test_generator_rows_independent(sb):
+    """Rows draw independent uniform columns (round 5: rounds 1-4 started row
+    i+1's stream where row i's left off after one draw, so runs of rows
+    shared their column sets; profiles/r05/gen/).  On config 2's first 20k
+    heavy rows and 20k light rows the distinct-column fraction matches
+    uniform draws and consecutive rows share ~nothing."""
+    n = 2_000_000
+    rp = sb.gen_synth_rowptr(n)
+    for a, L in ((0, 96), (1_000_000, 9)):
+        col, _ = sb.gen_synth_rows(n, rp, a, a + 20000)
+        c = col.reshape(-1, L)
+        want = n * (1 - np.exp(-col.size / n)) / col.size
+        assert abs(len(np.unique(col)) / col.size - want) < 0.01
+        shared = [len(np.intersect1d(c[i], c[i + 1])) for i in range(0, len(c) - 1, 7)]
+        assert np.mean(shared) < 0.05 * L and max(shared) <= 3
+    # the SpTRSV stand-in's columns likewise (per-column streams)
+    cp, ri, _ = sb.gen_lower_banded(200000, 5, 80000, 47)
+    both = [len(np.intersect1d(ri[cp[j] + 1:cp[j + 1]], ri[cp[j + 1] + 1:cp[j + 2]])) for j in range(1000, 5000)]
+    assert sum(both) <= 10  # ~25 / 80000 per pair expected
+
+
 def test_config2_shape(sb):
     rp = sb.gen_synth_rowptr(2_000_000)
     assert int(rp[-1]) == 39_750_000  # SURVEY M1-cfg2
