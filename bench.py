@@ -659,6 +659,65 @@ def config5_leg(args, torch, sblas, rank, world, evict, sync_barrier):
     return out
 
 
+STRUCTURED = (("stencil27", "27-point 3-D stencil, 128^3 mesh (FEM-block pattern)", 128),
+              ("stencil7", "7-point 3-D stencil, 160^3 mesh (finite-difference pattern)", 160),
+              ("rmat", "R-MAT power-law graph, 2^21 vertices, edge factor 16", 21))
+
+
+def structured_leg(args, torch, sblas, evict):
+    """North star's ">= 60% of the HBM roofline on fp64 CSR SpMV for
+    SuiteSparse-class matrices at 1 GPU" on every N = 1 line: SuiteSparse
+    itself is not in the container, so the generators' structured stand-ins
+    (sblas_gen_stencil3d, sblas_gen_rmat) run through the same persistent API
+    as the headline -- AUTO's pick, y = alpha*A*x + beta*y, the call's device
+    span (sblas_spmv_timed) after the 1 GiB sweep, mean of --steps -- and the
+    roofline is the same algorithmic-bytes formula over 8 TB/s.  Correctness
+    on these matrices is the -m gpu suite's (tests/test_spmv_gpu.py)."""
+    out = {"what": "SuiteSparse-class stand-ins (north star: >= 0.60 of the HBM roofline at 1 GPU), "
+                   "AUTO's kernel, cold device span, algorithmic bytes / 8 TB/s"}
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.Stream(device=dev)
+    sp = stream.cuda_stream
+    names = {sblas.ROWSPLIT: "rowsplit", sblas.CSR5: "csr5", sblas.PANEL: "panel", sblas.XSORT: "xsort"}
+    for kind, what, size in STRUCTURED:
+        t0 = time.perf_counter()
+        if kind == "rmat":
+            rp, col, val = sblas.gen_rmat(size, 16, seed=50)
+        else:
+            rp, col, val = sblas.gen_stencil3d(size, size, size, int(kind[7:]), seed=49)
+        n, nnz = len(rp) - 1, int(rp[-1])
+        A = sblas.DeviceCSR.upload(dev.index, n, rp, col, val)
+        del rp, col, val
+        try:
+            algo = A.pick(sp)
+            A.analyse(algo, sp)
+            build_s = time.perf_counter() - t0
+            x = torch.from_numpy(sblas.gen_vector(n, 43)).to(dev)
+            y = torch.from_numpy(sblas.gen_vector(n, 44)).to(dev)
+            with torch.cuda.stream(stream):
+                for _ in range(2):
+                    A.spmv(algo, ALPHA, x.data_ptr(), BETA, y.data_ptr(), sp)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(args.steps):
+                evict()
+                torch.cuda.synchronize()
+                ts.append(A.spmv_timed(algo, ALPHA, x.data_ptr(), BETA, y.data_ptr(), sp))
+            t = float(np.mean(ts))
+            abytes = A.algorithmic_bytes(True)
+            out[kind] = {"matrix": what, "n": n, "nnz": nnz, "algo": names.get(algo, str(algo)),
+                         "kernel_ms": round(t, 5), "gflops": round(2.0 * nnz / (t * 1e-3) / 1e9, 3),
+                         "algorithmic_bytes": abytes,
+                         "roofline_frac": round(abytes / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "build_s": round(build_s, 2)}
+            del x, y
+        except Exception as e:  # noqa: BLE001 -- reported, not raised: the headline must not fall with it
+            out[kind] = {"matrix": what, "error": f"{type(e).__name__}: {e}"}
+        finally:
+            A.close()
+    return out
+
+
 def config5_blocks4(args, torch, sblas, cp, ri, vi, n, nnz, bi, xref, gpus, evict):
     """configs[4]'s 4 blocks (sblas_trsv_mgpu, 4 // gpus blocks per GPU), cold."""
     t0 = time.perf_counter()
@@ -952,7 +1011,7 @@ def run_ctx(args) -> int:
         if N > 1:  # beside the literal nnz split: the cost-weighted whole-row split
             config3["cost_weighted"] = cost_weighted(ctx_config3(ctx, args, sblas, n, rowptr, col, val, x_h, evict,
                                                                  delay_us, partition=2))
-    config4 = config5 = None
+    config4 = config5 = structured = None
     if N == 1 and not args.ctx_loopback:  # one device: the same single-GPU legs as the torch driver
         import sblas_dist
         torch.cuda.set_device(0)
@@ -960,6 +1019,8 @@ def run_ctx(args) -> int:
             config4 = config4_leg(args, torch, sblas, sblas_dist, None, 0, 1, 0, evict, sync_all)
         if not args.no_config5:
             config5 = config5_leg(args, torch, sblas, 0, 1, evict, sync_all)
+        if not args.no_structured:
+            structured = structured_leg(args, torch, sblas, evict)
     del scrubs
     total_flops = 2.0 * nnz
     achieved0 = dev_bytes[0] / (dev_kern[0] * 1e-3) / 1e9
@@ -1031,6 +1092,8 @@ def run_ctx(args) -> int:
         out["config4"] = config4
     if config5 is not None:
         out["config5"] = config5
+    if structured is not None:
+        out["structured"] = structured
     out["traffic_source"] = dict(TRAFFIC_NOTES)
     if args.ctx_loopback:
         out["note"] = (f"loopback rehearsal: {N} context ranks on {ndev} GPU(s), collectives as "
@@ -1113,6 +1176,8 @@ def main() -> int:
                     help="skip the BASELINE configs[3] leg (SpMM, rail4284-shaped x 64) every line carries")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip the BASELINE configs[4] leg (sync-free SpTRSV, circuit5M-class) every line carries")
+    ap.add_argument("--no-structured", action="store_true",
+                    help="skip the SuiteSparse-class stand-ins leg (N = 1: stencil27, stencil7, rmat)")
     ap.add_argument("--no-check-legs", action="store_true",
                     help="skip the config4 / config5 post-timing checks (every C entry under the fp64 bound; "
                          "the SpTRSV known answer exactly)")
@@ -1335,6 +1400,9 @@ def main() -> int:
         config4 = config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier)
     if not args.no_config5:
         config5 = config5_leg(args, torch, sblas, rank, world, evict, sync_barrier)
+    structured = None
+    if world == 1 and not args.no_structured:
+        structured = structured_leg(args, torch, sblas, evict)
     del scrub
     peak = measured_peak(torch, sblas, dev, stream) if world == 1 and not args.no_peak else None
 
@@ -1451,6 +1519,8 @@ def main() -> int:
             out["config4"] = config4
         if config5 is not None:
             out["config5"] = config5
+        if structured is not None:
+            out["structured"] = structured
         out["traffic_source"] = dict(TRAFFIC_NOTES)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)

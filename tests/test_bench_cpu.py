@@ -131,6 +131,15 @@ def test_config4_config5_on_by_default():
     assert src.count("if not args.no_config4:") == 2 and src.count("if not args.no_config5:") == 2
 
 
+def test_structured_leg_on_by_default():
+    """Both drivers add the SuiteSparse-class stand-ins (north star's >= 60%
+    target) at N = 1 unless --no-structured is given; three matrices."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('out["structured"] = structured') == 2
+    assert src.count("not args.no_structured") == 2
+    assert [k for k, _, _ in bench.STRUCTURED] == ["stencil27", "stencil7", "rmat"]
+
+
 def test_traffic_requires_matching_library_hash(tmp_path, monkeypatch):
     """roofline.traffic comes from a committed PMC summary only while its
     lib_sha256 stamp equals the loaded libsblas.so's hash."""
