@@ -1000,6 +1000,15 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             q[t % 8].push_back({a0, a1});
         }
     }
+    if (timing) {
+        long long empty_subs = 0;
+        for (int i : wide)
+            for (int k = 0; k < 8; ++k)
+                empty_subs += blk[(size_t)i * G + (size_t)(k + 1) * P.q] == blk[(size_t)i * G + (size_t)k * P.q];
+        fprintf(stderr, "xsort plan: %d ranges, %zu wide (%lld of their %zu sub-items empty), %zu narrow, "
+                        "%lld chunks, G %d, q %d, solo %d\n",
+                I, wide.size(), empty_subs, 8 * wide.size(), nsub.size(), nchunks, G, P.q, (int)P.solo);
+    }
     P.nranges = I;
     P.nwide = (int)wide.size();
     P.nchunks = nchunks;
