@@ -51,6 +51,7 @@ struct sblas_trsv_s {
     unsigned *ctl = nullptr;   // [0] ticket, [kAbort] timeout flag (kCtlBytes block)
     int nlevels = -1;
     int auto_algo = 0;         // sblas_trsv_solve algo 4: the pull executor's ticket order (1 or 3)
+    int pull_threads = 0;      // SBLAS_TRSV_THREADS at create (0: by ticket order, pull_threads())
     // level-set executor (algo 2), built on its first solve: rows in level
     // order (stable by row), the CSR rows copied into that order, level
     // pointers, and the launch schedule (runs of narrow levels -> one
@@ -839,6 +840,29 @@ __global__ __launch_bounds__(1024) void k_trsv_level_grid(
     }
 }
 
+// Threads per pull workgroup (one workgroup per CU, grid_for): the waves
+// spinning on a CU.  Every pending lane polls, and the polls share the
+// memory path with the producers' stores and loads, so fewer waves shorten
+// each dependency hop -- as long as enough rows are in flight to cover a
+// level.  Config-5 stand-in (natural order, 985 levels): 1 / 2 / 3 / 4 waves
+// per CU 2.44 / 2.12 / 2.24 / 2.45 ms; level order (a ticket holds 64 rows of
+// one level): 27-point 100^3 1.79 / 1.92 / 1.99 / 2.03 ms, 7-point 0.81 /
+// 0.85 / 0.87 / 0.89 ms (profiles/r05/trsv_waves/).  SBLAS_TRSV_THREADS
+// (64 / 128 / 192 / 256) overrides.  The multi-device blocks keep 256: four
+// blocks sharing one GPU ran 4.7 ms at 4 waves per CU and 6.2 at 2 (each
+// block then has a quarter of the grid), and one block per GPU is unmeasured
+// here.
+static int pull_threads_env()  // read when a handle is created
+{
+    const char *e = getenv("SBLAS_TRSV_THREADS");
+    const int t = e ? atoi(e) : 0;
+    return t == 64 || t == 128 || t == 192 || t == 256 ? t : 0;
+}
+static int pull_threads(bool level_order, int forced)
+{
+    return forced ? forced : level_order ? 64 : 128;
+}
+
 static int grid_for(int dev)
 {
     hipDeviceProp_t p;
@@ -870,6 +894,7 @@ int sblas_trsv_create(sblas_trsv *out, int device, int n, int nnz, const int *d_
     T->n = n;
     T->nnz = nnz;
     T->substitution = substitution;
+    T->pull_threads = pull_threads_env();
     auto fail = [&](hipError_t e) {
         set_error("sblas_trsv_create: %s", hipGetErrorString(e));
         sblas_trsv_destroy(T);
@@ -1136,9 +1161,10 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     // and deeper lose; profiles/r03/sptrsv_sleep/)
     int slp = algo == 3 ? -6 : 1;
     if (const char *e = getenv("SBLAS_TRSV_SLEEP")) slp = std::max(-10, std::min(64, atoi(e)));
+    const int pth = pull_threads(algo == 3, T->pull_threads);
     if (algo == 3) {  // sync-free pull, tickets in level order
         fill_pending((unsigned long long *)d_x, T->n, s);
-        hipLaunchKernelGGL(k_trsv_pull<true>, dim3(grid), dim3(256), 0, s, T->lrp, T->lcol, T->lval, T->n,
+        hipLaunchKernelGGL(k_trsv_pull<true>, dim3(grid), dim3(pth), 0, s, T->lrp, T->lcol, T->lval, T->n,
                            T->substitution, d_b, (unsigned long long *)d_x, T->ctl, T->lrow, slp);
     } else if (algo == 0) {
         SBLAS_HIP(hipMemsetAsync(T->done, 0, sizeof(int) * T->n, s));
@@ -1147,7 +1173,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
                            T->in_degree, T->n, T->substitution, d_b, d_x, T->done, T->left, T->ctl);
     } else {
         fill_pending((unsigned long long *)d_x, T->n, s);
-        hipLaunchKernelGGL(k_trsv_pull<false>, dim3(grid), dim3(256), 0, s, T->rrowptr, T->rcol, T->rval,
+        hipLaunchKernelGGL(k_trsv_pull<false>, dim3(grid), dim3(pth), 0, s, T->rrowptr, T->rcol, T->rval,
                            T->n, T->substitution, d_b, (unsigned long long *)d_x, T->ctl, nullptr, slp);
     }
     SBLAS_HIP(hipGetLastError());
@@ -1329,6 +1355,7 @@ struct TrsvMgpuDev {
 struct sblas_trsv_mgpu_s {
     int n = 0, rhs = 1, nblocks = 0, ndev = 0;
     bool bwd = false, serial = false, trace = false;
+    int pull_threads = 0;  // SBLAS_TRSV_THREADS at create (0: 256 threads per workgroup)
     std::vector<int> ob;                  // block boundaries in the solve order
     std::vector<TrsvMgpuDev> D;
     std::vector<hipStream_t> streams;     // per block (serial: per device's first block)
@@ -1378,6 +1405,7 @@ int trsv_mgpu_build(sblas_trsv_mgpu_s *H, const int *colptr, const int *rowidx, 
     H->nblocks = nblocks;
     H->ndev = ndev;
     H->serial = getenv("SBLAS_TRSV_MGPU_SERIAL") && atoi(getenv("SBLAS_TRSV_MGPU_SERIAL")) != 0;
+    H->pull_threads = pull_threads_env();
     H->trace = getenv("SBLAS_TRSV_TRACE") != nullptr;
     const int nnz = colptr[n];
     const bool bwd = H->bwd = substitution == 1;
@@ -1513,7 +1541,8 @@ int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solv
         const int grid = H->serial ? grid_for(q.phys) : std::max(1, grid_for(q.phys) / H->on_phys[q.phys]);
         if (nloc > 0 && rhs == 1) {
             TrsvPart P{q.rowptr, q.col, q.val, q.b, q.xs, ngpu, d, ob[d], nloc, n, bwd ? 1 : 0};
-            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(256), 0, H->stream_of(d), P, q.ctl);
+            hipLaunchKernelGGL(k_trsv_pull_part, dim3(grid), dim3(H->pull_threads ? H->pull_threads : 256), 0, H->stream_of(d), P,
+                               q.ctl);
         } else if (nloc > 0) {
             TrsmArgs P{q.rowptr, q.col, q.val, q.b,    q.x, q.xs, ngpu, d, ob[d], nloc, n, rhs, bwd ? 1 : 0, 0,
                        nullptr, 1};

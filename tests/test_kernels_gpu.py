@@ -418,6 +418,45 @@ def test_sptrsv_pull_backoff(torch_cuda, sb, monkeypatch, algo, sleep):
         T.close()
 
 
+@pytest.mark.parametrize("threads", ["64", "128", "192", "256"])
+@pytest.mark.parametrize("algo", [1, 3])
+def test_sptrsv_pull_threads(torch_cuda, sb, monkeypatch, algo, threads):
+    """Waves per CU of the pull executors (SBLAS_TRSV_THREADS, read when the
+    handle is created; defaults 128 natural / 64 level order) change only how
+    many rows are in flight, never the result: exact KAT, and a banded
+    triangle with long dependency chains identical to the default's x."""
+    torch = torch_cuda
+    for name, sub in (("qh768", 0), ("ash85", 1)):
+        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{'fwd' if sub == 0 else 'bwd'}.npz"))
+        cp, ri, cv, b = g["colptr"], g["rowidx"], g["val"], g["b"]
+        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
+        xd = torch.zeros(len(cp) - 1, dtype=torch.float64, device="cuda")
+        monkeypatch.setenv("SBLAS_TRSV_THREADS", threads)
+        T = sb.DeviceTRSV(0, len(cp) - 1, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sub)
+        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(xd.cpu().numpy(), g["x_ref"])  # exact KAT
+        T.close()
+    n = 200_000
+    cp, ri, v = sb.gen_lower_banded(n, 5, 4000, 3)
+    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
+    b = np.bincount(ri, weights=v * (1.0 + cols % 7), minlength=n)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, v, b)]
+    xs = []
+    for th in (None, threads):
+        if th is None:
+            monkeypatch.delenv("SBLAS_TRSV_THREADS", raising=False)
+        else:
+            monkeypatch.setenv("SBLAS_TRSV_THREADS", th)
+        T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 0)
+        xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
+        torch.cuda.synchronize()
+        xs.append(xd.cpu().numpy())
+        T.close()
+    assert np.array_equal(xs[0], xs[1])  # same sums, same order: bit-identical
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     """Random lower-triangular with long chains and a long column/row."""
