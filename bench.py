@@ -498,7 +498,22 @@ def _hold_events(torch, stream, fn):
     return ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
 
 
-def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier):
+_RAIL = {}
+
+
+def _rail_matrix():
+    """configs[3]'s rail4284-shaped stand-in, generated once per process."""
+    if not _RAIL:
+        sys.path.insert(0, os.path.join(ROOT, "s-blas_amd", "tools"))
+        from bench_spmm import rail_like
+        t0 = time.perf_counter()
+        rp, col = rail_like(4284, 1_092_610, 11_279_748, 44)
+        val = np.random.default_rng(45).random(11_279_748)
+        _RAIL.update(rp=rp, col=col, val=val, gen_s=time.perf_counter() - t0)
+    return _RAIL["rp"], _RAIL["col"], _RAIL["val"], _RAIL["gen_s"]
+
+
+def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier, split="rows"):
     """configs[3] on every line: the SpMM, rows of A split
     by nnz over the ranks (B replicated, C row slices all-gathered; the
     reference's dspmm_mgpu_baseline.cu:147-150 splits B/C columns instead),
@@ -506,20 +521,17 @@ def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evic
     hold, HIP events on the launch stream around kernel and all-gather), max
     over ranks; then one fresh product from C0 whose EVERY entry rank 0
     checks against the oracle's csrmm restatement under the per-entry fp64
-    bound (dspmm_baseline_test.cu:544-549 checks every entry too)."""
-    sys.path.insert(0, os.path.join(ROOT, "s-blas_amd", "tools"))
-    from bench_spmm import rail_like
-    m, k, n, nnz = 4284, 1_092_610, 64, 11_279_748
+    bound (dspmm_baseline_test.cu:544-549 checks every entry too).  split
+    "grid" (N > 1, reported beside): row blocks x B/C column groups
+    (sblas_dist.spmm_grid_shape)."""
+    m, k, n = 4284, 1_092_610, 64
     alpha, beta = -0.7, 0.8
-    t0 = time.perf_counter()
-    rp, col = rail_like(m, k, nnz, 44)
-    val = np.random.default_rng(45).random(nnz)
-    gen_s = time.perf_counter() - t0
+    rp, col, val, gen_s = _rail_matrix()
     dev = torch.device("cuda", dev_idx)
     B = torch.rand((k, n), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(45))
     C0 = torch.rand((n, m), dtype=torch.float64, device=dev, generator=torch.Generator(dev).manual_seed(46))
     stream = torch.cuda.Stream(device=dev)
-    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist)
+    op = sblas_dist.DistSpMM(rp, col, val, k, n, world, rank, dev_idx, torch, dist, split=split)
     sp = stream.cuda_stream
     with torch.cuda.stream(stream):
         op.load_c(C0)
@@ -547,8 +559,9 @@ def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evic
         xch.append(b)
         sync_barrier()
     r0, r1 = op.r0, op.r1
+    wc = op.wc if split == "grid" else n  # the rank's C (and B) columns
     lnnz = int(rp[r1] - rp[r0])
-    lbytes = 12 * lnnz + 4 * (r1 - r0 + 1) + 8 * k * n + 16 * (r1 - r0) * n
+    lbytes = 12 * lnnz + 4 * (r1 - r0 + 1) + 8 * k * wc + 16 * (r1 - r0) * wc
     mine = np.array([np.mean(kern), np.mean(xch), np.mean(np.array(kern) + np.array(xch)), lbytes, lnnz])
     per = _gather_rows(torch, dist, dev, mine, world)
     check = None
@@ -567,10 +580,30 @@ def config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evic
             check = {"entries": int(diff.size), "pass": bool(np.all(diff <= bound)),
                      "max_excess_over_bound": float(np.max(diff - bound)),
                      "abs_1e-3": bool(np.all(diff < 1e-3 * np.maximum(1.0, np.abs(want))))}
+    shape = (op.R, op.Cg) if split == "grid" else None
     op.close()
     del B, C0
+    if split == "grid":
+        return config4_grid_object(per, shape, check)
     return config4_object(world, per, first_s, gen_s, check,
                           _stamped_traffic("spmm_ctile") if world == 1 else None)
+
+
+def config4_grid_object(per, shape, check):
+    """`config4.grid` (N > 1): the same step over the 2-D split."""
+    per = np.asarray(per, np.float64)
+    kmax, xmax, smax = (float(per[:, i].max()) for i in range(3))
+    flops = 2.0 * 11_279_748 * 64
+    return {
+        "partition": (f"{shape[0]} row block(s) of A by nnz x {shape[1]} column group(s) of B/C "
+                      "(sblas_dist.spmm_grid_shape), C blocks all-gathered"),
+        "row_blocks": shape[0], "column_groups": shape[1],
+        "kernel_ms_max": round(kmax, 5), "exchange_ms_max": round(xmax, 5), "step_ms": round(smax, 5),
+        "gflops": round(flops / (smax * 1e-3) / 1e9, 3),
+        "kernel_ms_per_rank": [round(float(v), 5) for v in per[:, 0]],
+        "algorithmic_bytes_per_rank": [int(b) for b in per[:, 3]],
+        "check": check,
+    }
 
 
 def config4_object(world, per, first_s, gen_s, check, traffic):
@@ -1398,6 +1431,9 @@ def main() -> int:
     config4 = config5 = None
     if not args.no_config4:
         config4 = config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict, sync_barrier)
+        if world > 1:  # beside the literal row split: row blocks x column groups
+            config4["grid"] = config4_leg(args, torch, sblas, sblas_dist, dist, rank, world, dev_idx, evict,
+                                          sync_barrier, split="grid")
     if not args.no_config5:
         config5 = config5_leg(args, torch, sblas, rank, world, evict, sync_barrier)
     structured = None

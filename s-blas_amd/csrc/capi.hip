@@ -515,7 +515,7 @@ int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb, int
     if (b_layout == 1 && ldb < n) return SBLAS_ERR_INVALID;
     if (ldc < A->m) return SBLAS_ERR_INVALID;
     DeviceGuard g(A->device);
-    if (!A->mm.ready) SBLAS_TRY(build_spmm_plan(*A, (hipStream_t)stream));
+    if (!A->mm.ready) SBLAS_TRY(build_spmm_plan(*A, n, (hipStream_t)stream));
     return launch_spmm(*A, n, alpha, d_B, ldb, b_layout, beta, d_C, ldc, (hipStream_t)stream);
 }
 

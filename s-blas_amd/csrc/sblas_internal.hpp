@@ -323,7 +323,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x,
 int build_xsort_plan(sblas_csr_s &A, hipStream_t s);
 void free_xsort_plan(sblas_csr_s &A);
 
-int build_spmm_plan(sblas_csr_s &A, hipStream_t s);
+int build_spmm_plan(sblas_csr_s &A, int ncols, hipStream_t s);  // C width of the first call
 void free_spmm_plan(sblas_csr_s &A);
 int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B,
                 int ldb, int b_layout, double beta, double *C, int ldc,

@@ -368,25 +368,46 @@ __global__ __launch_bounds__(kCtThreads) void k_spmm_ctile(
     }
 }
 
-// C = alpha * sum_slot part[slot] (+ beta * C), slots in order
+// C = alpha * sum_slot part[slot] (+ beta * C).  A workgroup owns 64 C
+// entries (consecutive in the column-major partials, so every load is one
+// coalesced 512-B run); its 4 waves split the slots (wave w: w, w+4, ...,
+// 8 loads in flight per lane) and wave 0 adds the four sums in wave order:
+// a fixed order, so C is the same on every run.  (One thread per entry
+// walking all slots took 18-34 us on a rank's slice at N = 8, 64-128 slots.)
+constexpr int kCtRedWaves = 4;
 template <bool kBeta>
-__global__ __launch_bounds__(256) void k_spmm_ctreduce(const double *__restrict__ part, int nslot, int m, int n,
-                                                       double alpha, double beta, double *__restrict__ C,
-                                                       long long ldc)
+__global__ __launch_bounds__(64 * kCtRedWaves) void k_spmm_ctreduce(const double *__restrict__ part, int nslot,
+                                                                    int m, int n, double alpha, double beta,
+                                                                    double *__restrict__ C, long long ldc)
 {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (long long)m * n) return;
-    const int c = (int)(i / m), r = (int)(i - (long long)c * m);
+    __shared__ double red[kCtRedWaves][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * 64 + lane;
+    const long long mn = (long long)m * n;
+    const bool live = i < mn;
+    const int c = live ? (int)(i / m) : 0, r = live ? (int)(i - (long long)c * m) : 0;
+    const double *p = part + (long long)c * m + r;
+    const long long qs = (long long)n * m;  // one slot
     double s = 0.0;
-    for (int q = 0; q < nslot; ++q) s += part[((long long)q * n + c) * m + r];
-    double *o = C + (long long)c * ldc + r;
-    *o = kBeta ? alpha * s + beta * *o : alpha * s;
+    if (live) {
+#pragma unroll 8
+        for (int q = w; q < nslot; q += kCtRedWaves) s += p[(long long)q * qs];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && live) {
+        double t = red[0][lane];
+#pragma unroll
+        for (int k = 1; k < kCtRedWaves; ++k) t += red[k][lane];
+        double *o = C + (long long)c * ldc + r;
+        *o = kBeta ? alpha * t + beta * *o : alpha * t;
+    }
 }
 
 // host: the C-tile layout.  Returns SBLAS_ERR_UNSUPPORTED (caller keeps the
 // other forms) when the packed key cannot hold XCD-local column and row.
 static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::vector<int> &hcol,
-                       const std::vector<double> &hval)
+                       const std::vector<double> &hval, int ncols)
 {
     SpmmPlan &P = A.mm;
     const int m = A.m, k = A.n;
@@ -402,8 +423,15 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     const long long nslab = ((long long)k + (1LL << wlog) - 1) >> wlog;
     const long long jc_max = ((nslab + 7) / 8) << wlog;  // XCD-local columns
     if (rbits + 1 > 32 || jc_max > (1LL << (32 - rbits))) return SBLAS_ERR_UNSUPPORTED;
-    // slab sets per XCD: about one workgroup per CU at n = 64 (4 column groups)
-    int ns = std::max(1, 32 / (nrb * 4));
+    // slab sets per XCD: about one workgroup per CU (8 x ns x nrb x column
+    // groups) for the C width of the call that builds the plan -- a rank of
+    // a column split (16 or 32 columns) otherwise filled only 1/4 or 1/2 of
+    // the CUs (config 4's column split at N = 2: 332 us against 345 at N = 1)
+    // (two workgroups per CU where two tiles fit the LDS measured slower on
+    // rank slices: config 4's N = 8 row block 105 -> 127 us, twice the
+    // partial slots for the reduce; profiles/r05/spmm_grid/)
+    const int ncg = std::max(1, (ncols + kCtCols - 1) / kCtCols);
+    int ns = std::max(1, 32 / (nrb * ncg));
     if (const char *e = getenv("SBLAS_SPMM_CTNS")) ns = std::max(1, atoi(e));
     // per-slab entry counts -> contiguous sets of about equal entries per XCD
     std::vector<long long> scount((size_t)nslab, 0);
@@ -572,7 +600,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     return SBLAS_OK;
 }
 
-int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
+int build_spmm_plan(sblas_csr_s &A, int ncols, hipStream_t s)
 {
     if (A.mm.ready) return SBLAS_OK;
     SpmmPlan &P = A.mm;
@@ -648,7 +676,7 @@ int build_spmm_plan(sblas_csr_s &A, hipStream_t s)
     bool ct = P.nmfma == 0 && m > 0 && m <= 16384 && A.n >= (1 << 17);
     if (const char *e = getenv("SBLAS_SPMM_CTILE")) ct = atoi(e) != 0 && P.nmfma == 0 && m > 0;
     if (ct) {
-        const int rc = build_ctile(A, rp, hcol, hval);
+        const int rc = build_ctile(A, rp, hcol, hval, ncols);
         if (rc != SBLAS_OK && rc != SBLAS_ERR_UNSUPPORTED) return rc;
     }
     (void)s;
@@ -753,13 +781,13 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
         hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(kCtThreads), lds, s, P.ct_key, P.ct_val, P.ct_key2,
                            P.ct_val2, P.ct_off, P.ct_ns, P.ct_nrb, P.ct_R, P.ct_rbits, P.ct_wlog, ncg, Brow, ldr,
                            n, A.m, part);
-        const unsigned nb = (unsigned)(((long long)A.m * n + 255) / 256);
+        const unsigned nb = (unsigned)(((long long)A.m * n + 63) / 64);
         if (beta != 0.0)
-            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
-                               beta, C, (long long)ldc);
+            hipLaunchKernelGGL(k_spmm_ctreduce<true>, dim3(nb), dim3(64 * kCtRedWaves), 0, s, part, nslot, A.m, n,
+                               alpha, beta, C, (long long)ldc);
         else
-            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(256), 0, s, part, nslot, A.m, n, alpha,
-                               beta, C, (long long)ldc);
+            hipLaunchKernelGGL(k_spmm_ctreduce<false>, dim3(nb), dim3(64 * kCtRedWaves), 0, s, part, nslot, A.m, n,
+                               alpha, beta, C, (long long)ldc);
         SBLAS_HIP(hipGetLastError());
         return SBLAS_OK;
     }

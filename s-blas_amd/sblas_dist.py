@@ -376,6 +376,18 @@ def row_blocks_by_nnz(rowptr: np.ndarray, world: int) -> np.ndarray:
     return np.maximum.accumulate(rb)
 
 
+def spmm_grid_shape(world: int, ncols: int):
+    """(row blocks, column groups) of DistSpMM's split "grid": the most column
+    groups that leave every rank a multiple of 16 C columns (the C tile's
+    16-column fast path), the rest of the ranks as whole-row blocks by nnz.
+    A rank then reads 1/R of A and its 1/Cg of every B row its rows touch;
+    on configs[3] (64 columns) N = 2 / 4 / 8 -> (1, 2) / (1, 4) / (2, 4)."""
+    for cg in range(world, 0, -1):
+        if world % cg == 0 and ncols % cg == 0 and (ncols // cg) % 16 == 0:
+            return world // cg, cg
+    return world, 1
+
+
 class DistSpMM:
     """One rank's share of C = alpha*A*B + beta*C (B row-major k x ncols on
     every rank; C column-major m x ncols, kept as a (ncols, m) tensor).
@@ -384,7 +396,10 @@ class DistSpMM:
     by nnz, C row slices all-gathered.  split "cols" (the reference's own,
     dspmm_mgpu_baseline.cu:147-150): A replicated, rank d owns C/B columns
     [floor(d*n/g), floor((d+1)*n/g)) -- its C slice is a contiguous block of
-    the (ncols, m) tensor -- and the column slices are all-gathered."""
+    the (ncols, m) tensor -- and the column slices are all-gathered.  split
+    "grid": both at once (spmm_grid_shape): rank d = (row block d // Cg,
+    column group d % Cg) owns that C block; the blocks are all-gathered and
+    placed."""
 
     def __init__(self, rowptr, col, val, k: int, ncols: int, world: int, rank: int, device: int,
                  torch, dist=None, split: str = "rows"):
@@ -394,6 +409,9 @@ class DistSpMM:
         self.split = split
         if split == "cols":
             self._init_cols(rp, col, val, k, device)
+            return
+        if split == "grid":
+            self._init_grid(rp, col, val, k, device)
             return
         self.rb = row_blocks_by_nnz(rp, world)
         r0, r1 = int(self.rb[rank]), int(self.rb[rank + 1])
@@ -422,15 +440,46 @@ class DistSpMM:
         self.c_full = torch.zeros((n, m), dtype=f64, device=dev)
         self.stride = m
 
+    def _init_grid(self, rp, col, val, k, device):
+        torch, n, g = self.torch, self.ncols, self.world
+        self.R, self.Cg = spmm_grid_shape(g, n)
+        self.rb = row_blocks_by_nnz(rp, self.R)
+        self.cb = [c * n // self.Cg for c in range(self.Cg + 1)]
+        ri, ci = self.rank // self.Cg, self.rank % self.Cg
+        self.r0, self.r1 = int(self.rb[ri]), int(self.rb[ri + 1])
+        self.c0, self.c1 = self.cb[ci], self.cb[ci + 1]
+        i0, i1 = int(rp[self.r0]), int(rp[self.r1])
+        self.A = sblas.DeviceCSR.upload_slice(device, k, rp, np.ascontiguousarray(col, np.int32),
+                                              np.ascontiguousarray(val, np.float64), self.r0, self.r1, i0, i1)
+        self.stride = int(max(1, np.diff(self.rb).max()))
+        self.wc = n // self.Cg
+        dev = torch.device("cuda", device)
+        f64 = torch.float64
+        self.c_local = torch.zeros((self.wc, self.stride), dtype=f64, device=dev)  # ld = stride
+        self.gathered = torch.zeros((g, self.wc, self.stride), dtype=f64, device=dev)
+        self.c_full = torch.zeros((n, self.m), dtype=f64, device=dev)
+
+    def _grid_block(self, d):
+        ri, ci = d // self.Cg, d % self.Cg
+        return int(self.rb[ri]), int(self.rb[ri + 1]), self.cb[ci], self.cb[ci + 1]
+
     def load_c(self, c_full) -> None:
         """Set C (a (ncols, m) device tensor) as the next call's input."""
         self.c_full.copy_(c_full)
+        if self.split == "grid":
+            self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[self.c0:self.c1, self.r0:self.r1])
+            return
         if self.split == "cols":
             self.c_local[: self.c1 - self.c0].copy_(self.c_full[self.c0:self.c1])
             return
         self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[:, self.r0:self.r1])
 
     def kernel(self, alpha: float, B, beta: float, stream=None) -> None:
+        if self.split == "grid":  # rows [r0, r1) x B/C columns [c0, c1), ld = ncols
+            if self.r1 > self.r0:
+                self.A.spmm(self.wc, alpha, B.data_ptr() + 8 * self.c0, self.ncols, 1, beta,
+                            self.c_local.data_ptr(), self.stride, stream)
+            return
         if self.split == "cols":
             dn = self.c1 - self.c0
             if dn > 0 and self.m > 0:  # B[:, c0:c1] row-major with ld = ncols
@@ -443,6 +492,19 @@ class DistSpMM:
 
     def exchange(self) -> None:
         if self.world == 1:
+            return
+        if self.split == "grid":
+            if self.dist.get_backend() == "nccl":
+                self.dist.all_gather_into_tensor(self.gathered.view(-1), self.c_local.reshape(-1))
+            else:  # gloo rehearsal (CPU staging)
+                parts = [torch_zeros_like_cpu(self.c_local) for _ in range(self.world)]
+                self.dist.all_gather(parts, self.c_local.cpu())
+                self.gathered.copy_(self.torch.stack(parts).to(self.gathered.device))
+            for d in range(self.world):
+                r0, r1, c0, c1 = self._grid_block(d)
+                if r1 > r0:
+                    self.c_full[c0:c1, r0:r1].copy_(self.gathered[d, :, : r1 - r0])
+            self.c_local[:, : self.r1 - self.r0].copy_(self.c_full[self.c0:self.c1, self.r0:self.r1])
             return
         if self.split == "cols":
             if self.dist.get_backend() == "nccl":

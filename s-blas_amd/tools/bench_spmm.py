@@ -130,7 +130,7 @@ def main():
                     help="rank 0 compares EVERY entry of C with the oracle (orc_spmm_omp) under the "
                          "per-entry fp64 bound (DESIGN.md §3), as dspmm_baseline_test.cu:544-549 "
                          "checks every entry; test infrastructure, after the timed steps")
-    ap.add_argument("--split", choices=["rows", "cols"], default="rows",
+    ap.add_argument("--split", choices=["rows", "cols", "grid"], default="rows",
                     help="rows: whole-row blocks of A by nnz (north star); cols: A replicated, "
                          "B/C columns split (the reference's dspmm_mgpu_baseline.cu:147-150)")
     args = ap.parse_args()
@@ -258,6 +258,8 @@ def main():
                        "partition": ("single GPU" if world == 1 else
                                      "whole-row blocks by nnz, B replicated, C all-gathered"
                                      if args.split == "rows" else
+                                     "row blocks by nnz x B/C column groups, C blocks all-gathered"
+                                     if args.split == "grid" else
                                      "A replicated, B/C column slices, C all-gathered"),
                        "mfma_fill_threshold": os.environ.get("SBLAS_SPMM_MFMA_FILL", "0.08")},
             "roofline": {"bound": "hbm", "achieved": round(abytes / kern_max / 1e6, 1), "peak": 8000.0,

@@ -37,8 +37,9 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--ncols", type=int, default=64)
-    ap.add_argument("--split", choices=["rows", "cols"], default="rows",
-                    help="rows (north star; DistSpMM split='rows') or cols (the reference's column split)")
+    ap.add_argument("--split", choices=["rows", "cols", "grid"], default="rows",
+                    help="rows (north star; DistSpMM split='rows'), cols (the reference's column split) "
+                         "or grid (row blocks x column groups, sblas_dist.spmm_grid_shape)")
     args = ap.parse_args()
     import torch
     import sblas
@@ -57,6 +58,11 @@ def main():
     for world in [int(w) for w in args.worlds.split(",")]:
         if args.split == "cols":
             per = cols_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch, sblas)
+            summary(world, per, c_bytes)
+            continue
+        if args.split == "grid":
+            per = grid_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch, sblas,
+                              sblas_dist)
             summary(world, per, c_bytes)
             continue
         rb = sblas_dist.row_blocks_by_nnz(rp, world)
@@ -124,6 +130,32 @@ def cols_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch,
                           "algorithmic_bytes": abytes,
                           "roofline_frac": round(abytes / (us * 1e-6) / 8e12, 4)}), flush=True)
     A.close()
+    return per
+
+
+def grid_slices(args, world, m, k, n, rp, col, val, B, C0, scrub, stream, torch, sblas, sblas_dist):
+    """Row blocks by nnz x column groups (DistSpMM split "grid"): rank d's
+    rows of A times its columns of B into its C block (ld = rows)."""
+    R, Cg = sblas_dist.spmm_grid_shape(world, n)
+    rb = sblas_dist.row_blocks_by_nnz(rp, R)
+    per = []
+    for d in range(world):
+        r0, r1 = int(rb[d // Cg]), int(rb[d // Cg + 1])
+        c0, c1 = d % Cg * n // Cg, (d % Cg + 1) * n // Cg
+        A = sblas.DeviceCSR.upload_slice(0, k, rp, col, val, r0, r1, int(rp[r0]), int(rp[r1]))
+        stride = max(1, r1 - r0)
+        Cl = C0[c0:c1, r0:r1].contiguous()
+        us = timed_cold(args, torch, stream, scrub,
+                        lambda: A.spmm(c1 - c0, -0.7, B.data_ptr() + 8 * c0, n, 1, 0.8, Cl.data_ptr(), stride,
+                                       stream.cuda_stream))
+        lnnz = int(rp[r1] - rp[r0])
+        abytes = 12 * lnnz + 4 * (r1 - r0 + 1) + 8 * k * (c1 - c0) + 16 * (r1 - r0) * (c1 - c0)
+        per.append(us)
+        print(json.dumps({"world": world, "rank": d, "split": "grid", "shape": [R, Cg], "rows": r1 - r0,
+                          "cols": c1 - c0, "nnz": lnnz, "kernel_cold_us": round(us, 1),
+                          "algorithmic_bytes": abytes,
+                          "roofline_frac": round(abytes / (us * 1e-6) / 8e12, 4)}), flush=True)
+        A.close()
     return per
 
 

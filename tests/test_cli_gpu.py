@@ -205,25 +205,27 @@ def test_config3_two_ranks(extra):
         assert sum(c3["nnz_per_device"]) == 39_750_000
 
 
-@pytest.mark.parametrize("split", ["rows", "cols"])
-@pytest.mark.parametrize("ranks", [2, 3])
-def test_spmm_multi_rank_config4(split, ranks):
-    """sblas_dist.DistSpMM on 2 and 3 ranks (torchrun children, gloo exchange,
+@pytest.mark.parametrize("split,ranks,ncols", [("rows", 2, 64), ("rows", 3, 64), ("cols", 2, 64), ("cols", 3, 64),
+                                               ("grid", 2, 64), ("grid", 4, 32)])
+def test_spmm_multi_rank_config4(split, ranks, ncols):
+    """sblas_dist.DistSpMM on 2-4 ranks (torchrun children, gloo exchange,
     HIP kernels) at BASELINE configs[3]'s full size (rail4284-shaped, 4,284 x
-    1,092,610, 11.28M nnz, 64 columns): the north star's row blocks and the
-    reference's column split.  Rank 0 compares EVERY entry of the assembled C
-    with the oracle (orc_spmm_omp) under the per-entry fp64 bound, as
-    dspmm_baseline_test.cu:544-549 checks every entry."""
+    1,092,610, 11.28M nnz, 64 columns): the north star's row blocks, the
+    reference's column split, and the 2-D grid (2 ranks: 2 column groups; 4
+    ranks at 32 columns: 2 row blocks x 2 column groups).  Rank 0 compares
+    EVERY entry of the assembled C with the oracle (orc_spmm_omp) under the
+    per-entry fp64 bound, as dspmm_baseline_test.cu:544-549 checks every
+    entry."""
     args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
             "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
             os.path.join(ROOT, "s-blas_amd", "tools", "bench_spmm.py"), "--steps", "2", "--warmup", "1",
-            "--dist-backend", "gloo", "--split", split, "--check", "--no-cpu-baseline"]
+            "--dist-backend", "gloo", "--split", split, "--check", "--no-cpu-baseline", "--ncols", str(ncols)]
     rc, out, err = run(args, timeout=115)
     assert rc == 0, out[-3000:] + err[-3000:]
     res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert res["n_gpus"] == ranks and res["config"]["nnz"] == 11_279_748, res
     chk = res["check_vs_oracle"]
-    assert chk["entries"] == 4284 * 64 and chk["pass"] and chk["abs_1e-3"], chk
+    assert chk["entries"] == 4284 * ncols and chk["pass"] and chk["abs_1e-3"], chk
 
 
 def test_torchrun_8_ranks_full_size():

@@ -216,3 +216,70 @@ def test_gloo_spmm_protocol(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+def test_spmm_grid_shape():
+    """DistSpMM split "grid": the most column groups that keep a multiple of
+    16 C columns per rank, the rest as row blocks."""
+    import sblas_dist
+    g = sblas_dist.spmm_grid_shape
+    assert [g(w, 64) for w in (1, 2, 3, 4, 6, 8, 16)] == [(1, 1), (1, 2), (3, 1), (1, 4), (3, 2), (2, 4), (4, 4)]
+    assert g(8, 100) == (8, 1) and g(8, 128) == (1, 8) and g(2, 16) == (2, 1)
+
+
+def _spmm_grid_worker(rank, world, port, result_q):
+    """SpMM grid protocol: rank d owns the C block (row block d // Cg by nnz)
+    x (column group d % Cg), computed from its rows of A and its columns of
+    B, all-gathered as equal-shape (wc x stride) buffers and placed -- as
+    sblas_dist.DistSpMM(split="grid") does on the GPU.  The rank-local
+    product is the oracle (checker)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import orc
+    import sblas_dist
+    rng = np.random.default_rng(4)
+    m, k = 257, 390
+    ncols = 64 if world == 2 else 32  # (1, 2) at 2 ranks; (2, 2) at 4: row blocks AND column groups
+    lens = rng.integers(0, 30, m)
+    lens[7] = 300
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(k, L, replace=False)) for L in lens]).astype(np.int32)
+    val = rng.standard_normal(int(rp[-1]))
+    B = rng.standard_normal((k, ncols))
+    C0 = rng.standard_normal((m, ncols))
+    R, Cg = sblas_dist.spmm_grid_shape(world, ncols)
+    rb = sblas_dist.row_blocks_by_nnz(rp, R)
+    cb = [c * ncols // Cg for c in range(Cg + 1)]
+    wc, stride = ncols // Cg, int(max(1, np.diff(rb).max()))
+    blk = lambda d: (int(rb[d // Cg]), int(rb[d // Cg + 1]), cb[d % Cg], cb[d % Cg + 1])  # noqa: E731
+    r0, r1, c0, c1 = blk(rank)
+    lrp = rp[r0:r1 + 1] - rp[r0]
+    part = orc.spmm(r1 - r0, wc, k, -0.7, lrp, col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]],
+                    np.ascontiguousarray(B[:, c0:c1]), 0.8,
+                    np.ascontiguousarray(C0[r0:r1, c0:c1])) if r1 > r0 else np.zeros((0, wc))
+    buf = torch.zeros((wc, stride), dtype=torch.float64)
+    buf[:, : r1 - r0] = torch.from_numpy(np.ascontiguousarray(part.T))
+    out = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf)
+    C = np.zeros((ncols, m))
+    for d in range(world):
+        a, b, ca, cb_ = blk(d)
+        C[ca:cb_, a:b] = out[d].numpy()[:, : b - a]
+    want = orc.spmm(m, ncols, k, -0.7, rp, col, val, B, 0.8, C0).T
+    result_q.put((rank, bool(np.allclose(C, want, rtol=1e-12, atol=1e-12))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_spmm_grid_protocol(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spmm_grid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
