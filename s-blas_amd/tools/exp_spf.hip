@@ -5,7 +5,7 @@
 // wave touches the span's lines with scalar loads up to `dist` bytes ahead of
 // the vector front (an LDS counter).  Modes: 0 vector only, 1 vector + scalar
 // prefetch, 2 scalar touch only (bytes covered / time).
-// Build: hipcc --offload-arch=gfx950 -O3 spf.hip -o spf ; run: ./spf
+// Build: hipcc --offload-arch=gfx950 -O3 exp_spf.hip -o exp_spf ; run: ./exp_spf
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>

@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/r05_spmm
 mkdir -p $O
 T="timeout -k 10"
-$T 120 s-blas_amd/tools/exp/spf > $O/spf.jsonl 2>&1 || exit 1
+$T 120 s-blas_amd/tools/exp_spf > $O/spf.jsonl 2>&1 || exit 1
 $T 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_configs_gpu.py -x -q --timeout 120 --timeout-method thread -k "spmm" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for r in 1 2; do
