@@ -3,7 +3,11 @@
 # default bench command -> profiles/pmc_{xsort,csr5,rowsplit,spmm_ctile}.json
 # (stamped with the libsblas.so sha256 they ran), then the default bench line
 # (whose roofline.traffic those stamps now validate), rocprofv3 kernel-trace
-# stats of that same command, and the ctx driver's N = 1 line.
+# stats of that same command (headline_kernels.json: the headline's own xsort
+# launches; the stats csv also averages in the structured leg's), and the ctx
+# driver's N = 1 line.  gpurun returns only gpurun_out/: copy
+# gpurun_out/r05_end/pmc_*.json to profiles/ afterwards (the stamped summaries
+# bench.py reads).
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05_end
@@ -23,5 +27,6 @@ for a in xsort csr5 rowsplit spmm_ctile; do cp $O/pmc_$a.json profiles/pmc_$a.js
 $T 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
 $T 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
 $T 300 python bench.py --driver ctx --no-cpu-baseline > $O/bench_ctx1.json 2> $O/bench_ctx1.err || { tail -20 $O/bench_ctx1.err; exit 1; }
+python3 s-blas_amd/tools/headline_kernels.py $O/prof/run_kernel_trace.csv --out $O/headline_kernels.json > /dev/null || exit 1
 for a in xsort csr5 rowsplit spmm_ctile; do python3 -c "import json;d=json.load(open('$O/pmc_$a.json'));print('$a', round(d['traffic_over_algorithmic'],3), round(d['l2_hit_rate'],3))"; done
 python3 -c "import json;d=json.loads(open('$O/bench_default.json').read().strip().splitlines()[-1]);print(d['value'], d['ms_per_step'], d['roofline'], d['traffic_source'], d['config3']['kernel_ms_max'], d['config4']['kernel_ms_max'], d['config5']['ms'], d['cpu_baseline']['value'])"
