@@ -131,6 +131,18 @@ def test_config4_config5_on_by_default():
     assert src.count("if not args.no_config4:") == 2 and src.count("if not args.no_config5:") == 2
 
 
+def test_config4_grid_object_and_call():
+    """At N > 1 the SpMM leg reports the 2-D grid split beside the row split
+    (`config4.grid`), from the same per-rank rows as config4_object."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'config4["grid"] = config4_leg(' in src and 'split="grid"' in src
+    per = [[0.08, 0.01, 0.09, 2.0e8, 5_639_874], [0.07, 0.01, 0.08, 2.0e8, 5_639_874]]
+    g = bench.config4_grid_object(per, (1, 2), {"pass": True, "entries": 4284 * 64})
+    assert g["row_blocks"] == 1 and g["column_groups"] == 2
+    assert g["kernel_ms_max"] == 0.08 and g["step_ms"] == 0.09 and g["check"]["pass"]
+    assert g["gflops"] > 0 and len(g["kernel_ms_per_rank"]) == 2
+
+
 def test_structured_leg_on_by_default():
     """Both drivers add the SuiteSparse-class stand-ins (north star's >= 60%
     target) at N = 1 unless --no-structured is given; three matrices."""
