@@ -714,14 +714,15 @@ def structured_leg(args, torch, sblas, evict):
     names = {sblas.ROWSPLIT: "rowsplit", sblas.CSR5: "csr5", sblas.PANEL: "panel", sblas.XSORT: "xsort"}
     for kind, what, size in STRUCTURED:
         t0 = time.perf_counter()
-        if kind == "rmat":
-            rp, col, val = sblas.gen_rmat(size, 16, seed=50)
-        else:
-            rp, col, val = sblas.gen_stencil3d(size, size, size, int(kind[7:]), seed=49)
-        n, nnz = len(rp) - 1, int(rp[-1])
-        A = sblas.DeviceCSR.upload(dev.index, n, rp, col, val)
-        del rp, col, val
+        A = None
         try:
+            if kind == "rmat":
+                rp, col, val = sblas.gen_rmat(size, 16, seed=50)
+            else:
+                rp, col, val = sblas.gen_stencil3d(size, size, size, int(kind[7:]), seed=49)
+            n, nnz = len(rp) - 1, int(rp[-1])
+            A = sblas.DeviceCSR.upload(dev.index, n, rp, col, val)
+            del rp, col, val
             algo = A.pick(sp)
             A.analyse(algo, sp)
             build_s = time.perf_counter() - t0
@@ -747,7 +748,8 @@ def structured_leg(args, torch, sblas, evict):
         except Exception as e:  # noqa: BLE001 -- reported, not raised: the headline must not fall with it
             out[kind] = {"matrix": what, "error": f"{type(e).__name__}: {e}"}
         finally:
-            A.close()
+            if A is not None:
+                A.close()
     return out
 
 
