@@ -45,6 +45,10 @@ def test_bench_ctx_driver(algo, partition, exchange):
     c3 = line["config3"]
     assert set(CONFIG3_KEYS) <= set(c3), c3
     assert c3["check"] is True and c3["algo"] == "csr5" and c3["n_gpus"] == 1
+    # the north star's SuiteSparse-class stand-ins ride on every N = 1 line
+    st = line["structured"]
+    for kind in ("stencil27", "stencil7", "rmat"):
+        assert "error" not in st[kind] and 0.0 < st[kind]["roofline_frac"] < 1.0, st[kind]
 
 
 @pytest.mark.parametrize("gpus,algo,partition,exchange", [
