@@ -56,6 +56,7 @@ namespace sblas {
 
 constexpr int kXsThreads = 1024;
 constexpr long long kXsAllWideMaxNnz = 6000000;  // all ranges wide up to this many entries (planner)
+constexpr long long kXs768MinNnz = 20000000;     // 768-thread workgroups from this many entries (planner)
 // LDS row accumulators per workgroup: 16384 = 128 KiB (default); an
 // experiment build may raise it towards the 160 KiB of a gfx950 CU
 // (SBLAS_XS_LDS_ROWS=19456: 152 KiB of rows + ~6 KiB of bookkeeping)
@@ -356,8 +357,8 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     double alpha, double beta,
                                                     double *__restrict__ y)
 {
-    static_assert(kWG == 1024 || (kWG == 512 && !kPair), "workgroup shapes");
-    __shared__ double acc_all[kWG == 1024 ? kXsRows : kXsHalfRows];
+    static_assert(kWG == 1024 || (kWG == 768 && kPair) || (kWG == 512 && !kPair), "workgroup shapes");
+    __shared__ double acc_all[kWG >= 768 ? kXsRows : kXsHalfRows];
     __shared__ long long s_bnd_all[2][256];
     __shared__ long long s_rec_all[2][128 + 5];
     __shared__ unsigned long long s_tend[2];
@@ -667,18 +668,31 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // workgroup shape (SBLAS_XS_WG / SBLAS_XS_PAIR select the experiments'
     // alternatives); resident workgroups = item slots, a paired item holds
     // two sub-items
-    P.nt = kXsThreads;
-    if (const char *e = getenv("SBLAS_XS_WG")) P.nt = atoi(e) == 512 ? 512 : kXsThreads;
-    P.pair = P.nt == kXsThreads && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
+    // Workgroup: two 6-wave teams (768 threads, 3 waves per SIMD, ~170 VGPRs
+    // a wave) from kXs768MinNnz entries, two 8-wave teams (1024) below.  The
+    // wider register budget lets the compiler keep more of the stream in
+    // flight: 27-point 128^3 129.4-129.9 -> 120.0-122.0 us, 7-point 160^3
+    // 86.7 -> 82.7-83.7, config 2 and R-MAT unchanged; rank slices of 5-10M
+    // entries lost 5-7% (profiles/r05/wg768/).  SBLAS_XS_WG = 512 / 768 /
+    // 1024 forces the shape (512: two unpaired workgroups per CU).
+    P.nt = nnz >= kXs768MinNnz ? 768 : kXsThreads;
+    if (const char *e = getenv("SBLAS_XS_WG")) P.nt = atoi(e) == 512 ? 512 : atoi(e) == 768 ? 768 : kXsThreads;
+    P.pair = P.nt >= 768 && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
+    if (P.nt == 768 && !P.pair) P.nt = kXsThreads;
+    if (P.nt == 768 && getenv("SBLAS_XS_TRACE")) P.nt = kXsThreads;  // the timeline twins are 1024-thread
     P.split = 8;  // waves of the first (narrow) team of a pair: 5, 6, 7 or 8
     if (const char *e = getenv("SBLAS_XS_SPLIT")) P.split = std::min(8, std::max(5, atoi(e)));
     P.dyn = P.pair && P.split == 8 && !(getenv("SBLAS_XS_DYN") && atoi(getenv("SBLAS_XS_DYN")) == 0);
+    if (P.nt == 768 && !P.dyn) P.nt = kXsThreads;  // the 768 shape has the dynamic-claim kernel only
     int dev = 0, ncu = 0, per_cu = 0;
     SBLAS_HIP(hipGetDevice(&dev));
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (P.nt == 512)
         SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, k_spmv_xsort<true, 0, 512, false>, 512, 0));
+    else if (P.nt == 768)
+        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, k_spmv_xsort<true, 0, 768, true, 6, false, true, 2>, 768, 0));
     else
         SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, k_spmv_xsort<true, 0, kXsThreads, true>, kXsThreads, 0));
@@ -1200,8 +1214,19 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         if (mode == 16 && xu == 1) kern = XS_DYN(16, 1);  // experiment: L2-resident gathers
 #undef XS_DYN
     }
+    if (P.nt == 768) {  // 6 + 6 waves, U = P.u chunks per claim
+        const int xu = P.u;
+        if (b) kern = xu == 1 ? k_spmv_xsort<true, 0, 768, true, 6, false, true, 1>
+                      : xu == 3 ? k_spmv_xsort<true, 0, 768, true, 6, false, true, 3>
+                      : xu == 4 ? k_spmv_xsort<true, 0, 768, true, 6, false, true, 4>
+                                : k_spmv_xsort<true, 0, 768, true, 6, false, true, 2>;
+        else kern = xu == 1 ? k_spmv_xsort<false, 0, 768, true, 6, false, true, 1>
+                    : xu == 3 ? k_spmv_xsort<false, 0, 768, true, 6, false, true, 3>
+                    : xu == 4 ? k_spmv_xsort<false, 0, 768, true, 6, false, true, 4>
+                              : k_spmv_xsort<false, 0, 768, true, 6, false, true, 2>;
+    }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
-    if (trace_path && mode == 0 && P.split == 8) {  // debugging aid: the timeline-stamping twins
+    if (trace_path && mode == 0 && P.split == 8 && P.nt != 768) {  // debugging aid: the timeline-stamping twins
         if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
         else if (P.pair && P.dyn && xu == 1)
             kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1> : k_spmv_xsort<false, 0, W, true, 8, true, true, 1>;

@@ -31,7 +31,8 @@ ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
          (5, {"SBLAS_XS_ALLWIDE": "0"}), (5, {"SBLAS_XS_ALLWIDE": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_WG": "768"}),
+         (5, {"SBLAS_XS_WG": "768", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_WG": "768", "SBLAS_XS_SOLO": "1"}),
          (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_Q": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_Q": "3"}),
          (5, {"SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
@@ -41,7 +42,8 @@ ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (1, {"SBLAS_RS_SEQ": "0"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "2"}),
          (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"})]
 ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide", "xsort_narrow", "xsort_narrow_w50", "xsort_unpaired", "xsort_wg512", "xsort_static", "xsort_static_w50",
+            "xsort_allwide", "xsort_narrow", "xsort_narrow_w50", "xsort_unpaired", "xsort_wg512", "xsort_wg768",
+            "xsort_wg768_w50", "xsort_wg768_solo", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_u2_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
             "rowsplit_panel3"]
