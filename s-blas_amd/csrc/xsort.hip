@@ -56,7 +56,6 @@ namespace sblas {
 
 constexpr int kXsThreads = 1024;
 constexpr long long kXsAllWideMaxNnz = 6000000;  // all ranges wide up to this many entries (planner)
-constexpr long long kXs768MinNnz = 20000000;     // 768-thread workgroups from this many entries (planner)
 // LDS row accumulators per workgroup: 16384 = 128 KiB (default); an
 // experiment build may raise it towards the 160 KiB of a gfx950 CU
 // (SBLAS_XS_LDS_ROWS=19456: 152 KiB of rows + ~6 KiB of bookkeeping)
@@ -357,8 +356,8 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
                                                     double alpha, double beta,
                                                     double *__restrict__ y)
 {
-    static_assert(kWG == 1024 || (kWG == 768 && kPair) || (kWG == 512 && !kPair), "workgroup shapes");
-    __shared__ double acc_all[kWG >= 768 ? kXsRows : kXsHalfRows];
+    static_assert(kWG == 1024 || (kWG == 768 && kPair) || kWG == 512, "workgroup shapes");
+    __shared__ double acc_all[(kWG >= 768 || kPair) ? kXsRows : kXsHalfRows];
     __shared__ long long s_bnd_all[2][256];
     __shared__ long long s_rec_all[2][128 + 5];
     __shared__ unsigned long long s_tend[2];
@@ -668,26 +667,35 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // workgroup shape (SBLAS_XS_WG / SBLAS_XS_PAIR select the experiments'
     // alternatives); resident workgroups = item slots, a paired item holds
     // two sub-items
-    // Workgroup: two 6-wave teams (768 threads, 3 waves per SIMD, ~170 VGPRs
-    // a wave) from kXs768MinNnz entries, two 8-wave teams (1024) below.  The
-    // wider register budget lets the compiler keep more of the stream in
-    // flight: 27-point 128^3 129.4-129.9 -> 120.0-122.0 us, 7-point 160^3
-    // 86.7 -> 82.7-83.7, config 2 and R-MAT unchanged; rank slices of 5-10M
-    // entries lost 5-7% (profiles/r05/wg768/).  SBLAS_XS_WG = 512 / 768 /
-    // 1024 forces the shape (512: two unpaired workgroups per CU).
-    P.nt = nnz >= kXs768MinNnz ? 768 : kXsThreads;
-    if (const char *e = getenv("SBLAS_XS_WG")) P.nt = atoi(e) == 512 ? 512 : atoi(e) == 768 ? 768 : kXsThreads;
-    P.pair = P.nt >= 768 && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
+    // Workgroup: two 4-wave teams (512 threads, 2 waves per SIMD, up to 256
+    // VGPRs a wave) -- the register budget lets the compiler keep more of
+    // the stream in flight than two 8-wave teams (1024 threads, 128 VGPRs) or
+    // two 6-wave teams (768, ~170): with 2 chunks per claim, config 2 N = 1 /
+    // 2 / 4 / 8 150.6-152.5 / 96.4-96.7 / 65.5-65.6 / 40.7-40.8 us against
+    // 153.0-153.3 / 99.1 / 66.3-66.9 / 42.1-42.5, 27-point 128^3 117 vs 121,
+    // 7-point 160^3 83 vs 85, R-MAT equal (profiles/r05/wg512p/).
+    // SBLAS_XS_WG = 512p (default) / 768 / 1024 forces a paired shape, 512
+    // two unpaired workgroups per CU.
+    const char *wge = getenv("SBLAS_XS_WG");
+    const bool pair512 = !wge || strcmp(wge, "512p") == 0;
+    P.nt = pair512 ? 512 : atoi(wge) == 512 ? 512 : atoi(wge) == 768 ? 768 : kXsThreads;
+    P.pair = (P.nt >= 768 || pair512) && !(getenv("SBLAS_XS_PAIR") && atoi(getenv("SBLAS_XS_PAIR")) == 0);
     if (P.nt == 768 && !P.pair) P.nt = kXsThreads;
-    if (P.nt == 768 && getenv("SBLAS_XS_TRACE")) P.nt = kXsThreads;  // the timeline twins are 1024-thread
+    if (pair512 && !P.pair) {  // SBLAS_XS_PAIR=0 with the default shape: the unpaired 1024 form
+        P.nt = kXsThreads;
+    }
+    if ((P.nt == 768 || (P.nt == 512 && P.pair)) && getenv("SBLAS_XS_TRACE")) P.nt = kXsThreads;  // trace twins: 1024
     P.split = 8;  // waves of the first (narrow) team of a pair: 5, 6, 7 or 8
     if (const char *e = getenv("SBLAS_XS_SPLIT")) P.split = std::min(8, std::max(5, atoi(e)));
     P.dyn = P.pair && P.split == 8 && !(getenv("SBLAS_XS_DYN") && atoi(getenv("SBLAS_XS_DYN")) == 0);
-    if (P.nt == 768 && !P.dyn) P.nt = kXsThreads;  // the 768 shape has the dynamic-claim kernel only
+    if ((P.nt == 768 || (P.nt == 512 && P.pair)) && !P.dyn) P.nt = kXsThreads;  // dynamic-claim kernels only
     int dev = 0, ncu = 0, per_cu = 0;
     SBLAS_HIP(hipGetDevice(&dev));
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    if (P.nt == 512)
+    if (P.nt == 512 && P.pair)
+        SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, k_spmv_xsort<true, 0, 512, true, 4, false, true, 2>, 512, 0));
+    else if (P.nt == 512)
         SBLAS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, k_spmv_xsort<true, 0, 512, false>, 512, 0));
     else if (P.nt == 768)
@@ -1044,7 +1052,8 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     {
         const char *ue = getenv("SBLAS_XS_U");
         const double per_wave = (double)nchunks / ((double)std::max(P.nitems, 1) * (P.nt / 64));
-        P.u = ue ? std::max(1, std::min(4, atoi(ue))) : (per_wave >= 24.0 ? 2 : 1);
+        // (two 4-wave teams: 2 everywhere, the N = 8 slice 42.7-43.7 -> 40.7-40.8 us)
+        P.u = ue ? std::max(1, std::min(4, atoi(ue))) : (P.nt == 512 && P.pair) ? 2 : (per_wave >= 24.0 ? 2 : 1);
     }
     int nstat = 0;
     for (int k = 0; k < 8; ++k) {
@@ -1183,7 +1192,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
     K kern;
     const bool b = beta != 0.0;
     constexpr int W = kXsThreads;
-    if (P.nt == 512) {
+    if (P.nt == 512 && !P.pair) {
         if (mode == 1) kern = b ? k_spmv_xsort<true, 1, 512, false> : k_spmv_xsort<false, 1, 512, false>;
         else if (mode == 2) kern = b ? k_spmv_xsort<true, 2, 512, false> : k_spmv_xsort<false, 2, 512, false>;
         else if (mode == 3) kern = b ? k_spmv_xsort<true, 3, 512, false> : k_spmv_xsort<false, 3, 512, false>;
@@ -1214,7 +1223,18 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
         if (mode == 16 && xu == 1) kern = XS_DYN(16, 1);  // experiment: L2-resident gathers
 #undef XS_DYN
     }
-    if (P.nt == 768) {  // 6 + 6 waves, U = P.u chunks per claim
+    if (P.nt == 512 && P.pair) {  // 4 + 4 waves (the default shape)
+        const int xu = P.u;
+        if (b) kern = xu == 1 ? k_spmv_xsort<true, 0, 512, true, 4, false, true, 1>
+                      : xu == 3 ? k_spmv_xsort<true, 0, 512, true, 4, false, true, 3>
+                      : xu == 4 ? k_spmv_xsort<true, 0, 512, true, 4, false, true, 4>
+                                : k_spmv_xsort<true, 0, 512, true, 4, false, true, 2>;
+        else kern = xu == 1 ? k_spmv_xsort<false, 0, 512, true, 4, false, true, 1>
+                    : xu == 3 ? k_spmv_xsort<false, 0, 512, true, 4, false, true, 3>
+                    : xu == 4 ? k_spmv_xsort<false, 0, 512, true, 4, false, true, 4>
+                              : k_spmv_xsort<false, 0, 512, true, 4, false, true, 2>;
+    }
+    if (P.nt == 768) {  // 6 + 6 waves (SBLAS_XS_WG=768), U = P.u chunks per claim
         const int xu = P.u;
         if (b) kern = xu == 1 ? k_spmv_xsort<true, 0, 768, true, 6, false, true, 1>
                       : xu == 3 ? k_spmv_xsort<true, 0, 768, true, 6, false, true, 3>
@@ -1226,7 +1246,7 @@ int launch_spmv_xsort(const sblas_csr_s &A, double alpha, const double *x, doubl
                               : k_spmv_xsort<false, 0, 768, true, 6, false, true, 2>;
     }
     static const char *trace_path = getenv("SBLAS_XS_TRACE");
-    if (trace_path && mode == 0 && P.split == 8 && P.nt != 768) {  // debugging aid: the timeline-stamping twins
+    if (trace_path && mode == 0 && P.split == 8 && P.nt != 768 && !(P.nt == 512 && P.pair)) {  // debugging aid: the timeline-stamping twins
         if (P.nt == 512) kern = b ? k_spmv_xsort<true, 0, 512, false, 8, true> : k_spmv_xsort<false, 0, 512, false, 8, true>;
         else if (P.pair && P.dyn && xu == 1)
             kern = b ? k_spmv_xsort<true, 0, W, true, 8, true, true, 1> : k_spmv_xsort<false, 0, W, true, 8, true, true, 1>;

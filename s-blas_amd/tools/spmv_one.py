@@ -69,7 +69,7 @@ def main():
     t = [e0.elapsed_time(e1) for e0, e1 in ms]
     abytes = A.algorithmic_bytes(True)
     print(f"{a.matrix} {a.algo} n={n}: plan {plan_s:.2f} s, mean {np.mean(t) * 1e3:.1f} us, "
-          f"min {np.min(t) * 1e3:.1f} us, {abytes / np.mean(t) / 1e9 * 1e3 / 1e3:.1f} GB/s alg.",
+          f"min {np.min(t) * 1e3:.1f} us, {abytes / (np.mean(t) * 1e-3) / 1e9:.1f} GB/s alg.",
           flush=True)
     A.close()
 

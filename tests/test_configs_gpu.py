@@ -78,10 +78,10 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
     (1, {"SBLAS_RS_PANEL": "0"}), (1, {"SBLAS_RS_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
     (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_U": "2"}),
     (5, {"SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (5, {"SBLAS_XS_WG": "1024"}),
-    (1, {"SBLAS_RS_SEQ": "0"})],
+    (1, {"SBLAS_RS_SEQ": "0"}), (5, {"SBLAS_XS_WG": "768"}), (5, {"SBLAS_XS_U": "1"})],
     ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "csr5_plain", "csr5_form0", "csr5_form1",
          "csr5_form3_plain", "rowsplit_plain", "rowsplit_panels", "panel", "xsort", "xsort_static", "xsort_q3",
-         "xsort_fused", "xsort_u2", "xsort_allwide", "xsort_solo", "xsort_wg1024", "rowsplit_vec4"])
+         "xsort_fused", "xsort_u2", "xsort_allwide", "xsort_solo", "xsort_wg1024", "rowsplit_vec4", "xsort_wg768", "xsort_u1"])
 def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
     """BASELINE configs[1] at full size, every algorithm against the oracle."""
     for k, v in env.items():
@@ -166,7 +166,8 @@ def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
 
 
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_SOLO": "1"}, {"SBLAS_XS_WG": "768"}], ids=["default", "solo", "wg768"])
+@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_SOLO": "1"}, {"SBLAS_XS_WG": "768"}, {"SBLAS_XS_WG": "1024"}],
+                         ids=["default", "solo", "wg768", "wg1024"])
 def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world, rank, env):
     """A rank's cyclic slice of config 2 (bench.py's N > 1 share) with the
     persistent column-sorted kernel (and its solo-item layout), three launches

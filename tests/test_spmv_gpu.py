@@ -40,13 +40,17 @@ ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
          (5, {"SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}),
          (5, {"SBLAS_XS_SOLO": "1"}), (5, {"SBLAS_XS_SOLO": "1", "SBLAS_XS_WSTAR": "50"}),
          (1, {"SBLAS_RS_SEQ": "0"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "2"}),
-         (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"})]
+         (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"}),
+         (5, {"SBLAS_XS_WG": "1024"}), (5, {"SBLAS_XS_WG": "1024", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_U": "1"}), (5, {"SBLAS_XS_U": "3", "SBLAS_XS_WSTAR": "50"}),
+         (5, {"SBLAS_XS_WG": "512p", "SBLAS_XS_SOLO": "1", "SBLAS_XS_WSTAR": "50"})]
 ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
             "xsort_allwide", "xsort_narrow", "xsort_narrow_w50", "xsort_unpaired", "xsort_wg512", "xsort_wg768",
             "xsort_wg768_w50", "xsort_wg768_solo", "xsort_static", "xsort_static_w50",
             "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
             "xsort_u2_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
-            "rowsplit_panel3"]
+            "rowsplit_panel3", "xsort_wg1024", "xsort_wg1024_w50", "xsort_u1", "xsort_u3_w50",
+            "xsort_wg512p_solo_w50"]
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
