@@ -499,6 +499,32 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
         }
         if (kTrace && (threadIdx.x & 63) == 0)  // debugging aid: this team's last wave
             atomicMax(&s_tend[half], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        // A narrow sub-item alone in its item (the partner team empty: solo
+        // items, SBLAS_XS_SOLO, or a leftover) is written by the whole
+        // workgroup: its rows may fill both teams' LDS halves.
+        const int s0 = kPair ? (int)s_rec_all[0][0] : -1;
+        const bool solo = kPair && (int)s_rec_all[1][0] < 0 && s0 >= 0 && (s0 & 255) == 0;  // uniform
+        constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
+        constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
+        // 4-wave teams (256-VGPR budget): a narrow epilogue's y loads are
+        // issued before the barrier below, so their latency overlaps the
+        // wait for the workgroup's last wave (at 128 VGPRs they spilled)
+        constexpr bool kEarlyY = kBeta && kPair && kWG == 512;
+        const bool ynarrow = solo || (sub >= 0 && !k1);
+        const int et = solo ? (int)threadIdx.x : ht;
+        const int eNT = solo ? kWG : NT;
+        const long long rr = solo ? s_rec_all[0][1] : ((long long)(unsigned)R.row0 | ((long long)R.nrows << 32));
+        const int row0 = (int)(rr & 0xffffffffLL), nrows = (int)(rr >> 32);
+        double y0[kEp];
+        if constexpr (kEarlyY) {
+            if (ynarrow) {
+#pragma unroll
+                for (int e = 0; e < kEp; ++e) {
+                    const int r = et + e * eNT;
+                    y0[e] = r < nrows ? y[row0 + r] : 0.0;
+                }
+            }
+        }
         if (threadIdx.x < 64) {
             const int own = __shfl(pre, 0, 64);
             const int it = !a.dynamic ? -1 : own < a.qlen[xcc] ? xcc * a.qstride + own : xs_claim(a, xcc);
@@ -514,20 +540,11 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             a.trace[ts + 4] = (long long)s_tend[0];
             a.trace[ts + 5] = (long long)s_tend[1];
         }
-        // A narrow sub-item alone in its item (the partner team empty: solo
-        // items, SBLAS_XS_SOLO, or a leftover) is written by the whole
-        // workgroup: its rows may fill both teams' LDS halves.
-        const int s0 = kPair ? (int)s_rec_all[0][0] : -1;
-        const bool solo = kPair && (int)s_rec_all[1][0] < 0 && s0 >= 0 && (s0 & 255) == 0;  // uniform
         if (sub >= 0 && k1) {
             // epilogue: a team owns <= kXsHalfRows rows, at most kEp per
             // thread; every y load of the thread is issued before the first
             // use, so the y latency is paid once, not once per row (a rolled
             // loop put ~10 us of serial latency on the end of every item).
-            // (Issuing them before the barrier above spilled registers: the
-            // kernel sits at its 128-VGPR cap.)
-            constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
-            constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
             double *out = a.partial + R.pbase + (long long)(k1 - 1) * R.nrows;
             // agent-scope (sc1) stores when the fused reduce may read them
             // on another XCD (whose L2 is not coherent with this one);
@@ -550,17 +567,10 @@ __global__ __launch_bounds__(kWG) void k_spmv_xsort(const XsArgs a,
             // narrow: y = alpha * acc + beta * y over the sub-item's rows;
             // a solo item's <= kXsRows rows over all kWG threads, a team's
             // <= kXsHalfRows over its NT
-            constexpr int kTeamMin = kPair ? (SA < SB ? SA : SB) * 64 : kWG;
-            constexpr int kEp = ((kWG == 1024 && !kPair ? kXsRows : kXsHalfRows) + kTeamMin - 1) / kTeamMin;
             static_assert(!kPair || kEp * kWG >= kXsRows, "a solo item's rows fit the epilogue");
-            const int et = solo ? (int)threadIdx.x : ht;
-            const int eNT = solo ? kWG : NT;
-            const long long rr = solo ? s_rec_all[0][1] : ((long long)(unsigned)R.row0 | ((long long)R.nrows << 32));
-            const int row0 = (int)(rr & 0xffffffffLL), nrows = (int)(rr >> 32);
             const double *eacc = solo ? acc_all : acc;
             double *yr = y + row0;
-            double y0[kEp];
-            if constexpr (kBeta) {
+            if constexpr (kBeta && !kEarlyY) {
 #pragma unroll
                 for (int e = 0; e < kEp; ++e) {
                     const int r = et + e * eNT;
