@@ -161,6 +161,9 @@ def _interleave_memory():
         nodes.extend(range(int(a), int(b or a) + 1))
     if len(nodes) < 2:
         return spec + " (one node: nothing to interleave)"
+    import platform
+    if platform.machine() != "x86_64":  # syscall 238 is set_mempolicy on x86_64 only
+        return spec + f" (not interleaved: set_mempolicy syscall number unknown on {platform.machine()})"
     import ctypes as C
     mask = (C.c_ulong * 16)()
     for nd in nodes:
@@ -210,6 +213,10 @@ def cpu_baseline_child(args) -> int:
     except (AttributeError, OSError):
         mask = os.cpu_count() or 1
     numa = _interleave_memory()
+    if args.cpu_leg == "spmm":
+        return cpu_baseline_spmm_child(args, mask, numa)
+    if args.cpu_leg == "sptrsv":
+        return cpu_baseline_sptrsv_child(args)
     import sblas
     W = Workload(args, sblas)
     col, val = W.rows(0, W.n)
@@ -231,19 +238,10 @@ def cpu_baseline_child(args) -> int:
     st = [_time_cpu(g, cargs, (), budget * 0.35 / 3) for _ in range(3)]
     t_mt = float(np.median([t for _, t in mt]))
     t_st = float(np.median([t for _, t in st]))
-    model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as fh:
-            for line in fh:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     quota = _cpu_quota()
     print(json.dumps({
         "value": round(gf(t_mt), 3), "unit": "GFLOP/s", "cores": best,
-        "kind": "port", "cpu_model": model,
+        "kind": "port", "cpu_model": _cpu_model(),
         "sample": (f"full matrix of the workload, orc_csr_spmv_omp (OpenMP, schedule dynamic, "
                    f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} OMP_PLACES={os.environ.get('OMP_PLACES')}, "
                    f"{mask} CPUs in the affinity mask, cgroup quota "
@@ -261,16 +259,132 @@ def cpu_baseline_child(args) -> int:
     return 0
 
 
-def cpu_baseline(args):
-    """The oracle restatement (oracle/liboracle.so) timed on this host's cores,
-    in a child process (cpu_baseline_child) with the threads pinned
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_spmm_child(args, mask, numa) -> int:
+    """configs[3]'s CPU baseline (BASELINE.md §3, SURVEY M1-cpu): the oracle's
+    csrmm restatement orc_spmm_omp (OpenMP over rows of A, B row-major, the
+    same C = -0.7*A*B + 0.8*C over the rail4284-shaped stand-in x 64 columns)
+    with the SpMV baseline's thread sweep; the best count is timed again,
+    median of 3.  B / C0 are host U[0,1) draws of the same shapes (the GPU leg
+    draws them on the device: timing only, the values do not matter)."""
+    import ctypes as C
+    m, k, n = 4284, 1_092_610, 64
+    rp, col, val, _ = _rail_matrix()
+    rng = np.random.default_rng(45)
+    B = rng.random((k, n))
+    C0 = np.asfortranarray(rng.random((m, n)))
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    f = lib.orc_spmm_omp
+    f.restype = None
+    f.argtypes = [C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                  C.c_int, C.c_double, C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+    rp32 = np.ascontiguousarray(rp, np.int32)
+    Cw = np.array(C0, copy=True, order="F")
+    cargs = (m, n, -0.7, rp32.ctypes.data, col.ctypes.data, val.ctypes.data, B.ctypes.data, n, 1, 0.8,
+             Cw.ctypes.data, m, None)
+    nnz = int(rp[-1])
+    gf = lambda t: 2.0 * nnz * n / t / 1e9  # noqa: E731
+    counts = sorted({c for c in (16, 32, 64, 128, 256, 512) if c < mask} | {mask})
+    budget = args.cpu_budget * 0.5
+    sweep = {c: gf(_time_cpu(f, cargs, (c,), budget * 0.4 / len(counts), 50)[1]) for c in counts}
+    best = max(sweep, key=sweep.get)
+    mt = [_time_cpu(f, cargs, (best,), budget * 0.6 / 3, 50) for _ in range(3)]
+    t_mt = float(np.median([t for _, t in mt]))
+    quota = _cpu_quota()
+    print(json.dumps({
+        "value": round(gf(t_mt), 3), "unit": "GFLOP/s", "cores": best, "kind": "port",
+        "cpu_model": _cpu_model(),
+        "sample": (f"full configs[3] product (m {m}, k {k}, nnz {nnz}, 64 columns), orc_spmm_omp (oracle "
+                   f"restatement of cusparseDcsrmm's definition, OpenMP over rows, B row-major), "
+                   f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} OMP_PLACES={os.environ.get('OMP_PLACES')}, "
+                   f"{mask} CPUs in the affinity mask, cgroup quota "
+                   f"{'none' if quota is None else f'{quota:.1f} CPUs'}, NUMA {numa}; thread sweep "
+                   + ", ".join(f"{c}: {v:.1f}" for c, v in sweep.items()) +
+                   f" GFLOP/s; best {best} threads, median of 3 runs of "
+                   f"{'/'.join(str(r) for r, _ in mt)} reps = {t_mt * 1e3:.2f} ms per product"),
+        "ms_per_call": round(t_mt * 1e3, 3),
+        "thread_sweep_gflops": {str(c): round(v, 3) for c, v in sweep.items()},
+        "affinity_cpus": mask, "cgroup_cpu_quota": quota,
+    }), flush=True)
+    return 0
+
+
+def cpu_baseline_sptrsv_child(args) -> int:
+    """configs[4]'s CPU baseline: the
+    reference's OWN serial sync-free solver (sptrsv_syncfree_analyser +
+    _executor, sptrsv/sptrsv_v1/src/sptrsv_syncfree_serialref.h:6-108,
+    compiled in place into oracle/_ref/libsblas_ref.so) on the same
+    known-answer system, one core; the figure is the executor time the
+    reference itself prints (serialref.h:142-155: flop = 2*nnz over the
+    executor), median of 3 solves, x checked against x_ref exactly.  Without
+    oracle/_ref (reference checkout absent when the tree was built) the
+    oracle's restatement orc_sptrsv_serial is timed instead (kind "port")."""
+    import ctypes as C
+    import sblas
+    cp, ri, vi, xref, bi = config5_system(sblas)
+    n, nnz = CONFIG5_N, len(ri)
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libsblas_ref.so")
+    P = C.c_void_p
+    runs, exact = [], True
+    if os.path.exists(ref_path):
+        f = C.CDLL(ref_path).ref_sptrsv_serial_timed
+        f.restype = C.c_int
+        f.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P, P]
+        kind, what = "reference", ("sptrsv_syncfree_analyser + _executor (the reference's serialref, "
+                                   "oracle/_ref, compiled in place)")
+        for _ in range(3):
+            x = np.zeros(n)
+            an, ex = C.c_double(), C.c_double()
+            f(cp.ctypes.data, ri.ctypes.data, vi.ctypes.data, n, nnz, 0, 1, bi.ctypes.data, x.ctypes.data,
+              C.byref(an), C.byref(ex))
+            runs.append((an.value, ex.value))
+            exact = exact and bool(np.array_equal(x, xref))
+    else:
+        g = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")).orc_sptrsv_serial
+        g.restype = C.c_int
+        g.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, P, P]
+        kind, what = "port", "orc_sptrsv_serial (oracle restatement; oracle/_ref absent)"
+        for _ in range(3):
+            x = np.zeros(n)
+            t0 = time.perf_counter()
+            g(cp.ctypes.data, ri.ctypes.data, vi.ctypes.data, n, 0, 1, bi.ctypes.data, x.ctypes.data)
+            runs.append((0.0, (time.perf_counter() - t0) * 1e3))
+            exact = exact and bool(np.array_equal(x, xref))
+    ex_ms = float(np.median([e for _, e in runs]))
+    an_ms = float(np.median([a for a, _ in runs]))
+    print(json.dumps({
+        "value": round(2.0 * nnz / (ex_ms * 1e-3) / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": kind,
+        "cpu_model": _cpu_model(),
+        "sample": (f"full configs[4] system (n {n}, nnz {nnz}), {what}, single core, median of 3 solves: "
+                   f"executor {ex_ms:.1f} ms (the figure serialref.h:150-155 prints), analyser {an_ms:.1f} ms"),
+        "executor_ms": round(ex_ms, 3), "analyser_ms": round(an_ms, 3),
+        "check_exact_vs_xref": exact,
+    }), flush=True)
+    return 0
+
+
+def cpu_baseline(args, leg="spmv"):
+    """The oracle restatement (oracle/liboracle.so; for configs[4] the
+    reference's own serial solver, oracle/_ref) timed on this host's cores, in
+    a child process (cpu_baseline_child) with the threads pinned
     (OMP_PROC_BIND=close, OMP_PLACES=cores) and the thread count swept.  Only
-    this leg of bench.py (and the post-timing --check) touches oracle/."""
+    these legs of bench.py (and the post-timing checks) touch oracle/."""
     import subprocess
     env = dict(os.environ, OMP_PROC_BIND="close", OMP_PLACES="cores")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--matrix", args.matrix,
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--cpu-leg", leg,
+           "--matrix", args.matrix,
            "--nrows", str(args.nrows), "--heavy", str(args.heavy), "--light", str(args.light),
            "--cols", args.cols, "--grid", str(args.grid), "--scale", str(args.scale),
            "--cpu-budget", str(args.cpu_budget)]
@@ -278,6 +392,18 @@ def cpu_baseline(args):
     if r.returncode != 0:
         return {"error": f"cpu baseline child exited {r.returncode}: {r.stderr[-400:]}"}
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def attach_cpu_baselines(out, args):
+    """N = 1 lines: the headline's `cpu_baseline` plus one per BASELINE leg
+    that the line carries: `config4.cpu_baseline`
+    (SpMM, OpenMP restatement, thread-swept) and `config5.cpu_baseline` (the
+    reference's own serial SpTRSV, one core)."""
+    out["cpu_baseline"] = cpu_baseline(args)
+    if isinstance(out.get("config4"), dict):
+        out["config4"]["cpu_baseline"] = cpu_baseline(args, "spmm")
+    if isinstance(out.get("config5"), dict):
+        out["config5"]["cpu_baseline"] = cpu_baseline(args, "sptrsv")
 
 
 def measured_peak(torch, sblas, dev, stream):
@@ -633,6 +759,23 @@ def config4_object(world, per, first_s, gen_s, check, traffic):
     }
 
 
+CONFIG5_N = 5_558_326
+
+
+def config5_system(sblas):
+    """configs[4]'s integer known-answer system: the unit-lower CSC stand-in
+    (colptr, rowidx, val), x_ref in 1..10 and b = L x_ref (exact in fp64)."""
+    n = CONFIG5_N
+    cp, ri, _ = sblas.gen_lower_banded(n, 5, 80_000, 47)
+    nnz = len(ri)
+    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
+    vi = np.random.default_rng(5).integers(1, 11, nnz).astype(np.float64)
+    vi[cp[:-1]] = 1.0  # unit diagonal
+    xref = np.floor(sblas.gen_vector(n, 48) * 10.0) + 1.0
+    bi = np.bincount(ri, weights=vi * xref[cols], minlength=n)  # integers < 2^53: exact
+    return cp, ri, vi, xref, bi
+
+
 def config5_leg(args, torch, sblas, rank, world, evict, sync_barrier):
     """configs[4] on every line: the sync-free SpTRSV.
     Rank 0 solves the integer known-answer system (x must equal x_ref
@@ -642,18 +785,12 @@ def config5_leg(args, torch, sblas, rank, world, evict, sync_barrier):
     order, block d on device d % visible, producers pushing x_i into later
     blocks' fine-grained x), each timed cold (1 GiB sweep on every device it
     uses before each solve).  The other ranks wait at the barrier."""
-    n, offd, band = 5_558_326, 5, 80_000
+    n = CONFIG5_N
     out = {"what": CONFIG5, "n": n}
     if rank == 0:
         t0 = time.perf_counter()
-        cp, ri, _ = sblas.gen_lower_banded(n, offd, band, 47)
+        cp, ri, vi, xref, bi = config5_system(sblas)
         nnz = len(ri)
-        cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
-        vi = np.random.default_rng(5).integers(1, 11, nnz).astype(np.float64)
-        vi[cp[:-1]] = 1.0  # unit diagonal
-        xref = np.floor(sblas.gen_vector(n, 48) * 10.0) + 1.0
-        bi = np.bincount(ri, weights=vi * xref[cols], minlength=n)  # integers < 2^53: exact
-        del cols
         gen_s = time.perf_counter() - t0
         dev = torch.device("cuda", torch.cuda.current_device())
         stream = torch.cuda.Stream(device=dev)
@@ -774,14 +911,18 @@ def config5_blocks4(args, torch, sblas, cp, ri, vi, n, nnz, bi, xref, gpus, evic
             mms.append(t4)
             ok = ok and bool(np.array_equal(x, xref))
         del scr
+        where = H.info()
     finally:
         H.close()
-    return config5_blocks(nnz, gpus, float(np.mean(mms)), ok, build_s)
+    out = config5_blocks(nnz, gpus, float(np.mean(mms)), ok, build_s)
+    out["block_devices"] = [d for d, _ in where]
+    out["block_rows"] = [r for _, r in where]
+    return out
 
 
 def config5_single(nnz, levels, order, t, exact, gen_s, setup_s):
     """configs[4]'s single-device figures, t in ms."""
-    n = 5_558_326
+    n = CONFIG5_N
     abytes = 12 * nnz + 4 * (n + 1) + 16 * n
     ach = abytes / (t * 1e-3) / 1e9
     return {
@@ -811,6 +952,32 @@ def config5_blocks(nnz, gpus, t4, ok, build_s):
                  "one GPU visible: the 4 blocks run concurrently on it (the peer-store protocol on local "
                  "fine-grained memory)"),
     }
+
+
+def peer_matrix(torch):
+    """hipDeviceCanAccessPeer over the visible devices (1 on the diagonal)."""
+    nd = torch.cuda.device_count()
+    return [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(nd)]
+            for i in range(nd)]
+
+
+def _pci_bus(torch, d):
+    p = torch.cuda.get_device_properties(d)
+    bus = getattr(p, "pci_bus_id", None)
+    return None if bus is None else f"{getattr(p, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(p, 'pci_device_id', 0):02x}"
+
+
+def topology_object(driver, backend, nranks, ordinals, pci, peers, note=None):
+    """What a multi-GPU line ran on: the communicator's
+    rank count and each rank's device ordinal / PCI address, and the
+    hipDeviceCanAccessPeer matrix of the visible devices."""
+    out = {"driver": driver, "backend": backend, "comm_ranks": int(nranks),
+           "device_ordinals": [int(d) for d in ordinals], "pci_bus": list(pci),
+           "visible_devices": len(peers), "peer_access": peers,
+           "all_pairs_peer": bool(all(all(r) for r in peers))}
+    if note:
+        out["note"] = note
+    return out
 
 
 def _gather_rows(torch, dist, dev, row, world):
@@ -1133,8 +1300,13 @@ def run_ctx(args) -> int:
     if args.ctx_loopback:
         out["note"] = (f"loopback rehearsal: {N} context ranks on {ndev} GPU(s), collectives as "
                        "stream-ordered device copies (no RCCL); not a measurement")
+    nranks, ords = ctx.comm_info()
+    out["topology"] = topology_object(
+        "ctx (one process, ncclCommInitAll)", "rccl" if nranks else "loopback (no communicator)", nranks, ords,
+        [_pci_bus(torch, d) for d in ords], peer_matrix(torch),
+        note=None if nranks else "loopback: ranks wrapped onto the visible GPUs, no RCCL communicator")
     if N == 1 and not args.no_cpu_baseline and not args.ctx_loopback:
-        out["cpu_baseline"] = cpu_baseline(args)
+        attach_cpu_baselines(out, args)
     print(json.dumps(out), flush=True)
     ctx.close()
     return 0
@@ -1164,8 +1336,10 @@ def main() -> int:
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the "
                          "multi-rank path with several ranks on one GPU")
     ap.add_argument("--check", action="store_true",
-                    help="after timing, verify the assembled y of one fresh step against the "
-                         "oracle (rank 0; small n only)")
+                    help="(default; kept for old command lines) after timing, verify the assembled y "
+                         "of one fresh step against the oracle on rank 0 -> `check_vs_oracle`")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the post-timing oracle check of the headline y (on by default)")
     ap.add_argument("--cache", choices=["cold", "warm"], default="cold",
                     help="cold (default; SURVEY M1-cache / BASELINE.md: the headline uses cold "
                          "timing): a 1 GiB sweep (--scrub) before every timed step evicts the 256 MB "
@@ -1217,8 +1391,10 @@ def main() -> int:
                     help="skip the config4 / config5 post-timing checks (every C entry under the fp64 bound; "
                          "the SpTRSV known answer exactly)")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-leg", choices=["spmv", "spmm", "sptrsv"], default="spmv", help=argparse.SUPPRESS)
     args = ap.parse_args()
     args.check_legs = not args.no_check_legs
+    args.check = not args.no_check
     if args.cpu_baseline_only:  # child of cpu_baseline(): host only, no torch, no GPU
         return cpu_baseline_child(args)
 
@@ -1249,6 +1425,11 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    # the communicator and devices this line runs on (rank 0 reports them)
+    ordinals = _gather_rows(torch, dist, dev, [float(dev_idx)], world)[:, 0] if dist is not None else [dev_idx]
+    topo = topology_object("torch (one process per GPU)", dist.get_backend() if dist is not None else "none",
+                           dist.get_world_size() if dist is not None else 1, ordinals,
+                           [_pci_bus(torch, int(d)) for d in ordinals], peer_matrix(torch))
 
     algo_ids = {"rowsplit": sblas.ROWSPLIT, "csr5": sblas.CSR5, "panel": sblas.PANEL,
                 "xsort": sblas.XSORT}
@@ -1547,6 +1728,7 @@ def main() -> int:
         }
         if world > 1 and args.dist_backend != "nccl":
             out["note"] = f"rehearsal: {world} ranks on {ndev} GPU(s) over {args.dist_backend}"
+        out["topology"] = topo
         if check is not None:
             out["check_vs_oracle"] = check
         if rowsplit_beside is not None:
@@ -1561,7 +1743,7 @@ def main() -> int:
             out["structured"] = structured
         out["traffic_source"] = dict(TRAFFIC_NOTES)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+            attach_cpu_baselines(out, args)
         print(json.dumps(out), flush=True)
     op.close()
     if dist is not None:

@@ -288,7 +288,17 @@ int sblas_trsv_mgpu_create(sblas_trsv_mgpu *out, const int *colptr, const int *r
                            const double *val, int n, int substitution, int rhs, int ngpu,
                            int tasks, int balance);
 int sblas_trsv_mgpu_run(sblas_trsv_mgpu h, const double *b, double *x, double *solve_ms);
+/* Where the blocks run: block d's physical device and row count (arrays of
+ * *nblocks entries; any may be NULL). */
+int sblas_trsv_mgpu_info(sblas_trsv_mgpu h, int *nblocks, int *block_device, int *block_rows);
 int sblas_trsv_mgpu_destroy(sblas_trsv_mgpu h);
+/* create fails with SBLAS_ERR_UNSUPPORTED (or SBLAS_ERR_HIP) before anything
+ * is launched when two of its devices have no peer access (producers store
+ * x_i into later blocks' memory; sptrsv_v3 needs NVSHMEM the same way,
+ * sptrsv_v3/src/sptrsv_syncfree_cuda.h:245-249), so no block ever waits on a
+ * store that cannot arrive; fine-grained allocation failures return the same
+ * way.  Peer links are reference-counted per process: destroying one handle
+ * or context never takes a link away from another live one. */
 
 /* Multi-partition y assembly after an allgather of padded slices: partition
  * r's slice starts at d_gathered + r*stride; d_meta (DEVICE, 3*g ints) holds
@@ -332,6 +342,10 @@ typedef enum {
 int sblas_ctx_create(sblas_ctx *out, int ngpu, const int *devlist);
 int sblas_ctx_destroy(sblas_ctx ctx);
 int sblas_ctx_ngpu(sblas_ctx ctx, int *ngpu);
+/* The communicator as RCCL reports it: *nranks = ncclCommCount of device 0's
+ * communicator (0 for a loopback context, which has none), and per context
+ * device d its ordinal (ncclCommCuDevice; the wrapped ordinal in loopback). */
+int sblas_ctx_comm_info(sblas_ctx ctx, int *nranks, int *devices);
 /* HOST CSR (int64 rowptr) distributed over the devices and analysed for
  * `algo` (sblas_spmv_algo).  partition 0 = cyclic row chunks (chunk j of
  * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
@@ -482,6 +496,14 @@ int sblas_hbm_probe(int mode, const void *src, void *dst, long long bytes, int w
  * runtime stamps at the kernel's start and end, as sblas_spmv_timed). */
 int sblas_hbm_probe_timed(int mode, const void *src, void *dst, long long bytes, int wg_per_cu,
                           void *stream, float *ms);
+
+/* Test hooks (not part of the reference API). */
+/* on != 0: every peer link the library asks for is refused, and a
+ * multi-block trsv_mgpu treats blocks sharing a GPU as distinct devices, so
+ * the refusal path runs on a one-GPU box.  Process-wide. */
+int sblas_test_deny_peer_access(int on);
+/* References the library holds on the a -> b peer link (0: none). */
+int sblas_peer_refs(int a, int b);
 
 #ifdef __cplusplus
 }

@@ -58,4 +58,26 @@ int ref_sptrsv_serial(const int *colptr, const int *rowidx, const double *val,
     return rc;
 }
 
+// The same two calls timed apart, the way sptrsv_syncfree_serialref
+// (sptrsv_syncfree_serialref.h:110-155) times and prints them: analyser ms
+// and executor ms (the executor figure is the reference's CPU baseline for
+// configs[4]).  bench.py's cpu_baseline child only.
+int ref_sptrsv_serial_timed(const int *colptr, const int *rowidx, const double *val,
+                            int n, int nnz, int substitution, int rhs,
+                            const double *b, double *x, double *analyser_ms, double *executor_ms)
+{
+    int *deg = (int *)malloc(sizeof(int) * n);
+    struct timeval t1, t2;
+    gettimeofday(&t1, NULL);
+    sptrsv_syncfree_analyser(rowidx, n, n, nnz, deg);
+    gettimeofday(&t2, NULL);
+    *analyser_ms = (t2.tv_sec - t1.tv_sec) * 1000.0 + (t2.tv_usec - t1.tv_usec) / 1000.0;
+    gettimeofday(&t1, NULL);
+    int rc = sptrsv_syncfree_executor(colptr, rowidx, val, deg, n, n, substitution, rhs, b, x);
+    gettimeofday(&t2, NULL);
+    *executor_ms = (t2.tv_sec - t1.tv_sec) * 1000.0 + (t2.tv_usec - t1.tv_usec) / 1000.0;
+    free(deg);
+    return rc;
+}
+
 }  // extern "C"

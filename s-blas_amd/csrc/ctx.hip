@@ -19,6 +19,8 @@
 // (k_assemble_carry).
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -91,7 +93,79 @@ constexpr double kCtxRowCost = 3.0;
 namespace sblas {
 static sblas_ctx g_bound = nullptr;
 sblas_ctx bound_ctx() { return g_bound; }
+
+namespace {
+struct PeerLink {
+    int refs = 0;
+    bool owned = false;  // enabled by the library (disabled at the last release)
+};
+std::mutex g_peer_mu;
+std::map<std::pair<int, int>, PeerLink> g_peer;
+bool g_peer_deny = false;
+}  // namespace
+
+bool peer_denied() { return g_peer_deny; }
+
+int peer_acquire(int a, int b, const char *who)
+{
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    if (g_peer_deny) {
+        set_error("%s: peer access %d -> %d refused (sblas_test_deny_peer_access)", who, a, b);
+        return SBLAS_ERR_UNSUPPORTED;
+    }
+    PeerLink &L = g_peer[{a, b}];
+    if (L.refs == 0) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+            (void)hipGetLastError();
+            set_error("%s: no peer access between devices %d and %d", who, a, b);
+            return SBLAS_ERR_UNSUPPORTED;
+        }
+        DeviceGuard g(a);
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {  // enabled outside the library: use, never disable
+            (void)hipGetLastError();
+            L.owned = false;
+        } else if (e != hipSuccess) {
+            set_error("%s: hipDeviceEnablePeerAccess(%d -> %d): %s", who, a, b, hipGetErrorString(e));
+            return SBLAS_ERR_HIP;
+        } else {
+            L.owned = true;
+        }
+    }
+    ++L.refs;
+    return SBLAS_OK;
+}
+
+void peer_release(int a, int b)
+{
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    auto it = g_peer.find({a, b});
+    if (it == g_peer.end() || it->second.refs <= 0) return;
+    if (--it->second.refs == 0) {
+        if (it->second.owned) {
+            DeviceGuard g(a);
+            (void)hipDeviceDisablePeerAccess(b);
+            (void)hipGetLastError();
+        }
+        g_peer.erase(it);
+    }
+}
 }  // namespace sblas
+
+extern "C" int sblas_test_deny_peer_access(int on)
+{
+    std::lock_guard<std::mutex> lk(sblas::g_peer_mu);
+    sblas::g_peer_deny = on != 0;
+    return SBLAS_OK;
+}
+
+extern "C" int sblas_peer_refs(int a, int b)
+{
+    std::lock_guard<std::mutex> lk(sblas::g_peer_mu);
+    auto it = sblas::g_peer.find({a, b});
+    return it == sblas::g_peer.end() ? 0 : it->second.refs;
+}
 
 namespace {
 
@@ -397,8 +471,10 @@ int upload_parts(sblas_ctx_s &C, int d, const std::vector<long long> &lrp, const
 // The loopback all-reduce (k_ctx_sum) reads every rank's send buffer from
 // the summing rank's device: ranks wrapped onto distinct GPUs need peer
 // access between them (refused if a pair has none).  Only this exchange
-// needs it -- the all-gather's device-to-device copies do not -- and what
-// the context enables here it disables on destroy.
+// needs it -- the all-gather's device-to-device copies do not.  The links
+// are reference-counted process-wide (peer_acquire), so a second context or
+// a trsv_mgpu handle on the same pair keeps its access when this context is
+// destroyed.
 int enable_loopback_peers(sblas_ctx_s &C)
 {
     for (int a = 0; a < C.g; ++a)
@@ -406,23 +482,7 @@ int enable_loopback_peers(sblas_ctx_s &C)
             const int da = C.dev[a], db = C.dev[b];
             if (da == db) continue;
             if (std::find(C.peers.begin(), C.peers.end(), std::make_pair(da, db)) != C.peers.end()) continue;
-            int can = 0;
-            if (hipDeviceCanAccessPeer(&can, da, db) != hipSuccess || !can) {
-                set_error("sblas_ctx_matrix_upload: loopback all-reduce over devices %d and %d without peer "
-                          "access", da, db);
-                return SBLAS_ERR_UNSUPPORTED;
-            }
-            DeviceGuard gd(da);
-            const hipError_t e = hipDeviceEnablePeerAccess(db, 0);
-            if (e == hipErrorPeerAccessAlreadyEnabled) {  // enabled by someone else: leave it on
-                (void)hipGetLastError();
-                continue;
-            }
-            if (e != hipSuccess) {
-                set_error("sblas_ctx_matrix_upload: hipDeviceEnablePeerAccess(%d -> %d): %s", da, db,
-                          hipGetErrorString(e));
-                return SBLAS_ERR_HIP;
-            }
+            SBLAS_TRY(peer_acquire(da, db, "sblas_ctx_matrix_upload (loopback all-reduce)"));
             C.peers.emplace_back(da, db);
         }
     return SBLAS_OK;
@@ -548,10 +608,7 @@ int sblas_ctx_destroy(sblas_ctx C)
         DeviceGuard g(C->evp_dev[i]);
         if (C->evp[i]) (void)hipEventDestroy(C->evp[i]);
     }
-    for (const auto &pr : C->peers) {
-        DeviceGuard g(pr.first);
-        (void)hipDeviceDisablePeerAccess(pr.second);
-    }
+    for (const auto &pr : C->peers) peer_release(pr.first, pr.second);
     (void)hipGetLastError();
     delete C;
     return SBLAS_OK;
@@ -561,6 +618,21 @@ int sblas_ctx_ngpu(sblas_ctx C, int *ngpu)
 {
     if (!C || !ngpu) return SBLAS_ERR_INVALID;
     *ngpu = C->g;
+    return SBLAS_OK;
+}
+
+int sblas_ctx_comm_info(sblas_ctx C, int *nranks, int *devices)
+{
+    if (!C) return SBLAS_ERR_INVALID;
+    const bool has_comm = !C->comm.empty() && C->comm[0];
+    if (nranks) {
+        *nranks = 0;
+        if (has_comm) SBLAS_NCCL(ncclCommCount(C->comm[0], nranks));
+    }
+    for (int d = 0; devices && d < C->g; ++d) {
+        devices[d] = C->dev[d];
+        if (has_comm && d < (int)C->comm.size() && C->comm[d]) SBLAS_NCCL(ncclCommCuDevice(C->comm[d], &devices[d]));
+    }
     return SBLAS_OK;
 }
 

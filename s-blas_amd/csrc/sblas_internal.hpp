@@ -348,6 +348,17 @@ struct DeviceGuard {
     }
 };
 
+// Process-wide peer access (ctx.hip).  Peer access is per process, so every
+// user (the loopback all-reduce of a context, a trsv_mgpu handle) takes a
+// reference on the (a -> b) link: the first acquire enables it (a link
+// already enabled by someone outside the library is used and never
+// disabled), the last release disables what the library enabled.  acquire
+// returns SBLAS_ERR_UNSUPPORTED when the pair has no peer path (or the test
+// hook sblas_test_deny_peer_access is set), SBLAS_ERR_HIP when enabling fails.
+int peer_acquire(int a, int b, const char *who);
+void peer_release(int a, int b);
+bool peer_denied();  // the test hook's state
+
 // Host helpers shared by capi / refapi (host_utils.cpp).
 int row_of_index(int m, const long long *rowptr, long long idx);
 int resolve_device(int ordinal, int *phys);  // wraps ordinals on few GPUs

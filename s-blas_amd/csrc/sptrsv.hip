@@ -1360,6 +1360,7 @@ struct sblas_trsv_mgpu_s {
     std::vector<TrsvMgpuDev> D;
     std::vector<hipStream_t> streams;     // per block (serial: per device's first block)
     std::vector<int> on_phys, first_on;
+    std::vector<std::pair<int, int>> peers;  // peer links taken (peer_acquire), released on destroy
     hipStream_t stream_of(int d) const { return streams[serial ? first_on[D[d].phys] : d]; }
 };
 
@@ -1382,6 +1383,7 @@ void trsv_mgpu_free(sblas_trsv_mgpu_s *H)
             DeviceGuard g(H->D[d].phys);
             (void)hipStreamDestroy(H->streams[d]);
         }
+    for (const auto &pr : H->peers) peer_release(pr.first, pr.second);
     delete H;
 }
 
@@ -1457,18 +1459,20 @@ int trsv_mgpu_build(sblas_trsv_mgpu_s *H, const int *colptr, const int *rowidx, 
         DeviceGuard g(H->D[d].phys);
         MG(hipStreamCreateWithFlags(&H->streams[d], hipStreamNonBlocking));
     }
-    for (int p = 0; p < nphys; ++p) {
-        DeviceGuard g(p);
+    // producers store x_i into every later block's fine-grained x: blocks on
+    // distinct devices need the peer link, and without it the build fails
+    // here -- before anything is launched, so no block can spin on an x it
+    // will never receive (sptrsv_v3's NVSHMEM setup fails the same way,
+    // sptrsv_syncfree_cuda.h:245-249).  The sblas_test_deny_peer_access hook
+    // treats blocks sharing one GPU as distinct devices, so a one-GPU box
+    // exercises the refusal.
+    for (int p = 0; p < nphys; ++p)
         for (int q = 0; q < nphys; ++q) {
             if (q == p) continue;
-            int can = 0;
-            if (hipDeviceCanAccessPeer(&can, p, q) == hipSuccess && can) {
-                hipError_t e = hipDeviceEnablePeerAccess(q, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) MG(e);
-                (void)hipGetLastError();
-            }
+            SBLAS_TRY(peer_acquire(p, q, "trsv_mgpu"));
+            H->peers.emplace_back(p, q);
         }
-    }
+    if (ngpu > 1 && peer_denied()) SBLAS_TRY(peer_acquire(H->D[0].phys, H->D[1].phys, "trsv_mgpu"));
     std::vector<unsigned long long *> xs(ngpu);
     for (int d = 0; d < ngpu; ++d) {
         TrsvMgpuDev &q = H->D[d];
@@ -1636,6 +1640,17 @@ int sblas_trsv_mgpu_run(sblas_trsv_mgpu H, const double *b, double *x, double *s
 {
     if (!H || !b || !x) return SBLAS_ERR_INVALID;
     return trsv_mgpu_run(H, b, x, solve_ms);
+}
+
+int sblas_trsv_mgpu_info(sblas_trsv_mgpu H, int *nblocks, int *block_device, int *block_rows)
+{
+    if (!H) return SBLAS_ERR_INVALID;
+    if (nblocks) *nblocks = H->nblocks;
+    for (int d = 0; d < H->nblocks; ++d) {
+        if (block_device) block_device[d] = H->D[d].phys;
+        if (block_rows) block_rows[d] = H->D[d].nloc;
+    }
+    return SBLAS_OK;
 }
 
 int sblas_trsv_mgpu_destroy(sblas_trsv_mgpu H)

@@ -112,6 +112,10 @@ _sig("sblas_coo_sortbyrow", _i, _i, _ll, _p, _p, _p, _p)
 _sig("sblas_trsv_mgpu_create", _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i)
 _sig("sblas_trsv_mgpu_run", _i, _p, _p, _p, _p)
 _sig("sblas_trsv_mgpu_destroy", _i, _p)
+_sig("sblas_trsv_mgpu_info", _i, _p, _p, _p, _p)
+_sig("sblas_ctx_comm_info", _i, _p, _p, _p)
+_sig("sblas_test_deny_peer_access", _i, _i)
+_sig("sblas_peer_refs", _i, _i, _i)
 _sig("sblas_ctx_create", _i, _p, _i, _p)
 _sig("sblas_ctx_destroy", _i, _p)
 _sig("sblas_ctx_ngpu", _i, _p, _p)
@@ -356,6 +360,15 @@ class TrsvMgpu:
         x = x[:self.n * self.rhs]
         return (x if self.rhs == 1 else x.reshape(self.n, self.rhs)), ms.value
 
+    def info(self):
+        """[(device, rows)] per block (sblas_trsv_mgpu_info)."""
+        nb = C.c_int()
+        check(lib.sblas_trsv_mgpu_info(self.h, C.byref(nb), None, None), "trsv_mgpu_info")
+        dv = np.zeros(nb.value, np.int32)
+        rw = np.zeros(nb.value, np.int32)
+        check(lib.sblas_trsv_mgpu_info(self.h, None, ptr(dv), ptr(rw)), "trsv_mgpu_info")
+        return [(int(d), int(r)) for d, r in zip(dv, rw)]
+
     def close(self):
         if self.h:
             lib.sblas_trsv_mgpu_destroy(self.h)
@@ -590,6 +603,17 @@ class DeviceCtx:
         check(lib.sblas_ctx_slice_info(self.h, d, C.byref(r), C.byref(z), C.byref(b)), "ctx_slice_info")
         return r.value, z.value, b.value
 
+    def comm_info(self):
+        """(RCCL rank count, device ordinal per context rank) as the
+        communicator reports them (ncclCommCount / ncclCommCuDevice; rank
+        count 0 for a loopback context)."""
+        nr = C.c_int()
+        g = C.c_int()
+        check(lib.sblas_ctx_ngpu(self.h, C.byref(g)), "ctx_ngpu")
+        dv = np.zeros(g.value, np.int32)
+        check(lib.sblas_ctx_comm_info(self.h, C.byref(nr), ptr(dv)), "ctx_comm_info")
+        return nr.value, [int(d) for d in dv]
+
     def slice_algo(self, d: int) -> int:
         """The SpMV algorithm device d's slice runs (resolved when AUTO)."""
         a = C.c_int()
@@ -685,3 +709,13 @@ class DeviceTRSV:
             self.close()
         except Exception:
             pass
+
+
+def test_deny_peer_access(on: bool) -> None:
+    """Test hook: refuse every peer link (sblas_test_deny_peer_access)."""
+    check(lib.sblas_test_deny_peer_access(int(bool(on))), "test_deny_peer_access")
+
+
+def peer_refs(a: int, b: int) -> int:
+    """References the library holds on the a -> b peer link."""
+    return int(lib.sblas_peer_refs(a, b))

@@ -3,6 +3,7 @@ N GPUs or exit non-zero -- one process per GPU under a launcher (WORLD_SIZE
 set), else one process driving N GPUs through the C-ABI context (sblas_ctx),
 mirroring the reference's single host call over every GPU
 (spmv/test/dspmv_test.cu:355-383 -> spmv/src/dspmv_mgpu_v1.cu:16-280)."""
+import json
 import os
 import subprocess
 import sys
@@ -166,3 +167,70 @@ def test_traffic_requires_matching_library_hash(tmp_path, monkeypatch):
     (prof / "pmc_z.json").write_text(json.dumps({"hbm_bytes_per_launch": 7.0e8}))
     assert bench._stamped_traffic("z") is None
     assert bench._stamped_traffic("absent") is None
+
+
+def _child(leg, budget):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_PROC_BIND="close", OMP_PLACES="cores")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-baseline-only", "--cpu-leg", leg,
+                        "--cpu-budget", str(budget)], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_cpu_baseline_sptrsv_child_is_the_reference_serialref():
+    """configs[4]'s CPU baseline: the reference's own
+    serial analyser + executor (sptrsv_syncfree_serialref.h, compiled in place
+    into oracle/_ref) on the full known-answer system, one core, x exact."""
+    b = _child("sptrsv", 1)
+    for k in ("value", "unit", "cores", "kind", "sample", "executor_ms", "analyser_ms", "check_exact_vs_xref"):
+        assert k in b, k
+    assert b["cores"] == 1 and b["check_exact_vs_xref"] is True and b["value"] > 0
+    ref_built = os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libsblas_ref.so"))
+    assert b["kind"] == ("reference" if ref_built else "port")
+
+
+def test_cpu_baseline_spmm_child_sweeps_threads():
+    """configs[3]'s CPU baseline: orc_spmm_omp over the full rail4284-shaped
+    product, thread count swept like the SpMV baseline."""
+    b = _child("spmm", 1)
+    for k in ("value", "unit", "cores", "kind", "sample", "thread_sweep_gflops", "ms_per_call"):
+        assert k in b, k
+    assert b["kind"] == "port" and b["value"] > 0 and str(b["cores"]) in b["thread_sweep_gflops"]
+
+
+def test_every_leg_carries_cpu_baseline_and_check(monkeypatch):
+    """attach_cpu_baselines puts a CPU baseline on the headline AND on the
+    config4 / config5 legs; the headline's post-timing oracle check is on by
+    default in both drivers (`check_vs_oracle`)."""
+    seen = []
+    monkeypatch.setattr(bench, "cpu_baseline", lambda args, leg="spmv": seen.append(leg) or {"leg": leg})
+    out = {"config4": {}, "config5": {}}
+    bench.attach_cpu_baselines(out, None)
+    assert out["cpu_baseline"] == {"leg": "spmv"}
+    assert out["config4"]["cpu_baseline"] == {"leg": "spmm"}
+    assert out["config5"]["cpu_baseline"] == {"leg": "sptrsv"}
+    out = {}
+    bench.attach_cpu_baselines(out, None)
+    assert "config4" not in out and "config5" not in out
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "args.check = not args.no_check" in src
+    assert src.count('out["check_vs_oracle"] = check') == 2
+    assert src.count("        attach_cpu_baselines(out, args)") == 2
+
+
+def test_topology_object_keys():
+    """Every line says what it ran on: communicator rank
+    count, per-rank device ordinal and PCI address, peer-access matrix."""
+    t = bench.topology_object("torch (one process per GPU)", "nccl", 8, list(range(8)),
+                              [f"0000:{b:02x}:00" for b in range(8)], [[1] * 8 for _ in range(8)])
+    for k in ("driver", "backend", "comm_ranks", "device_ordinals", "pci_bus", "visible_devices",
+              "peer_access", "all_pairs_peer"):
+        assert k in t, k
+    assert t["comm_ranks"] == 8 and t["all_pairs_peer"] and t["visible_devices"] == 8
+    t2 = bench.topology_object("ctx", "loopback (no communicator)", 0, [0, 0], [None, None], [[1]], note="x")
+    assert t2["comm_ranks"] == 0 and t2["note"] == "x"
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('out["topology"] = ') == 2
+    assert 'out["block_devices"] = ' in src

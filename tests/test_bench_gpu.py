@@ -38,6 +38,7 @@ def test_bench_ctx_driver(algo, partition, exchange):
     assert line["check_vs_oracle"] is True
     assert line["n_gpus"] == 1
     assert line["config"]["driver"].startswith("ctx")
+    assert line["topology"]["comm_ranks"] == 1 and line["topology"]["device_ordinals"] == [0]
     assert line["config"]["exchange"] == exchange
     assert line["ms_per_step"] > 0 and line["kernel_ms_max_over_ranks"] > 0
     assert line["ms_per_step"] >= line["kernel_ms_max_over_ranks"]
@@ -78,6 +79,13 @@ def test_bench_ctx_loopback(gpus, algo, partition, exchange):
     assert line["check_vs_oracle"] is True, line
     assert line["n_gpus"] == gpus and "loopback" in line["note"]
     assert len(line["kernel_ms_per_device"]) == gpus
+    # first-contact readiness: what the line ran on
+    topo = line["topology"]
+    assert topo["comm_ranks"] == 0 and topo["backend"].startswith("loopback")
+    assert len(topo["device_ordinals"]) == gpus and len(topo["pci_bus"]) == gpus
+    nd = topo["visible_devices"]
+    assert topo["device_ordinals"] == [d % nd for d in range(gpus)]
+    assert len(topo["peer_access"]) == nd and all(len(r) == nd for r in topo["peer_access"])
     assert sum(line["nnz_per_device"]) == line["config"]["nnz"]
     c3 = line["config3"]
     assert c3["check"] is True and c3["n_gpus"] == gpus and c3["exchange"] == "allreduce", c3

@@ -374,3 +374,46 @@ def test_ctx_loopback_cost_partition_config2_g8(torch_cuda, sb, orc, monkeypatch
     for d in range(1, 8):
         assert np.array_equal(got[0], got[d])
     ctx.close()
+
+
+def test_ctx_two_contexts_peer_refcount(torch_cuda, sb, orc, monkeypatch):
+    """peer links are reference-counted per process.  Two loopback
+    all-reduce contexts over the same device pair (distinct GPUs where the
+    box has two, else both ranks on one GPU, which needs no link), the first
+    destroyed, the second still runs and matches the oracle; a trsv_mgpu
+    handle on the same pair holds its own reference."""
+    monkeypatch.setenv("SBLAS_CTX_LOOPBACK", "1")
+    ndev = torch_cuda.cuda.device_count()
+    rng = np.random.default_rng(7)
+    m, n = 4000, 4000
+    rp, col, val = rand_csr(rng, m, n, 30)
+    x = rng.standard_normal(n)
+    y = rng.standard_normal(m)
+    alpha, beta = orc.alpha_beta()
+    want = orc.csr_spmv(rp, col, val, x, alpha, beta, y)
+    bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y)
+    link = 1 if ndev >= 2 else 0
+    ctxs = []
+    for _ in range(2):
+        c = sb.DeviceCtx(2)
+        c.upload(m, n, rp, col, val, 2, 1, 1)  # CSR5, nnz split, all-reduce
+        c.set_x(x)
+        c.set_y(y)
+        ctxs.append(c)
+    assert sb.peer_refs(0, 1) == 2 * link
+    nr, ords = ctxs[0].comm_info()
+    assert nr == 0 and ords == [d % ndev for d in range(2)]  # loopback: no communicator
+    ctxs[0].close()
+    assert sb.peer_refs(0, 1) == link
+    ctxs[1].spmv(alpha, beta)
+    assert np.all(np.abs(ctxs[1].get_y(0) - want) <= bound)
+    ctxs[1].close()
+    assert sb.peer_refs(0, 1) == 0
+
+
+def test_ctx_comm_info_rccl(torch_cuda, sb):
+    """A real (one-rank) RCCL communicator reports its rank count and device
+    through sblas_ctx_comm_info (the `topology` of every bench line)."""
+    ctx = sb.DeviceCtx(1)
+    assert ctx.comm_info() == (1, [0])
+    ctx.close()

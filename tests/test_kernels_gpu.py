@@ -901,3 +901,50 @@ def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols):
     # columns are sorted) with exact zeros for the holes: same bound applies
     assert np.all(np.abs(got - want) <= spmm_bound(rp, col, val, B, 0.75, -0.5, C0))
     A.close()
+
+
+@pytest.mark.parametrize("blocks", [1, 4])
+def test_sptrsv_mgpu_block_devices(torch_cuda, sb, blocks):
+    """sblas_trsv_mgpu_info: the device each block runs on and its rows (the
+    `config5.blocks4.block_devices` of every bench line): block d on device
+    d % visible, rows summing to n."""
+    n = 50_000
+    cp, ri, v, b0, xref = _banded_system(sb, n)
+    ngpu = min(blocks, torch_cuda.cuda.device_count())
+    H = sb.TrsvMgpu(cp, ri, v, n, ngpu, tasks=blocks // ngpu)
+    info = H.info()
+    assert len(info) == blocks and sum(r for _, r in info) == n
+    assert [d for d, _ in info] == [d % ngpu for d in range(blocks)]
+    x, _ = H.run(b0)
+    assert np.abs(x - xref).sum() / np.abs(xref).sum() <= 1e-12
+    H.close()
+
+
+def test_sptrsv_mgpu_peer_refusal_is_bounded(torch_cuda, sb):
+    """a multi-block solve whose peer links cannot be
+    enabled fails at create with SBLAS_ERR_* before launching anything (no
+    block spins on stores that can never arrive), in bounded time; the hook
+    (sblas_test_deny_peer_access) treats blocks sharing the GPU as distinct
+    devices so the refusal runs here.  After the hook is cleared the same
+    solve runs and is exact."""
+    import time
+    n = 50_000
+    cp, ri, v, b0, xref = _banded_system(sb, n)
+    sb.test_deny_peer_access(True)
+    try:
+        t0 = time.perf_counter()
+        with pytest.raises(sb.SblasError, match="peer"):
+            sb.TrsvMgpu(cp, ri, v, n, 1, tasks=4)
+        with pytest.raises(sb.SblasError, match="peer"):
+            sb.trsv_mgpu_solve_tasks(cp, ri, v, n, b0, 1, 4)
+        assert time.perf_counter() - t0 < 30.0
+        H1 = sb.TrsvMgpu(cp, ri, v, n, 1, tasks=1)  # one block: no peer link needed
+        x1, _ = H1.run(b0)
+        H1.close()
+    finally:
+        sb.test_deny_peer_access(False)
+    assert np.abs(x1 - xref).sum() / np.abs(xref).sum() <= 1e-12
+    H = sb.TrsvMgpu(cp, ri, v, n, 1, tasks=4)
+    x, _ = H.run(b0)
+    H.close()
+    assert np.abs(x - xref).sum() / np.abs(xref).sum() <= 1e-12
