@@ -980,6 +980,43 @@ def topology_object(driver, backend, nranks, ordinals, pci, peers, note=None):
     return out
 
 
+def deterministic_leg(args, torch, sblas, op, algo, x, local_bytes, nnz, stream, evict):
+    """`deterministic_beside` (N = 1): the headline's
+    handle switched to deterministic mode (sblas_csr_set_deterministic: the
+    same plan, xsort's ordered-add form), the same cold protocol; then two
+    fresh launches from one y0 compared bit for bit."""
+    A = op.A
+    sp = stream.cuda_stream
+    A.deterministic = True
+    try:
+        with torch.cuda.stream(stream):
+            for _ in range(2):
+                A.spmv(algo, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp)
+            ts = []
+            for _ in range(args.steps):
+                evict()
+                torch.cuda.synchronize()
+                ts.append(A.spmv_timed(algo, ALPHA, x.data_ptr(), BETA, op.y_local.data_ptr(), sp))
+            y0 = op.y_local.clone()
+            ys = []
+            for _ in range(2):
+                y = y0.clone()
+                A.spmv(algo, ALPHA, x.data_ptr(), BETA, y.data_ptr(), sp)
+                ys.append(y)
+            torch.cuda.synchronize()
+        same = bool(torch.equal(ys[0], ys[1]))
+    finally:
+        A.deterministic = False
+    t = float(np.mean(ts))
+    names = {sblas.ROWSPLIT: "rowsplit", sblas.CSR5: "csr5", sblas.PANEL: "panel", sblas.XSORT: "xsort"}
+    return {"algo": names.get(algo, str(algo)) + (" (ordered adds)" if algo == sblas.XSORT else ""),
+            "kernel_ms": round(t, 5), "gflops": round(2.0 * nnz / (t * 1e-3) / 1e9, 3),
+            "roofline_frac": round(local_bytes / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "bitwise_equal_two_launches": same, "cache": "cold",
+            "how": "sblas_csr_set_deterministic(A, 1) on the headline's plan (SBLAS_DETERMINISTIC=1 sets it "
+                   "for every new handle); AUTO's pick unchanged"}
+
+
 def _gather_rows(torch, dist, dev, row, world):
     """Every rank's stats row (numpy), as a (world, len) array."""
     if dist is None:
@@ -1603,6 +1640,9 @@ def main() -> int:
                            "cache": "cold",
                            # the row blocks' layout: 0 = plain, P = per XCD column panel
                            "xcd_panels": op.A.panels(sblas.ROWSPLIT)}
+    deterministic_beside = None
+    if world == 1 and not args.no_rowsplit_beside:
+        deterministic_beside = deterministic_leg(args, torch, sblas, op, algo, x, local_bytes, nnz, stream, evict)
     config3 = None
     if not args.no_config3:
         config3 = torch_config3(args, W, sblas, sblas_dist, torch, dist, rank, world, dev_idx, x, x_h, stream,
@@ -1733,6 +1773,8 @@ def main() -> int:
             out["check_vs_oracle"] = check
         if rowsplit_beside is not None:
             out["rowsplit_beside"] = rowsplit_beside
+        if deterministic_beside is not None:
+            out["deterministic_beside"] = deterministic_beside
         if config3 is not None:
             out["config3"] = config3
         if config4 is not None:

@@ -168,12 +168,22 @@ int sblas_spmv_timed(sblas_csr A, int algo, double alpha, const double *d_x,
  * is unsupported for the matrix, sblas_csr_analyse falls back to PANEL and the
  * choice becomes PANEL.  SBLAS_AUTO=<1..5> overrides the choice. */
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
+/* Bitwise-repeatable SpMV on this handle (on != 0).  ROWSPLIT, CSR5 and
+ * PANEL always are (each row's sum in a fixed order); XSORT then runs its
+ * ordered form (a stream's chunks added in chunk order, the narrow group
+ * walk fixed per range): the same y bit for bit on every call, within the
+ * same fp64 bound, at some cost (bench.py `deterministic_beside`).  AUTO's
+ * choice is unchanged.  New handles take SBLAS_DETERMINISTIC (=1: on; read
+ * once per process); the reference's cusparseDcsrmv
+ * (dspmv_mgpu_baseline.cu:163-167) is repeatable the same way. */
+int sblas_csr_set_deterministic(sblas_csr A, int on);
+int sblas_csr_get_deterministic(sblas_csr A, int *on);
 /* XCD column panels the analysed plan of `algo` runs over (0: the plain
- * layout / not analysed).  ROWSPLIT and CSR5 build per-panel plans on large
- * scattered-column matrices (x > 8 MiB, nnz >= 4M row split / 8M CSR5 -- 4M with 2 panels
- * on rows of < 12 entries on average --, most sampled rows span
- * > n/4 of the columns; SBLAS_RS_PANEL / SBLAS_CSR5_PANEL = 0 / 1 force);
- * PANEL always does (unless only one panel holds entries). */
+ * layout / not analysed).  ROWSPLIT and CSR5 build per-panel plans (P = 4
+ * on config 2) on large scattered-column matrices (x > 8 MiB, nnz >= 2M, most
+ * sampled rows span > n/4 of the columns; test hooks "rs_panel" /
+ * "csr5_panel" force either form); PANEL always does (unless only one panel
+ * holds entries). */
 int sblas_csr_panels(sblas_csr A, int algo, int *panels);
 /* Device bytes held by the analysis of `algo` (free memory before - after
  * sblas_csr_analyse; 0 if not analysed): the layout's cost beside the CSR. */
@@ -351,7 +361,7 @@ int sblas_ctx_comm_info(sblas_ctx ctx, int *nranks, int *devices);
  * ceil(m/(8g)) rows on device j % g; whole rows), 1 = spMV_mgpu_v1's
  * nnz-balanced split with split rows merged on the device, 2 = the
  * cost-weighted whole-row split (sblas_partition_cost, w =
- * SBLAS_CTX_ROW_COST, 3 by default).  Exchange SBLAS_CTX_ALLGATHER. */
+ * 3, the cost of a row end in CSR5 entries).  Exchange SBLAS_CTX_ALLGATHER. */
 int sblas_ctx_matrix_upload(sblas_ctx ctx, int m, int n, const long long *rowptr,
                             const int *col, const double *val, int algo, int partition);
 /* Same with the exchange chosen (sblas_ctx_exchange); SBLAS_CTX_ALLREDUCE
@@ -504,6 +514,13 @@ int sblas_hbm_probe_timed(int mode, const void *src, void *dst, long long bytes,
 int sblas_test_deny_peer_access(int on);
 /* References the library holds on the a -> b peer link (0: none). */
 int sblas_peer_refs(int a, int b);
+/* Planner override for tests (set = 0 clears it), read when a plan is built:
+ * "xs_cap" (xsort work per item: small values give many items, exercising the
+ * dynamic claims on small matrices), "xs_allwide" (0/1), "xs_solo" (0/1),
+ * "spmm_ctile" (0/1: C-tile form), "spmm_mfma_fill" (MFMA tile threshold),
+ * "rs_panel" / "csr5_panel" (0/1: XCD-panel forms), "panels" (panel count).
+ * Process-wide; production code never sets them. */
+int sblas_test_set_option(const char *name, double value, int set);
 
 #ifdef __cplusplus
 }

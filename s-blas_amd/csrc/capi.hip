@@ -2,6 +2,9 @@
 #include <algorithm>
 #include <cstring>
 #include <limits>
+#include <map>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "sblas_internal.hpp"
@@ -40,9 +43,43 @@ LaunchTimer &launch_timer()
     static thread_local LaunchTimer t;
     return t;
 }
+
+// Test hooks: planner overrides set through sblas_test_set_option (never
+// from the environment), read when a plan is built.
+namespace {
+std::mutex g_opt_mu;
+std::map<std::string, double> g_opt;
+}  // namespace
+
+bool test_option(const char *name, double *value)
+{
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    auto it = g_opt.find(name);
+    if (it == g_opt.end()) return false;
+    if (value) *value = it->second;
+    return true;
+}
+
+bool deterministic_default()
+{
+    static const bool on = [] {
+        const char *e = getenv("SBLAS_DETERMINISTIC");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
 }  // namespace sblas
 
 extern "C" {
+
+int sblas_test_set_option(const char *name, double value, int set)
+{
+    if (!name) return SBLAS_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    if (set) g_opt[name] = value;
+    else g_opt.erase(name);
+    return SBLAS_OK;
+}
 
 const char *sblas_status_string(int s)
 {
@@ -356,6 +393,20 @@ bool plan_ready(const sblas_csr_s &A, int algo)
     }
 }
 } // namespace
+
+int sblas_csr_set_deterministic(sblas_csr A, int on)
+{
+    if (!A) return SBLAS_ERR_INVALID;
+    A->deterministic = on != 0;
+    return SBLAS_OK;
+}
+
+int sblas_csr_get_deterministic(sblas_csr A, int *on)
+{
+    if (!A || !on) return SBLAS_ERR_INVALID;
+    *on = A->deterministic ? 1 : 0;
+    return SBLAS_OK;
+}
 
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo)
 {

@@ -674,9 +674,8 @@ int sblas_ctx_matrix_upload_ex(sblas_ctx C, int m, int n, const long long *rowpt
         if (partition == 1) {
             SBLAS_TRY(sblas_partition_nnz(m, C->nnz, rowptr, g, si.data(), ei.data(), sr.data(), er.data(),
                                           sf.data()));
-        } else {  // cost-weighted whole rows: per-row weight SBLAS_CTX_ROW_COST (default 3)
-            const char *we = getenv("SBLAS_CTX_ROW_COST");
-            SBLAS_TRY(sblas_partition_cost(m, rowptr, g, we ? atof(we) : kCtxRowCost, si.data(), ei.data(),
+        } else {  // cost-weighted whole rows: per-row weight kCtxRowCost
+            SBLAS_TRY(sblas_partition_cost(m, rowptr, g, kCtxRowCost, si.data(), ei.data(),
                                            sr.data(), er.data(), sf.data()));
         }
         C->h_meta.assign((size_t)3 * g, 0);

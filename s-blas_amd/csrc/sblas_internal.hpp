@@ -90,7 +90,7 @@ struct Csr5Plan {
     int *head_run = nullptr;       // [ntiles] > 0: tile t starts a run of that many tiles whose heads
                                    // continue one row (calibrated together), else 0
     bool ready = false;
-    int form = 2;                  // tile form (SBLAS_C5_PF, read at plan build; spmv.hip c5_form_env)
+    int form = 2;                  // tile form (spmv.hip c5_form_env; alternatives in experiment builds)
     // XCD-affine form (spmv.hip "CSR5 over column panels"): one tile plan per
     // column panel of the panel plan, panel p's tiles dealt to the XCDs with
     // blockIdx % P == p, alpha-scaled partial y per panel, then a reduce.
@@ -196,46 +196,32 @@ struct XsRange {
     int row0;
     int nrows;
     int wide;
-    int widx;         // wide: index among the wide ranges (arrival counter), else -1
-    long long pbase;  // wide: offset of the range's [G][nrows] partials
+    int widx;         // wide: index among the wide ranges, else -1
+    long long pbase;  // wide: offset of the range's [8][nrows] partials
 };
 
 struct XsArgs {
-    const XsRange *ranges;
-    const long long *blk;   // [nranges*G + 1] block offsets
     const uint32_t *key;
     const double *val;
     const long long *xrec;  // per (slot, team): sub, row0|nrows<<32, pbase, widx, G+1 block offsets
-    const int *qitems;      // [8][qstride][2] sub-item pairs (range << 8 | XCD + 1, 0 = narrow; -1 = none)
     int *qhead;             // [8] claim heads of this launch (start past the static items)
     int *qreset;            // the other parity's heads, re-armed to qstat by block 0
     int qstat[8];           // items per queue taken statically (block b: queue b%8, index b/8)
     int dynamic;            // items beyond the static share exist (claims needed)
-    int fused;              // wide ranges reduced in-kernel (xs_reduce_phase)
-    int nrtasks;
-    const int2 *rtasks;     // (range, first row) reduce tasks
-    unsigned *arrive;       // per wide range: sub-items counted in, cumulative
-    unsigned epoch;         // this launch's number (want 8 * epoch arrivals)
     double *partial;
     int qlen[8];
     int qstride;
     int G, q, Wg;
-    int use_xcc;
     int kstride, vstride;   // chunk strides in 16-B units (keys, values)
-    long long *trace;       // debugging aid (SBLAS_XS_TRACE), else null
 };
 
 struct XsPlan {
     int G = 0, q = 0, Wg = 0;
-    int nranges = 0, nwide = 0, nitems = 0, grid = 0, nt = 0;
-    XsRange *ranges = nullptr;
-    int *wide = nullptr;         // [nwide] range ids
+    int nranges = 0, nwide = 0, nitems = 0, grid = 0;
     XsRange *wranges = nullptr;  // [nwide] the wide ranges' records (k_xsort_reduce)
-    long long *blk = nullptr;
-    uint32_t *key = nullptr;     // owns the chunk storage (keys and values)
-    double *val = nullptr;       // values inside it (interleaved per chunk by default)
+    uint32_t *key = nullptr;     // owns the chunk storage (keys and values, interleaved per chunk)
+    double *val = nullptr;       // values inside it
     int kstride = 64, vstride = 128;
-    int *qitems = nullptr;
     long long *xrec = nullptr;   // item records (see XsArgs)
     int *qhead = nullptr;        // [2][16]: claim heads per launch parity
     mutable int parity = 0;      // flips every launch (stream-ordered launches)
@@ -243,18 +229,9 @@ struct XsPlan {
     int qlen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int qstat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int dynamic = 0;
-    bool fused = false;          // in-kernel reduce of the wide ranges
-    int nrtasks = 0;
-    int2 *rtasks = nullptr;
-    unsigned *arrive = nullptr;
-    mutable long long epoch = 0; // launches so far (arrival counters are cumulative)
     int qstride = 0;
     long long nchunks = 0;       // 256-entry chunks (blocks padded to whole chunks)
-    bool pair = true;            // items pair two sub-items (two teams of waves)
-    int split = 8;               // waves of a pair's first team (of 16)
-    bool dyn = true;             // pairs claim chunks dynamically (teams drain each other's streams)
     bool solo = false;           // narrow ranges are items of their own (16,384 LDS rows)
-    int u = 1;                   // chunks per dynamic claim (planner; SBLAS_XS_U)
     int maxc = 0;                // most chunks of one item (both sub-items)
     bool ready = false;
 };
@@ -268,9 +245,15 @@ struct RsPlan {
     int nslots = 0;
     bool ready = false;
     bool panels = false;           // run as the panel plan (XCD column panels, spmv.hip xcd_panels_pay)
-    bool seq = true;               // consecutive entries per thread (SBLAS_RS_SEQ=0: vec4 order), read at build
+    bool seq = true;               // consecutive entries per thread (experiment build SBLAS_RS_SEQ=0: vec4 order)
 };
 
+}  // namespace sblas
+
+namespace sblas {
+// SBLAS_DETERMINISTIC=1 (read once): new handles default to repeatable
+// (bitwise) SpMV results (sblas_csr_set_deterministic).
+bool deterministic_default();
 }  // namespace sblas
 
 struct sblas_csr_s {
@@ -295,6 +278,7 @@ struct sblas_csr_s {
     mutable size_t spmm_part_bytes = 0;
     long long plan_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device bytes per algorithm's plan
     int auto_algo = 0;          // SBLAS_SPMV_AUTO's choice (capi.hip pick_algo), 0 = not yet
+    bool deterministic = sblas::deterministic_default();  // bitwise-repeatable launches (xsort's ordered form)
     double col_adjacency = -1;  // its locality probe
     double col_maxshare = -1;   // its largest eighth-of-the-columns share of the sampled entries
     double col_scattered = -1;  // share of sampled rows whose columns span > n/4
@@ -358,6 +342,12 @@ struct DeviceGuard {
 int peer_acquire(int a, int b, const char *who);
 void peer_release(int a, int b);
 bool peer_denied();  // the test hook's state
+
+// Test hooks (capi.hip): a planner override set by sblas_test_set_option;
+// false when unset.  Names: "xs_cap", "xs_allwide", "xs_solo" (xsort
+// planner), "spmm_ctile", "spmm_mfma_fill" (SpMM plan form), "rs_panel",
+// "csr5_panel", "panels" (XCD-panel forms).
+bool test_option(const char *name, double *value);
 
 // Host helpers shared by capi / refapi (host_utils.cpp).
 int row_of_index(int m, const long long *rowptr, long long idx);

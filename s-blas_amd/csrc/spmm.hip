@@ -411,11 +411,18 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
 {
     SpmmPlan &P = A.mm;
     const int m = A.m, k = A.n;
-    int wlog = 11;  // 2048 B rows = 1 MiB of B per slab at n = 64
-    if (const char *e = getenv("SBLAS_SPMM_CTW")) wlog = std::max(4, std::min(20, atoi(e)));
+    // slab width 2^wlog columns (11: 2048 B rows = 1 MiB of B per slab at n =
+    // 64) and tile rows: experiment builds (Makefile `alt`) set
+    // -DSBLAS_SPMM_CTW / -DSBLAS_SPMM_CTR
+#ifndef SBLAS_SPMM_CTW
+#define SBLAS_SPMM_CTW 11
+#endif
+#ifndef SBLAS_SPMM_CTR
+#define SBLAS_SPMM_CTR kCtMaxRows
+#endif
+    const int wlog = std::max(4, std::min(20, SBLAS_SPMM_CTW));
     const int rcap = kCtMaxRows;
-    int rmax = rcap;  // experiments: SBLAS_SPMM_CTR caps the tile rows
-    if (const char *e = getenv("SBLAS_SPMM_CTR")) rmax = std::max(16, std::min(rcap, atoi(e)));
+    const int rmax = std::max(16, std::min(rcap, (int)(SBLAS_SPMM_CTR)));
     const int nrb = (m + rmax - 1) / rmax;
     const int R = (m + nrb - 1) / nrb;
     int rbits = 1;
@@ -431,8 +438,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // rank slices: config 4's N = 8 row block 105 -> 127 us, twice the
     // partial slots for the reduce; profiles/r05/spmm_grid/)
     const int ncg = std::max(1, (ncols + kCtCols - 1) / kCtCols);
-    int ns = std::max(1, 32 / (nrb * ncg));
-    if (const char *e = getenv("SBLAS_SPMM_CTNS")) ns = std::max(1, atoi(e));
+    const int ns = std::max(1, 32 / (nrb * ncg));
     // per-slab entry counts -> contiguous sets of about equal entries per XCD
     std::vector<long long> scount((size_t)nslab, 0);
     for (long long e = 0; e < A.nnz; ++e) scount[(size_t)(hcol[(size_t)e] >> wlog)]++;
@@ -457,8 +463,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     for (int b = 0; b < nbk; ++b) off[(size_t)b + 1] += off[(size_t)b];
     // direct keys (global column << rbits | row) when the column fits: the
     // kernel then needs no slab arithmetic; sorting is the same order
-    const bool direct = (long long)k <= (1LL << (32 - rbits)) && !(getenv("SBLAS_SPMM_CTDIRECT") &&
-                                                                     atoi(getenv("SBLAS_SPMM_CTDIRECT")) == 0);
+    const bool direct = (long long)k <= (1LL << (32 - rbits));
     std::vector<unsigned long long> kv((size_t)std::max<long long>(A.nnz, 1));  // key << 32 | entry index
     {
         std::vector<long long> next(off.begin(), off.end() - 1);
@@ -477,7 +482,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
     // in parity.  So inside each aligned 8-entry step, odd rows go to the even
     // slots and even rows to the odd slots as far as the step allows (the
     // order inside a step does not change which products are summed).
-    const bool pair_rows = !(getenv("SBLAS_SPMM_CTPAIR") && atoi(getenv("SBLAS_SPMM_CTPAIR")) == 0);
+    constexpr bool pair_rows = true;
 #pragma omp parallel for schedule(dynamic, 1)
     for (int b = 0; b < nbk; ++b) {
         std::sort(kv.begin() + off[(size_t)b], kv.begin() + off[(size_t)b + 1]);
@@ -499,7 +504,7 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
             }
         }
     }
-    // Column-run slots (opt-in, SBLAS_SPMM_CTSLOT=1): consecutive entries of
+    // Column-run slots (experiment builds, -DSBLAS_SPMM_CTSLOT=1): consecutive entries of
     // one column are paired into slots of two so one B segment feeds both
     // (rail4284: 0.59 slots per entry).  Measured slower on config 4: 0.435
     // against 0.362 ms -- L2 misses 10.0M against 6.0M per launch and more TD
@@ -516,8 +521,10 @@ static int build_ctile(sblas_csr_s &A, const std::vector<int> &rp, const std::ve
         }
         soff[(size_t)b + 1] = soff[(size_t)b] + ns_b;
     }
-    bool slots = false;
-    if (const char *e = getenv("SBLAS_SPMM_CTSLOT")) slots = atoi(e) != 0 && A.nnz > 0;
+#ifndef SBLAS_SPMM_CTSLOT
+#define SBLAS_SPMM_CTSLOT 0
+#endif
+    const bool slots = SBLAS_SPMM_CTSLOT != 0 && A.nnz > 0;
     const long long nunits = slots ? soff.back() : A.nnz;
     std::vector<unsigned> hkey((size_t)std::max<long long>(nunits, 1)), hkey2;
     std::vector<double> hv((size_t)std::max<long long>(nunits, 1)), hv2;
@@ -604,7 +611,8 @@ int build_spmm_plan(sblas_csr_s &A, int ncols, hipStream_t s)
 {
     if (A.mm.ready) return SBLAS_OK;
     SpmmPlan &P = A.mm;
-    if (const char *e = getenv("SBLAS_SPMM_MFMA_FILL")) P.fill_thresh = atof(e);
+    double opt = 0.0;
+    if (test_option("spmm_mfma_fill", &opt)) P.fill_thresh = opt;  // test hook
     const int m = A.m;
     const std::vector<int> &rp = A.h_rowptr;
     std::vector<int> hcol((size_t)A.nnz);
@@ -671,10 +679,10 @@ int build_spmm_plan(sblas_csr_s &A, int ncols, hipStream_t s)
     SBLAS_TRY(up(&P.srows, srows));
     // C-tile form: few rows (m <= 16,384: a tile of <= 1,204 rows per CU
     // covers them in <= 14 row blocks), B much taller than the L2s (k >=
-    // 2^17: >= 64 MiB at n = 64), no MFMA blocks.  SBLAS_SPMM_CTILE=0/1
-    // overrides the size rule (0: the row-wave kernels).
+    // 2^17: >= 64 MiB at n = 64), no MFMA blocks.  The test hook
+    // "spmm_ctile" = 0/1 overrides the size rule (0: the row-wave kernels).
     bool ct = P.nmfma == 0 && m > 0 && m <= 16384 && A.n >= (1 << 17);
-    if (const char *e = getenv("SBLAS_SPMM_CTILE")) ct = atoi(e) != 0 && P.nmfma == 0 && m > 0;
+    if (test_option("spmm_ctile", &opt)) ct = opt != 0.0 && P.nmfma == 0 && m > 0;
     if (ct) {
         const int rc = build_ctile(A, rp, hcol, hval, ncols);
         if (rc != SBLAS_OK && rc != SBLAS_ERR_UNSUPPORTED) return rc;
@@ -794,11 +802,9 @@ int launch_spmm(const sblas_csr_s &A, int n, double alpha, const double *B, int 
     // rows of sparse blocks (all rows when no plan / no dense block)
     const int nrows = P.ready ? P.nsparse : A.m;
     const int *rows = P.ready ? P.srows : nullptr;
-    // long rows on average -> a workgroup per (row, slab); env override for
-    // experiments: SBLAS_SPMM_SPLITK=0/1
+    // long rows on average -> a workgroup per (row, slab)
     const long long nnz_rows = P.ready ? P.sparse_nnz : A.nnz;
-    bool splitk = nrows > 0 && nnz_rows >= 256LL * nrows;
-    if (const char *e = std::getenv("SBLAS_SPMM_SPLITK")) splitk = nrows > 0 && std::atoi(e) != 0;
+    const bool splitk = nrows > 0 && nnz_rows >= 256LL * nrows;
     if (splitk) {
         const unsigned nb = (unsigned)((long long)nrows * nslab);
         if (beta != 0.0)

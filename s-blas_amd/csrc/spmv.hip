@@ -53,8 +53,11 @@ __device__ __forceinline__ void store_y(double *p, double v)
     else *p = v;
 }
 
-// kSeq (default; SBLAS_RS_SEQ=0 selects the earlier form for the row-split
-// launch): the stream block's entries are taken lane-consecutively
+#ifndef SBLAS_RS_SEQ  // experiment builds only (Makefile `alt`): 0 = the vec4 order
+#define SBLAS_RS_SEQ 1
+#endif
+// kSeq (default; an experiment build with SBLAS_RS_SEQ=0 selects the earlier
+// form for the row-split launch): the stream block's entries are taken lane-consecutively
 // -- thread t holds entries j0 + t + 256k, so one gather instruction of a
 // wave covers 64 CONSECUTIVE entries and the TA merges lanes whose columns
 // share an x line (a banded / stencil row's runs of neighbouring columns) --
@@ -251,13 +254,15 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
 // 79 / 58, 42 / 32, 24 / 25).  So both take panels from 2M entries.
 // (Rounds 1-4 set 8M / 4M thresholds and 2 panels on short rows on the
 // correlated generator, profiles/r05/gen/, whose heavy rows shared x lines.)
-// `env` = 1 / 0 forces either form.
+// The test hook `opt` ("rs_panel" / "csr5_panel", sblas_test_set_option)
+// = 1 / 0 forces either form.
 constexpr long long kPanelMinNnz = 2000000LL;
-static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *env, long long min_nnz, bool *use)
+static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *opt, long long min_nnz, bool *use)
 {
     *use = false;
-    if (const char *e = getenv(env)) {
-        *use = atoi(e) == 1;
+    double v = 0.0;
+    if (test_option(opt, &v)) {
+        *use = v == 1.0;
         return SBLAS_OK;
     }
     if ((long long)A.n * 8 <= (8LL << 20) || A.nnz < min_nnz) return SBLAS_OK;
@@ -270,15 +275,15 @@ int build_rowsplit_plan(sblas_csr_s &A, hipStream_t s)
 {
     if (A.rs.ready) return SBLAS_OK;
     DeviceGuard g(A.device);
-    // SBLAS_RS_SEQ=0: the vec4 entry order (A/B timing; read once per plan)
-    const char *seq_env = getenv("SBLAS_RS_SEQ");
-    A.rs.seq = !seq_env || atoi(seq_env) != 0;
+    // the vec4 entry order only in experiment builds (Makefile `alt`,
+    // -DSBLAS_RS_SEQ=0)
+    A.rs.seq = SBLAS_RS_SEQ != 0;
     // the same row blocks per XCD column panel on large scattered matrices
-    // (the panel plan, algo 4's layout; SBLAS_RS_PANEL=1 / 0 forces): decided
+    // (the panel plan, algo 4's layout; test hook "rs_panel"): decided
     // first, so a panel plan never keeps a second, unused set of row blocks
     if (!A.pn.degenerate) {
         bool use = false;
-        SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_RS_PANEL", kPanelMinNnz, &use));
+        SBLAS_TRY(xcd_panels_pay(A, s, "rs_panel", kPanelMinNnz, &use));
         if (use) {
             SBLAS_TRY(build_panel_plan(A, s));
             if (!A.pn.degenerate) {
@@ -793,15 +798,13 @@ __device__ __forceinline__ void csr5_tile_st(
     }
 }
 
-// SBLAS_C5_PF selects the tile form (A/B timing; read once per plan, at
-// build_csr5_plan): 0 plain, 1 phased loads + prefetched row ends,
-// 2 (default) staged y with non-temporal y accesses, 3 staged y with plain
-// accesses
-static int c5_form_env()
-{
-    const char *e = getenv("SBLAS_C5_PF");
-    return e ? std::max(0, std::min(3, atoi(e))) : 2;
-}
+// The tile form: 2 (default) staged y with non-temporal y accesses; the
+// experiment build (Makefile `alt`, -DSBLAS_C5_PF=f) selects 0 plain, 1
+// phased loads + prefetched row ends, 3 staged y with plain accesses
+#ifndef SBLAS_C5_PF
+#define SBLAS_C5_PF 2
+#endif
+static int c5_form_env() { return std::max(0, std::min(3, SBLAS_C5_PF)); }
 
 template <bool kBeta, int kForm = 2>
 __global__ __launch_bounds__(256) void k_spmv_csr5(
@@ -908,7 +911,7 @@ __global__ void k_empty_rows(const int *__restrict__ rows, int n, double beta,
 // ---- CSR5 tile descriptors built on the device ----------------------------
 // (the reference builds its descriptors on the GPU too:
 // spmv/include/detail/cuda/format_cuda.h:21-300).  Same arrays as the host
-// builder below (kept as SBLAS_CSR5_HOSTPLAN=1): row-start bits, the row of
+// builder below (kept as the "csr5_hostplan" test hook): row-start bits, the row of
 // each tile's first element (bit 31: the tile holds empty rows), and for such
 // tiles the explicit list of rows starting in the tile.
 __global__ void k_c5_flags(const int *__restrict__ rp, int m, uint32_t *__restrict__ flags,
@@ -1120,8 +1123,10 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     DeviceGuard g(A.device);
     Csr5Plan &P = A.c5;
     P.form = c5_form_env();
-    const char *hp = getenv("SBLAS_CSR5_HOSTPLAN");
-    const char *pe = getenv("SBLAS_CSR5_PANEL");
+    // test hook "csr5_hostplan": the host-built descriptors (the device
+    // builder's cross-check, tests/test_spmv_gpu.py)
+    double hv = 0.0;
+    const bool hostplan = test_option("csr5_hostplan", &hv) && hv != 0.0;
     // Tiles per XCD column panel (each XCD's gathers in a slice of x) when x
     // outgrows an XCD's L2, the rows' columns are scattered (the probe: most
     // sampled rows span > n/4 of the columns, spread over the eighths) and
@@ -1129,20 +1134,19 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     // P = default_panels (4 on config 2) whatever the row length: on the
     // uniform config 2 4 panels beat 2 and 8 on short rows (N = 8 light rank
     // 60 vs 68 / 67 us) and are within 4-8% of 8 on 96-entry rows
-    // (profiles/r05/c5P/).  SBLAS_CSR5_PANEL=1 / 0 forces either form,
-    // SBLAS_PANELS the count.
-    (void)pe;
+    // (profiles/r05/c5P/).  Test hooks "csr5_panel" (1 / 0 forces either
+    // form) and "panels" (the count).
     const int npanels = default_panels(A);
     bool panels = false;
-    SBLAS_TRY(xcd_panels_pay(A, s, "SBLAS_CSR5_PANEL", kPanelMinNnz, &panels));
-    if (panels && npanels >= 2 && !(hp && atoi(hp) == 1)) {
+    SBLAS_TRY(xcd_panels_pay(A, s, "csr5_panel", kPanelMinNnz, &panels));
+    if (panels && npanels >= 2 && !hostplan) {
         const int rc = build_csr5_panels(A, npanels, s);
         if (rc == SBLAS_OK) return SBLAS_OK;
         free_csr5_arrays(P);
         A.c5 = Csr5Plan{};
         if (rc != SBLAS_ERR_UNSUPPORTED) return rc;
     }
-    if (!(hp && atoi(hp) == 1)) return build_csr5_core(P, A.rowptr, A.col, A.val, A.m, A.nnz, s);
+    if (!hostplan) return build_csr5_core(P, A.rowptr, A.col, A.val, A.m, A.nnz, s);
     const long long nnz = A.nnz;
     const std::vector<int> &rp = A.h_rowptr;
     P.ntiles = (nnz + kC5Tile - 1) / kC5Tile;
@@ -1489,11 +1493,12 @@ static void free_panel_csr(PanelCsr &o)
 }
 
 // ~4 MiB of x per panel (one XCD's L2), at most one panel per XCD (config 2:
-// P = 4 beats 8, fewer partial-y bytes); SBLAS_PANELS overrides
+// P = 4 beats 8, fewer partial-y bytes); the test hook "panels" overrides
 static int default_panels(const sblas_csr_s &A)
 {
     int P = (int)std::min<long long>(8, std::max<long long>(1, ((long long)A.n * 8 + (4 << 20) - 1) >> 22));
-    if (const char *e = getenv("SBLAS_PANELS")) P = std::max(1, std::min(64, atoi(e)));
+    double v = 0.0;
+    if (test_option("panels", &v)) P = std::max(1, std::min(64, (int)v));
     if (A.n < P) P = std::max(1, A.n);
     return P;
 }
@@ -1591,10 +1596,12 @@ int launch_spmv_panel(const sblas_csr_s &A, double alpha, const double *x, doubl
     if (Q.degenerate) return launch_spmv_rowsplit(A, alpha, x, beta, y, s);
     if (A.m == 0) return SBLAS_OK;
     const long long grid = (long long)Q.maxblocks * Q.P;
-    static const bool sc1 = [] {
-        const char *e = getenv("SBLAS_PANEL_SC1");
-        return e && atoi(e) != 0;
-    }();
+    // agent-scope stores of the partials: experiment builds only (Makefile
+    // `alt`, -DSBLAS_PANEL_SC1=1)
+#ifndef SBLAS_PANEL_SC1
+#define SBLAS_PANEL_SC1 0
+#endif
+    constexpr bool sc1 = SBLAS_PANEL_SC1 != 0;
     if (grid > 0) {
         if (sc1)
             SBLAS_LAUNCH(k_spmv_panel<true>, dim3((unsigned)grid), dim3(kRsThreads), 0, s,

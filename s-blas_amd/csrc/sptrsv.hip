@@ -51,7 +51,7 @@ struct sblas_trsv_s {
     unsigned *ctl = nullptr;   // [0] ticket, [kAbort] timeout flag (kCtlBytes block)
     int nlevels = -1;
     int auto_algo = 0;         // sblas_trsv_solve algo 4: the pull executor's ticket order (1 or 3)
-    int pull_threads = 0;      // SBLAS_TRSV_THREADS at create (0: by ticket order, pull_threads())
+    int pull_threads = 0;      // fixed at create (0: by ticket order, pull_threads())
     // level-set executor (algo 2), built on its first solve: rows in level
     // order (stable by row), the CSR rows copied into that order, level
     // pointers, and the launch schedule (runs of narrow levels -> one
@@ -610,13 +610,15 @@ __global__ __launch_bounds__(256) void k_trsm_pull(const TrsmArgs P, unsigned *c
 // Natural order is bound by the ticket counter (~85 M claims/s, one claim
 // per 64 / RP rows) up to V = 4: wider lanes, fewer claims.  In level order a
 // wave's rows are independent rows of one level and longer per-lane rows
-// lengthen every level.  SBLAS_TRSM_V overrides.
+// lengthen every level.  An experiment build (Makefile `alt`,
+// -DSBLAS_TRSM_V=v) fixes V.
 static int trsm_cols_per_lane(int c, bool level)
 {
-    if (const char *e = getenv("SBLAS_TRSM_V")) {
-        const int a = atoi(e);
-        return a >= 8 ? 8 : a >= 4 ? 4 : a >= 2 ? 2 : 1;
-    }
+#ifdef SBLAS_TRSM_V
+    (void)c;
+    (void)level;
+    return SBLAS_TRSM_V >= 8 ? 8 : SBLAS_TRSM_V >= 4 ? 4 : SBLAS_TRSM_V >= 2 ? 2 : 1;
+#endif
     if (level) return c <= 8 ? 1 : c <= 32 ? 2 : 4;
     return c <= 8 ? 2 : c <= 32 ? 4 : 8;
 }
@@ -847,15 +849,17 @@ __global__ __launch_bounds__(1024) void k_trsv_level_grid(
 // level.  Config-5 stand-in (natural order, 985 levels): 1 / 2 / 3 / 4 waves
 // per CU 2.44 / 2.12 / 2.24 / 2.45 ms; level order (a ticket holds 64 rows of
 // one level): 27-point 100^3 1.79 / 1.92 / 1.99 / 2.03 ms, 7-point 0.81 /
-// 0.85 / 0.87 / 0.89 ms (profiles/r05/trsv_waves/).  SBLAS_TRSV_THREADS
-// (64 / 128 / 192 / 256) overrides.  The multi-device blocks keep 256: four
+// 0.85 / 0.87 / 0.89 ms (profiles/r05/trsv_waves/).  An experiment build
+// (-DSBLAS_TRSV_THREADS = 64 / 128 / 192 / 256) overrides.  The multi-device blocks keep 256: four
 // blocks sharing one GPU ran 4.7 ms at 4 waves per CU and 6.2 at 2 (each
 // block then has a quarter of the grid), and one block per GPU is unmeasured
 // here.
-static int pull_threads_env()  // read when a handle is created
+#ifndef SBLAS_TRSV_THREADS
+#define SBLAS_TRSV_THREADS 0
+#endif
+static int pull_threads_env()  // fixed when a handle is created
 {
-    const char *e = getenv("SBLAS_TRSV_THREADS");
-    const int t = e ? atoi(e) : 0;
+    constexpr int t = SBLAS_TRSV_THREADS;
     return t == 64 || t == 128 || t == 192 || t == 256 ? t : 0;
 }
 static int pull_threads(bool level_order, int forced)
@@ -867,12 +871,11 @@ static int grid_for(int dev)
 {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 1024;
-    // 256-thread workgroups per CU.  More spinning waves is slower: every
-    // polling lane costs an L2 request the producers need (config 5, pull:
-    // 1/CU 2.44 ms, 2/CU 2.99 ms, 4/CU 4.92 ms; 8/CU starves the chain).
-    int per_cu = 1;
-    if (const char *e = getenv("SBLAS_TRSV_WG_PER_CU")) per_cu = std::max(1, std::min(4, atoi(e)));
-    return p.multiProcessorCount * per_cu;
+    // one workgroup per CU (the pull executors' pull_threads() threads each,
+    // the push executor's 256).  More spinning waves is slower: every polling
+    // lane costs an L2 request the producers need (config 5, pull: 1/CU 2.44
+    // ms, 2/CU 2.99 ms, 4/CU 4.92 ms at 256 threads; 8/CU starves the chain).
+    return p.multiProcessorCount;
 }
 
 }  // namespace sblas
@@ -1025,10 +1028,10 @@ static int solve_levelset(sblas_trsv_s *T, const double *b, double *x, hipStream
     SBLAS_HIP(hipMemsetAsync(T->ctl, 0, kCtlBytes, s));
     int ncu = 0;
     SBLAS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, T->device));
-    static const int per_level = [] {  // experiments: one launch per wide level
-        const char *e = getenv("SBLAS_TRSV_LEVEL_LAUNCH");
-        return e ? atoi(e) : 0;
-    }();
+#ifndef SBLAS_TRSV_LEVEL_LAUNCH  // experiment builds: one launch per wide level
+#define SBLAS_TRSV_LEVEL_LAUNCH 0
+#endif
+    constexpr int per_level = SBLAS_TRSV_LEVEL_LAUNCH;
     for (const auto &seg : T->lsched) {
         if (seg.second < 0 && per_level) {
             for (int l = seg.first; l < -seg.second; ++l) {
@@ -1159,8 +1162,7 @@ int sblas_trsv_solve(sblas_trsv T, int algo, const double *d_b, double *d_x, voi
     // one s_sleep(1) per poll; level order the adaptive back-off up to 64
     // units (-6: 27-point 100^3 2.25 -> 2.03 ms, 7-point 0.97 -> 0.88 ms; -8
     // and deeper lose; profiles/r03/sptrsv_sleep/)
-    int slp = algo == 3 ? -6 : 1;
-    if (const char *e = getenv("SBLAS_TRSV_SLEEP")) slp = std::max(-10, std::min(64, atoi(e)));
+    const int slp = algo == 3 ? -6 : 1;
     const int pth = pull_threads(algo == 3, T->pull_threads);
     if (algo == 3) {  // sync-free pull, tickets in level order
         fill_pending((unsigned long long *)d_x, T->n, s);
@@ -1197,14 +1199,12 @@ static int trsm_pull(sblas_trsv_s *T, bool level, int rhs, const double *d_b, do
     TrsmArgs P{level ? T->lrp : T->rrowptr, level ? T->lcol : T->rcol, level ? T->lval : T->rval, d_b,
                (unsigned long long *)d_x, nullptr, 1, 0, 0, T->n, T->n, rhs, T->substitution, 1,
                level ? T->lrow : nullptr, level ? -6 : 1};
-    if (const char *e = getenv("SBLAS_TRSV_SLEEP")) P.slp = std::max(-10, std::min(64, atoi(e)));
     // workgroups per CU (x grid_for's): natural order at rhs >= 16 gains from
     // more rows in flight (config 5: rhs 16 / 32 / 64 at 1 -> 2 -> 4 per CU:
     // 6.50 / 10.2 / 16.1 -> 4.63 / 8.55 / 10.4 -> 4.86 / 8.53 / 9.26 ms); level
     // order loses (27-point stencil rhs 64: 4.93 / 5.12 / 5.32 ms;
-    // profiles/r03/sptrsm/trsm_grid2/).  SBLAS_TRSM_WG_PER_CU overrides.
-    int mult = level || rhs < 16 ? 1 : rhs <= 32 ? 2 : 4;
-    if (const char *e = getenv("SBLAS_TRSM_WG_PER_CU")) mult = std::max(1, std::min(8, atoi(e)));
+    // profiles/r03/sptrsm/trsm_grid2/).
+    const int mult = level || rhs < 16 ? 1 : rhs <= 32 ? 2 : 4;
     const int grid = grid_for(T->device) * mult;
     launch_trsm(P, T->ctl, grid, s);
     SBLAS_HIP(hipGetLastError());
@@ -1337,7 +1337,8 @@ namespace {
 // GPUs: each gets grid_for(dev) / (blocks on dev) workgroups, so the blocks
 // of one device are co-resident.  Launches go in block order; a block only
 // waits for lower blocks, which were enqueued first on every hardware queue,
-// so streams sharing a queue cannot deadlock.  SBLAS_TRSV_MGPU_SERIAL=1 runs
+// so streams sharing a queue cannot deadlock.  An experiment build with
+// -DSBLAS_TRSV_MGPU_SERIAL=1 runs
 // the blocks of one device in order on one stream instead (A/B timing).
 struct TrsvMgpuDev {
     int phys = 0;
@@ -1354,8 +1355,8 @@ struct TrsvMgpuDev {
 
 struct sblas_trsv_mgpu_s {
     int n = 0, rhs = 1, nblocks = 0, ndev = 0;
-    bool bwd = false, serial = false, trace = false;
-    int pull_threads = 0;  // SBLAS_TRSV_THREADS at create (0: 256 threads per workgroup)
+    bool bwd = false, serial = false;
+    int pull_threads = 0;  // fixed at create (0: 256 threads per workgroup)
     std::vector<int> ob;                  // block boundaries in the solve order
     std::vector<TrsvMgpuDev> D;
     std::vector<hipStream_t> streams;     // per block (serial: per device's first block)
@@ -1406,9 +1407,11 @@ int trsv_mgpu_build(sblas_trsv_mgpu_s *H, const int *colptr, const int *rowidx, 
     H->rhs = rhs;
     H->nblocks = nblocks;
     H->ndev = ndev;
-    H->serial = getenv("SBLAS_TRSV_MGPU_SERIAL") && atoi(getenv("SBLAS_TRSV_MGPU_SERIAL")) != 0;
+#ifndef SBLAS_TRSV_MGPU_SERIAL  // experiment builds: one device's blocks in order on one stream
+#define SBLAS_TRSV_MGPU_SERIAL 0
+#endif
+    H->serial = SBLAS_TRSV_MGPU_SERIAL != 0;
     H->pull_threads = pull_threads_env();
-    H->trace = getenv("SBLAS_TRSV_TRACE") != nullptr;
     const int nnz = colptr[n];
     const bool bwd = H->bwd = substitution == 1;
     // CSC of L == CSR of L^T; stable transpose gives CSR of L with columns
@@ -1567,11 +1570,6 @@ int trsv_mgpu_run(sblas_trsv_mgpu_s *H, const double *b, double *x, double *solv
         if (h[kAbort]) {
             set_error("trsv_mgpu: partition %d exceeded its spin limit", d);
             return SBLAS_ERR_HIP;
-        }
-        if (H->trace && q.nloc > 0) {  // debugging aid: block d's span on its device's clock
-            const unsigned long long *h64 = (const unsigned long long *)h;
-            printf("trsv_block %d dev %d rows %d start_us %.3f end_us %.3f\n", d, q.phys, q.nloc,
-                   (double)(~0ULL - h64[kTStart64]) * 1e-2, (double)h64[kTEnd64] * 1e-2);
         }
         // x rows of this block: contiguous rows in row space
         if (q.nloc == 0) continue;

@@ -805,6 +805,36 @@ struct MsdShape {
     int c = 0, bA = 0, bB = 0;
 };
 
+// Digit shapes and pass forms other than the defaults exist for experiment
+// builds only (Makefile `alt`, ALT_DEFS): -DSBLAS_TRANSPOSE_MSD_C / _MSD_A
+// (final / pass-A digit bits), -DSBLAS_TRANSPOSE_LSD (the LSD passes
+// everywhere), -DSBLAS_TRANSPOSE_RB8 (one-tile-per-workgroup 8-bit LSD),
+// _RBMAX, _WGCU, _DERIVE, _PACKA, _PACK, _DIRECT, _FTILE, _FLEAN as below.
+#ifndef SBLAS_TRANSPOSE_RBMAX
+#define SBLAS_TRANSPOSE_RBMAX 8
+#endif
+#ifndef SBLAS_TRANSPOSE_WGCU
+#define SBLAS_TRANSPOSE_WGCU 2
+#endif
+#ifndef SBLAS_TRANSPOSE_DERIVE
+#define SBLAS_TRANSPOSE_DERIVE 1
+#endif
+#ifndef SBLAS_TRANSPOSE_PACKA
+#define SBLAS_TRANSPOSE_PACKA 1
+#endif
+#ifndef SBLAS_TRANSPOSE_PACK
+#define SBLAS_TRANSPOSE_PACK 1
+#endif
+#ifndef SBLAS_TRANSPOSE_DIRECT
+#define SBLAS_TRANSPOSE_DIRECT 0
+#endif
+#ifndef SBLAS_TRANSPOSE_FTILE
+#define SBLAS_TRANSPOSE_FTILE 0
+#endif
+#ifndef SBLAS_TRANSPOSE_FLEAN
+#define SBLAS_TRANSPOSE_FLEAN 2
+#endif
+
 static MsdShape msd_shape(int nbits, int n, long long nnz)
 {
     MsdShape m;
@@ -813,10 +843,14 @@ static MsdShape msd_shape(int nbits, int n, long long nnz)
     // final workgroups count from the registers of their only tile
     m.c = std::min(8, nbits);
     while (m.c > 1 && nnz / std::max<long long>(1, ((long long)n + (1LL << m.c) - 1) >> m.c) > 3072) --m.c;
-    if (const char *e = getenv("SBLAS_TRANSPOSE_MSD_C")) m.c = std::max(1, std::min(8, atoi(e)));
+#ifdef SBLAS_TRANSPOSE_MSD_C
+    m.c = std::max(1, std::min(8, SBLAS_TRANSPOSE_MSD_C));
+#endif
     const int high = nbits - m.c;
     m.bA = (high + 1) / 2;
-    if (const char *e = getenv("SBLAS_TRANSPOSE_MSD_A")) m.bA = std::max(1, std::min(high - 1, atoi(e)));
+#ifdef SBLAS_TRANSPOSE_MSD_A
+    m.bA = std::max(1, std::min(high - 1, SBLAS_TRANSPOSE_MSD_A));
+#endif
     m.bB = high - m.bA;
     return m;
 }
@@ -832,21 +866,26 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     }
     int nbits = 0;
     while (nbits < 31 && (n - 1) >> nbits) ++nbits;
-    // algorithm: MSD (default where both high passes exist, i.e. n > 2^9),
-    // SBLAS_TRANSPOSE_ALGO=lsd the LSD passes below, SBLAS_TRANSPOSE_RB=8
-    // the one-tile-per-workgroup 8-bit LSD path
-    const char *alg_e = getenv("SBLAS_TRANSPOSE_ALGO");
-    const char *rb_e = getenv("SBLAS_TRANSPOSE_RB");
-    const int rb_env = rb_e ? atoi(rb_e) : 0;
+    // algorithm: MSD where both high passes exist (n > 2^9), else the LSD
+    // passes below (experiment builds: -DSBLAS_TRANSPOSE_LSD everywhere,
+    // -DSBLAS_TRANSPOSE_RB8 the one-tile-per-workgroup 8-bit LSD path)
+#ifdef SBLAS_TRANSPOSE_RB8
+    constexpr int rb_env = 8;
+#else
+    constexpr int rb_env = 0;
+#endif
+#ifdef SBLAS_TRANSPOSE_LSD
+    constexpr bool force_lsd = true;
+#else
+    constexpr bool force_lsd = false;
+#endif
     const MsdShape ms = msd_shape(nbits, n, nnz);
-    const bool msd = rb_env != 8 && !(alg_e && !strcmp(alg_e, "lsd")) && ms.bA >= 1 && ms.bB >= 1 &&
-                     ms.bA <= 8 && ms.bB <= 8;
-    // LSD: digits of at most SBLAS_TRANSPOSE_RBMAX bits (default 8: a
-    // workgroup's partially written digit runs -- 2^rb per array -- must fit
-    // its share of the XCD's L2 until they merge; 11-bit digits measured
-    // 0.85 ms per pass against ~0.3 ms), spread evenly over the passes
-    const char *rbm_e = getenv("SBLAS_TRANSPOSE_RBMAX");
-    const int rbmax = std::max(1, std::min(11, rbm_e ? atoi(rbm_e) : 8));
+    const bool msd = rb_env != 8 && !force_lsd && ms.bA >= 1 && ms.bB >= 1 && ms.bA <= 8 && ms.bB <= 8;
+    // LSD: digits of at most SBLAS_TRANSPOSE_RBMAX bits (8: a workgroup's
+    // partially written digit runs -- 2^rb per array -- must fit its share
+    // of the XCD's L2 until they merge; 11-bit digits measured 0.85 ms per
+    // pass against ~0.3 ms), spread evenly over the passes
+    const int rbmax = std::max(1, std::min(11, SBLAS_TRANSPOSE_RBMAX));
     const bool wide = rb_env != 8;
     const int passes = wide ? std::max(1, (nbits + rbmax - 1) / rbmax) : std::max(1, (nbits + 7) / 8);
     const int rb = wide ? std::max(1, (nbits + passes - 1) / passes) : 8;
@@ -858,9 +897,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     }
     // tiles per workgroup: one round of resident workgroups (2 per CU for
-    // <= 8-bit digits, 1 per CU above); SBLAS_TRANSPOSE_WGCU overrides
-    const char *wgcu_e = getenv("SBLAS_TRANSPOSE_WGCU");
-    const int wgcu = wgcu_e ? std::max(1, atoi(wgcu_e)) : 2;
+    // <= 8-bit digits, 1 per CU above)
+    const int wgcu = std::max(1, SBLAS_TRANSPOSE_WGCU);
     const int S_t = wide ? std::max(1, (ntiles + ncu * wgcu - 1) / (ncu * wgcu)) : 1;
     const int nwg = (ntiles + S_t - 1) / S_t;
     // MSD pass B: J parts per pass-A bucket, about two workgroups per CU
@@ -895,10 +933,10 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
     int *wgrow = scan + scan_ints;
     int *rout_final = rowidx ? rowidx : wgrow + wg_ints;
     double *vout_final = cval ? cval : (double *)(((uintptr_t)(rout_final + (rowidx ? 0 : z)) + 7) & ~(uintptr_t)7);
-    // MSD pass A derives the rows from rowptr (SBLAS_TRANSPOSE_DERIVE=0: from
-    // an expanded row array, as the LSD passes do)
-    const char *dv_e = getenv("SBLAS_TRANSPOSE_DERIVE");
-    const bool derive = msd && !(dv_e && atoi(dv_e) == 0);
+    // MSD pass A derives the rows from rowptr (experiment builds
+    // -DSBLAS_TRANSPOSE_DERIVE=0: from an expanded row array, as the LSD
+    // passes do)
+    const bool derive = msd && SBLAS_TRANSPOSE_DERIVE != 0;
     if (!derive)
         hipLaunchKernelGGL(k_expand_rows, dim3((m + 255) / 256), dim3(256), 0, s, A.rowptr, m, rowsB);
     if (msd) {
@@ -911,9 +949,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         SBLAS_TRY(scan_inclusive(cntA, ncntA, scan, s));
         // pass A -> pass B in one word per key (low bB + c bits + row offset in
         // the segment) when the segments' row spans allow; decided on the
-        // device from the spans the count pass wrote.  SBLAS_TRANSPOSE_PACKA=0 off.
-        const char *pa_e = getenv("SBLAS_TRANSPOSE_PACKA");
-        const int packA = (derive && nwg <= 512 && ms.bB + ms.c <= 24 && !(pa_e && atoi(pa_e) == 0))
+        // device from the spans the count pass wrote.
+        const int packA = (derive && nwg <= 512 && ms.bB + ms.c <= 24 && SBLAS_TRANSPOSE_PACKA != 0)
                               ? ms.bB + ms.c : -1;
         if (derive)
             hipLaunchKernelGGL((k_rx2_scatter<256, kSegTiles, kR2Threads, true>), dim3(nwg), dim3(kR2Threads), 0, s,
@@ -925,11 +962,10 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         // pass B: the next bB bits inside each pass-A bucket, set A -> set B.
         // Its output keeps (row << c | low c column bits) in one word when
         // they fit (the last pass needs nothing else of the key): 12 B per
-        // entry written and read instead of 16.  SBLAS_TRANSPOSE_PACK=0 off.
+        // entry written and read instead of 16.
         int mbits = 0;
         while (mbits < 31 && (m - 1) >> mbits) ++mbits;
-        const char *pk_e = getenv("SBLAS_TRANSPOSE_PACK");
-        const int pack = (mbits + ms.c <= 31 && !(pk_e && atoi(pk_e) == 0)) ? ms.c : -1;
+        const int pack = (mbits + ms.c <= 31 && SBLAS_TRANSPOSE_PACK != 0) ? ms.c : -1;
         const int nwgB = (1 << ms.bA) * JB;
         const SegArgs gB{0, 0, cntA, nwg, JB};
         hipLaunchKernelGGL(k_rx2_count<kSegBuckets>, dim3((unsigned)nwgB), dim3(kCntThreads), 0,
@@ -945,17 +981,16 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
                                0, wgrow, packA);
         // last pass: one workgroup per pass-B bucket (2^c columns), set B -> CSC + colptr
         const int nbC = 1 << (ms.bA + ms.bB);
-        // SBLAS_TRANSPOSE_DIRECT=1: entries written from registers (experiment)
-        const char *de = getenv("SBLAS_TRANSPOSE_DIRECT");
+        // SBLAS_TRANSPOSE_DIRECT=1 (experiment builds): entries written from registers
+        constexpr bool direct = SBLAS_TRANSPOSE_DIRECT == 1;
         const SegArgs gC{0, 0, cntB, JB, 1, nbC};
         // final tile: 3072 entries (6 per thread) when the buckets average <=
         // 2600 -- uniform columns then fit one tile (spread ~ sqrt(avg)) with
         // 83% of its lanes busy instead of 62% in a 4096 tile; fuller buckets
-        // keep the 4096 tile (SBLAS_TRANSPOSE_FTILE=4096 forces it)
+        // keep the 4096 tile (experiment builds: SBLAS_TRANSPOSE_FTILE=4096 forces it)
         const long long favg = nnz / std::max(1, nbC);
-        const char *ft_e = getenv("SBLAS_TRANSPOSE_FTILE");
-        const bool small_tile = ft_e ? atoi(ft_e) == 3072 : favg <= 2600;
-        auto kfin = (de && atoi(de) == 1)
+        const bool small_tile = SBLAS_TRANSPOSE_FTILE ? SBLAS_TRANSPOSE_FTILE == 3072 : favg <= 2600;
+        auto kfin = direct
                         ? (small_tile ? k_rx2_scatter<256, kSegFinalDirect, kR2Threads, false, 3072>
                                       : k_rx2_scatter<256, kSegFinalDirect, kR2Threads>)
                         : (small_tile ? k_rx2_scatter<256, kSegFinal, kR2Threads, false, 3072>
@@ -963,9 +998,8 @@ int launch_transpose(const sblas_csr_s &A, int *colptr, int *rowidx, double *cva
         // lean last pass (packed input, <= 7 final bits, 3072 tile; default):
         // no row staging and 128-digit tables leave 42 KB of LDS, and 80
         // VGPRs, so three workgroups share a CU (config 2: 332 -> 290 us).
-        // SBLAS_TRANSPOSE_FLEAN=1: lean at two per CU, =0: the staged form.
-        const char *fl_e = getenv("SBLAS_TRANSPOSE_FLEAN");
-        const int flean = (pack >= 0 && ms.c <= 7 && small_tile && !(de && atoi(de) == 1)) ? (fl_e ? atoi(fl_e) : 2) : 0;
+        // Experiment builds: SBLAS_TRANSPOSE_FLEAN=1 lean at two per CU, =0 the staged form.
+        const int flean = (pack >= 0 && ms.c <= 7 && small_tile && !direct) ? SBLAS_TRANSPOSE_FLEAN : 0;
         int fgrid = std::min(nbC, ncu * wgcu);
         if (flean == 1) kfin = k_rx2_scatter<128, kSegFinal, kR2Threads, false, 3072, true, 1>;
         if (flean == 2) {

@@ -116,6 +116,9 @@ _sig("sblas_trsv_mgpu_info", _i, _p, _p, _p, _p)
 _sig("sblas_ctx_comm_info", _i, _p, _p, _p)
 _sig("sblas_test_deny_peer_access", _i, _i)
 _sig("sblas_peer_refs", _i, _i, _i)
+_sig("sblas_test_set_option", _i, C.c_char_p, _d, _i)
+_sig("sblas_csr_set_deterministic", _i, _p, _i)
+_sig("sblas_csr_get_deterministic", _i, _p, _p)
 _sig("sblas_ctx_create", _i, _p, _i, _p)
 _sig("sblas_ctx_destroy", _i, _p)
 _sig("sblas_ctx_ngpu", _i, _p, _p)
@@ -532,6 +535,17 @@ class DeviceCSR:
         check(lib.sblas_csr_pick(self.h, stream, C.byref(a)), "csr_pick")
         return a.value
 
+    @property
+    def deterministic(self) -> bool:
+        """Bitwise-repeatable launches (sblas_csr_set_deterministic)."""
+        v = C.c_int()
+        check(lib.sblas_csr_get_deterministic(self.h, C.byref(v)), "csr_get_deterministic")
+        return bool(v.value)
+
+    @deterministic.setter
+    def deterministic(self, on: bool) -> None:
+        check(lib.sblas_csr_set_deterministic(self.h, int(bool(on))), "csr_set_deterministic")
+
     def panels(self, algo: int) -> int:
         """XCD column panels the analysed plan of `algo` runs over (0 = plain)."""
         p = C.c_int()
@@ -719,3 +733,28 @@ def test_deny_peer_access(on: bool) -> None:
 def peer_refs(a: int, b: int) -> int:
     """References the library holds on the a -> b peer link."""
     return int(lib.sblas_peer_refs(a, b))
+
+
+def set_test_option(name: str, value=None) -> None:
+    """Planner override for tests (sblas_test_set_option); value None clears
+    it.  Read when a plan is built."""
+    check(lib.sblas_test_set_option(name.encode(), float(value or 0.0), int(value is not None)),
+          "test_set_option")
+
+
+class test_options:
+    """`with sblas.test_options(xs_cap=50): ...` -- planner overrides for the
+    plans built inside the block, cleared on exit."""
+
+    def __init__(self, **opts):
+        self.opts = opts
+
+    def __enter__(self):
+        for k, v in self.opts.items():
+            set_test_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.opts:
+            set_test_option(k, None)
+        return False

@@ -58,8 +58,11 @@ def cfg2(request, sb, orc, torch_cuda):
     yield d
 
 
-def _run_cfg2(torch, sb, c, algo, launches=1):
+def _run_cfg2(torch, sb, c, algo, launches=1, det=False):
+    """launches of one plan, each against the oracle; returns the y's."""
     A = sb.DeviceCSR.upload(0, N2, c["rp"], c["col"], c["val"])
+    A.deterministic = det
+    ys = []
     try:
         A.analyse(algo)
         yd = torch.empty_like(c["y0d"])
@@ -67,28 +70,40 @@ def _run_cfg2(torch, sb, c, algo, launches=1):
             yd.copy_(c["y0d"])
             A.spmv(algo, c["alpha"], c["xd"].data_ptr(), c["beta"], yd.data_ptr())
             torch.cuda.synchronize()
-            _check_spmv(c["want"], c["bound"], yd.cpu().numpy(), f"algo {algo} launch {it}")
+            ys.append(yd.cpu().numpy())
+            _check_spmv(c["want"], c["bound"], ys[-1], f"algo {algo} launch {it}")
     finally:
         A.close()
+    return ys
 
 
-@pytest.mark.parametrize("algo,env", [
-    (1, {}), (2, {}), (3, {}), (2, {"SBLAS_CSR5_PANEL": "1"}), (2, {"SBLAS_CSR5_PANEL": "0"}),
-    (2, {"SBLAS_C5_PF": "0"}), (2, {"SBLAS_C5_PF": "1"}), (2, {"SBLAS_C5_PF": "3", "SBLAS_CSR5_PANEL": "0"}),
-    (1, {"SBLAS_RS_PANEL": "0"}), (1, {"SBLAS_RS_PANEL": "1"}), (4, {}), (5, {}), (5, {"SBLAS_XS_DYN": "0"}),
-    (5, {"SBLAS_XS_Q": "3"}), (5, {"SBLAS_XS_FUSE": "1"}), (5, {"SBLAS_XS_U": "2"}),
-    (5, {"SBLAS_XS_ALLWIDE": "1"}), (5, {"SBLAS_XS_SOLO": "1"}), (5, {"SBLAS_XS_WG": "1024"}),
-    (1, {"SBLAS_RS_SEQ": "0"}), (5, {"SBLAS_XS_WG": "768"}), (5, {"SBLAS_XS_U": "1"})],
-    ids=["rowsplit", "csr5", "csr5_alt", "csr5_panels", "csr5_plain", "csr5_form0", "csr5_form1",
-         "csr5_form3_plain", "rowsplit_plain", "rowsplit_panels", "panel", "xsort", "xsort_static", "xsort_q3",
-         "xsort_fused", "xsort_u2", "xsort_allwide", "xsort_solo", "xsort_wg1024", "rowsplit_vec4", "xsort_wg768", "xsort_u1"])
-def test_config2_full_size(torch_cuda, sb, cfg2, monkeypatch, algo, env):
-    """BASELINE configs[1] at full size, every algorithm against the oracle."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    launches = 25 if (algo == 5 and (not env or env == {"SBLAS_XS_SOLO": "1"})
-                      and not cfg2["prefix"]) else 1
-    _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
+@pytest.mark.parametrize("algo,opts", [
+    (1, {}), (2, {}), (3, {}), (2, {"csr5_panel": 0}), (1, {"rs_panel": 0}), (4, {}), (5, {}),
+    (5, {"xs_allwide": 1}), (5, {"xs_solo": 1})],
+    ids=["rowsplit", "csr5", "csr5_alt", "csr5_plain", "rowsplit_plain", "panel", "xsort", "xsort_allwide",
+         "xsort_solo"])
+def test_config2_full_size(torch_cuda, sb, cfg2, algo, opts):
+    """BASELINE configs[1] at full size, every algorithm against the oracle
+    (planner test options force the non-default layouts)."""
+    launches = 25 if (algo == 5 and opts in ({}, {"xs_solo": 1}) and not cfg2["prefix"]) else 1
+    with sb.test_options(**opts):
+        _run_cfg2(torch_cuda, sb, cfg2, algo, launches)
+
+
+def test_config2_auto_deterministic(torch_cuda, sb, cfg2):
+    """on a deterministic handle (SBLAS_DETERMINISTIC /
+    sblas_csr_set_deterministic) AUTO's launches on config 2 are bitwise
+    equal and within the per-row bound; AUTO still picks xsort (its ordered
+    form).  Without the flag xsort's LDS-atomic order varies."""
+    A = sb.DeviceCSR.upload(0, N2, cfg2["rp"], cfg2["col"], cfg2["val"])
+    try:
+        want = sb.ROWSPLIT if cfg2["prefix"] else sb.XSORT
+        assert A.pick() == want
+    finally:
+        A.close()
+    ys = _run_cfg2(torch_cuda, sb, cfg2, sb.AUTO, launches=4, det=True)
+    for it, y in enumerate(ys[1:], 1):
+        assert np.array_equal(ys[0], y), f"launch {it}: {np.sum(ys[0] != y)} rows differ"
 
 
 def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
@@ -166,16 +181,15 @@ def test_config2_nnz_split_light_rank_csr5(torch_cuda, sb, orc, cfg2, world):
 
 
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 0), (8, 0), (8, 7)])
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_SOLO": "1"}, {"SBLAS_XS_WG": "768"}, {"SBLAS_XS_WG": "1024"}],
-                         ids=["default", "solo", "wg768", "wg1024"])
-def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world, rank, env):
+@pytest.mark.parametrize("opts", [{}, {"xs_solo": 1}, {"det": 1}], ids=["default", "solo", "det"])
+def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, world, rank, opts):
     """A rank's cyclic slice of config 2 (bench.py's N > 1 share) with the
     persistent column-sorted kernel (and its solo-item layout), three launches
     on one plan against the oracle, and the beta = 0 form on a NaN-filled y."""
     import sblas_dist
     torch = torch_cuda
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    opts = dict(opts)
+    det = bool(opts.pop("det", 0))
     rp, col, val = cfg2["rp"], cfg2["col"], cfg2["val"]
     plan = sblas_dist.make_cyclic_plan(rp, N2, world)
     lrp, lcol, lval = sblas_dist.cyclic_local_csr(rp, plan, rank, lambda a, b: (col[rp[a]:rp[b]], val[rp[a]:rp[b]]))
@@ -184,8 +198,10 @@ def test_config2_rank_slice_xsort(torch_cuda, sb, orc, cfg2, monkeypatch, world,
     y0 = sb.gen_vector(m, 45)
     alpha, beta = cfg2["alpha"], cfg2["beta"]
     A = sb.DeviceCSR.upload(0, N2, lrp, lcol, lval)
+    A.deterministic = det
     try:
-        A.analyse(5)
+        with sb.test_options(**opts):
+            A.analyse(5)
         for b in (beta, 0.0):
             want = orc.csr_spmv_omp(lrp, lcol, lval, x, alpha, b, y0.copy())
             bound = orc.spmv_bound(lrp, lcol, lval, x, alpha, b, y0)
@@ -231,17 +247,13 @@ def test_config2_alpha_beta_zero(torch_cuda, sb, orc, cfg2):
     A.close()
 
 
-@pytest.mark.parametrize("pack,packa", [("1", "1"), ("1", "0"), ("0", "1")],
-                         ids=["packed", "packed_b_only", "packed_a_only"])
-def test_config2_transpose_full_size(torch_cuda, sb, orc, cfg2, monkeypatch, pack, packa):
+def test_config2_transpose_full_size(torch_cuda, sb, orc, cfg2):
     """CSR -> CSC of the config-2 matrix (the size tools/bench_transpose.py
     times): colptr, row indices and values bit-exact against orc_transpose
-    (tranpose.h:6-43's stable scatter).  Packed and unpacked pass-A and last-pass inputs."""
+    (tranpose.h:6-43's stable scatter)."""
     torch = torch_cuda
     if cfg2["prefix"]:
         pytest.skip("random columns only")
-    monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", pack)
-    monkeypatch.setenv("SBLAS_TRANSPOSE_PACKA", packa)
     rp, col, val = cfg2["rp"], cfg2["col"], cfg2["val"]
     nnz = int(rp[-1])
     cp, ri, cv = orc.transpose(N2, N2, rp, col, val)
@@ -275,17 +287,13 @@ def cfg4(orc):
                 want=want, bound=bound)
 
 
-@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "ctslot"), ("row", "rowwave")])
-def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form):
+@pytest.mark.parametrize("layout,form", [("row", "ctile"), ("col", "ctile"), ("row", "rowwave")])
+def test_config4_spmm_full_size(torch_cuda, sb, cfg4, layout, form):
     """BASELINE configs[3]: C = -0.7 A B + 0.8 C on the rail4284-shaped matrix,
     all 4284 x 64 entries of C checked (B row-major as resident in HBM, and
     the reference's column-major host layout), with the default column-sorted
-    C-tile form, its column-run slot variant and the row kernels."""
+    C-tile form and the row kernels (test option spmm_ctile=0)."""
     torch = torch_cuda
-    if form == "ctslot":
-        monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
-    if form == "rowwave":
-        monkeypatch.setenv("SBLAS_SPMM_CTILE", "0")
     c = cfg4
     m, k, n = c["m"], c["k"], c["n"]
     A = sb.DeviceCSR.upload(0, k, c["rp"], c["col"], c["val"])
@@ -294,7 +302,8 @@ def test_config4_spmm_full_size(torch_cuda, sb, cfg4, monkeypatch, layout, form)
     else:
         Bd, ldb, lay = torch.from_numpy(np.asfortranarray(c["B"]).ravel(order="F")).cuda(), k, 0
     Cd = torch.from_numpy(np.asfortranarray(c["C0"]).ravel(order="F")).cuda()
-    A.spmm(n, c["alpha"], Bd.data_ptr(), ldb, lay, c["beta"], Cd.data_ptr(), m)
+    with sb.test_options(**({"spmm_ctile": 0} if form == "rowwave" else {})):  # the plan builds on this call
+        A.spmm(n, c["alpha"], Bd.data_ptr(), ldb, lay, c["beta"], Cd.data_ptr(), m)
     torch.cuda.synchronize()
     got = Cd.cpu().numpy().reshape((n, m)).T
     A.close()

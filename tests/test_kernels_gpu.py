@@ -33,31 +33,19 @@ def spmm_bound(rp, col, val, B, alpha, beta, C0):
     return 4 * gam * S + 4 * u * np.abs(beta * C0) + 1e-300
 
 
-@pytest.mark.parametrize("splitk", ["auto", "0", "1", "ct", "ctw", "ctrows", "ctslab", "ctslot"])
+@pytest.mark.parametrize("form", ["rowwave", "splitk", "ct", "ctrows"])
 @pytest.mark.parametrize("ncols", [1, 16, 64, 100])
 @pytest.mark.parametrize("layout", [0, 1])
-def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
-    """Both row kernels: wave per row and workgroup per row (split over its
-    nonzeros; picked automatically for long rows) and the column-sorted
-    C-tile form (forced: "ct" = 3 slabs of 2048 columns, one slab set; "ctw"
-    = 313 slabs of 16 columns in 3 sets per XCD; "ctrows" = 2,500 rows, i.e.
-    3 row blocks of 834; "ctslab" XCD-local slab keys; "ctslot" column-run
-    slots of two entries)."""
+def test_spmm(torch_cuda, sb, orc, ncols, layout, form):
+    """Both row kernels: wave per row ("rowwave") and workgroup per row split
+    over its nonzeros (picked for rows of >= 256 entries on average:
+    "splitk", 60 rows of ~1,000), and the column-sorted C-tile form (test
+    option spmm_ctile=1: "ct" = 3 slabs of 2048 columns, one slab set;
+    "ctrows" = 2,500 rows, i.e. 3 row blocks of 834)."""
     torch = torch_cuda
-    if splitk in ("0", "1"):
-        monkeypatch.setenv("SBLAS_SPMM_SPLITK", splitk)
-    if splitk.startswith("ct"):
-        monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
-        if splitk == "ctslab":  # XCD-local slab keys instead of global columns
-            monkeypatch.setenv("SBLAS_SPMM_CTDIRECT", "0")
-        if splitk == "ctslot":  # column-run slots of two entries (opt-in form)
-            monkeypatch.setenv("SBLAS_SPMM_CTSLOT", "1")
-        if splitk == "ctw":
-            monkeypatch.setenv("SBLAS_SPMM_CTW", "4")
-            monkeypatch.setenv("SBLAS_SPMM_CTNS", "3")
     rng = np.random.default_rng(ncols + 10 * layout)
-    m, k = (2500 if splitk == "ctrows" else 700), 5000
-    rp, col, val = rand_csr(rng, m, k, 50, long_rows=[(3, 3000)])
+    m, k = {"ctrows": 2500, "splitk": 60}.get(form, 700), 5000
+    rp, col, val = rand_csr(rng, m, k, 2000 if form == "splitk" else 50, long_rows=[(3, 3000)])
     B = rng.standard_normal((k, ncols))
     C0 = rng.standard_normal((m, ncols))
     alpha, beta = -0.7, 0.8  # dspmm_baseline_test.cu:518-519
@@ -70,7 +58,8 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
         Bd = torch.from_numpy(np.ascontiguousarray(B).ravel()).cuda()
         ldb = ncols
     Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
-    A.spmm(ncols, alpha, Bd.data_ptr(), ldb, layout, beta, Cd.data_ptr(), m)
+    with sb.test_options(**({"spmm_ctile": 1} if form.startswith("ct") else {})):  # the plan builds here
+        A.spmm(ncols, alpha, Bd.data_ptr(), ldb, layout, beta, Cd.data_ptr(), m)
     torch.cuda.synchronize()
     got = Cd.cpu().numpy().reshape((ncols, m)).T
     assert np.all(np.abs(got - want) <= spmm_bound(rp, col, val, B, alpha, beta, C0))
@@ -79,12 +68,11 @@ def test_spmm(torch_cuda, sb, orc, monkeypatch, ncols, layout, splitk):
 
 @pytest.mark.parametrize("form", ["ctile"])
 @pytest.mark.parametrize("layout", [0, 1])
-def test_spmm_two_handles_two_streams(torch_cuda, sb, orc, monkeypatch, layout, form):
+def test_spmm_two_handles_two_streams(torch_cuda, sb, orc, layout, form):
     """Two handles of different matrices on two streams of one device, launched
     back to back without synchronising: each keeps its own scratch (B copy,
     C-tile partials: sblas_csr_s::spmm_*), so both C match the oracle."""
     torch = torch_cuda
-    monkeypatch.setenv("SBLAS_SPMM_CTILE", "1")
     ncols, k = 64, 6000
     outs = []
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -103,10 +91,11 @@ def test_spmm_two_handles_two_streams(torch_cuda, sb, orc, monkeypatch, layout, 
         Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
         outs.append((A, Bd, ldb, Cd, rp, col, val, B, C0, m))
     torch.cuda.synchronize()
-    for rep in range(3):  # C <- alpha*A*B + beta*C, three times on each stream
-        for (A, Bd, ldb, Cd, *_), st in zip(outs, streams):
-            A.spmm(ncols, 0.5, Bd.data_ptr(), ldb, layout, 0.0 if rep else 1.0, Cd.data_ptr(),
-                   Cd.numel() // ncols, st.cuda_stream)
+    with sb.test_options(spmm_ctile=1):  # the plans build on the first calls
+        for rep in range(3):  # C <- alpha*A*B + beta*C, three times on each stream
+            for (A, Bd, ldb, Cd, *_), st in zip(outs, streams):
+                A.spmm(ncols, 0.5, Bd.data_ptr(), ldb, layout, 0.0 if rep else 1.0, Cd.data_ptr(),
+                       Cd.numel() // ncols, st.cuda_stream)
     torch.cuda.synchronize()
     for A, Bd, ldb, Cd, rp, col, val, B, C0, m in outs:
         want = orc.spmm(m, ncols, k, 0.5, rp, col, val, B, 0.0, C0)
@@ -143,41 +132,18 @@ def test_csrmm_reference_api(torch_cuda, sb, orc, ngpu, split):
 
 
 # ----------------------------------------------------------- transpose ----
-@pytest.mark.parametrize("digits", ["default", "direct", "nopack", "nopacka", "noderive", "ftile4096", "ftile3072",
-                                    "flean1", "flean2",
-                                    "msd_c3", "msd_c5", "msd_c3_direct", "msd_c5_nopack", "lsd", "rb11", "rb8"])
 @pytest.mark.parametrize("case", ["qh768", "ash85", "random", "longcols", "wide", "big", "shortrows", "sparserows"])
-def test_transpose_bit_exact(torch_cuda, sb, orc, monkeypatch, case, digits):
-    """Stable transpose, every path: the MSD partition passes + per-bucket
-    final pass (default where n > 512; pass A derives each entry's row from rowptr,
-    SBLAS_TRANSPOSE_DERIVE=0 reads an expanded row array, and hands pass B one word of key bits
-    and row offset when the segments' row spans allow (SBLAS_TRANSPOSE_PACKA=0 two words; "sparserows"
-    spans too many rows, the device falls back); pass B hands the last pass one word of
-    row and low column bits, SBLAS_TRANSPOSE_PACK=0 two; SBLAS_TRANSPOSE_MSD_C moves the final
-    bucket width so small matrices take it too, with few, long buckets on
-    "longcols"), the LSD tiles-per-workgroup path with <= 8-bit digits ("big"
-    = 3 passes at n = 3M) and with 11-bit digits, and the one-tile 8-bit path."""
+def test_transpose_bit_exact(torch_cuda, sb, orc, case):
+    """Stable transpose, every path the default build takes: the MSD
+    partition passes + per-bucket final pass where n > 512 (pass A derives
+    each entry's row from rowptr and hands pass B one word of key bits and
+    row offset when the segments' row spans allow -- "sparserows" spans too
+    many rows, the device falls back; pass B hands the last pass one word of
+    row and low column bits; "longcols" gives few, long buckets; "big" 3M
+    columns), and the LSD passes on narrow matrices (qh768, ash85, "wide" is
+    n = 1e5 over 50 rows, "longcols" n = 40).  Colptr, row indices and values
+    bit-exact against orc_transpose (tranpose.h:6-43's stable scatter)."""
     torch = torch_cuda
-    if digits == "rb8":
-        monkeypatch.setenv("SBLAS_TRANSPOSE_RB", "8")
-    if digits in ("lsd", "rb11"):
-        monkeypatch.setenv("SBLAS_TRANSPOSE_ALGO", "lsd")
-    if digits == "rb11":
-        monkeypatch.setenv("SBLAS_TRANSPOSE_RBMAX", "11")
-    if digits.startswith("msd_c"):
-        monkeypatch.setenv("SBLAS_TRANSPOSE_MSD_C", digits[5])
-    if digits.endswith("direct"):  # last pass writes from registers
-        monkeypatch.setenv("SBLAS_TRANSPOSE_DIRECT", "1")
-    if digits.endswith("nopack"):  # pass B keeps separate key and row arrays
-        monkeypatch.setenv("SBLAS_TRANSPOSE_PACK", "0")
-    if digits == "noderive":  # pass A reads an expanded row array instead of deriving rows
-        monkeypatch.setenv("SBLAS_TRANSPOSE_DERIVE", "0")
-    if digits.startswith("flean"):  # last pass unpacks rows from the staged keys (1), 3 WGs per CU (2)
-        monkeypatch.setenv("SBLAS_TRANSPOSE_FLEAN", digits[5:])
-    if digits == "nopacka":  # pass A writes key and row arrays instead of one packed word
-        monkeypatch.setenv("SBLAS_TRANSPOSE_PACKA", "0")
-    if digits.startswith("ftile"):  # last-pass tile forced to 4096 / 3072 entries (3072: buckets
-        monkeypatch.setenv("SBLAS_TRANSPOSE_FTILE", digits[5:])  # past it take the multi-tile path)
     rng = np.random.default_rng(5)
     if case in ("qh768", "ash85"):
         m, n, rp, col, val = sb.mm_read(os.path.join(GOLDEN, f"{case}.mtx"), 0)
@@ -399,64 +365,6 @@ def test_sptrsv_auto_order(torch_cuda, sb, orc, kind):
         T.close()
 
 
-@pytest.mark.parametrize("sleep", ["0", "16", "-5"])
-@pytest.mark.parametrize("algo", [1, 3])
-def test_sptrsv_pull_backoff(torch_cuda, sb, monkeypatch, algo, sleep):
-    """The pull executors' poll back-off (SBLAS_TRSV_SLEEP: none, fixed,
-    adaptive) changes only when waves poll, never the result: exact KAT."""
-    monkeypatch.setenv("SBLAS_TRSV_SLEEP", sleep)
-    torch = torch_cuda
-    for name, sub in (("qh768", 0), ("ash85", 1)):
-        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{'fwd' if sub == 0 else 'bwd'}.npz"))
-        cp, ri, cv, b = g["colptr"], g["rowidx"], g["val"], g["b"]
-        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
-        xd = torch.zeros(len(cp) - 1, dtype=torch.float64, device="cuda")
-        T = sb.DeviceTRSV(0, len(cp) - 1, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sub)
-        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
-        torch.cuda.synchronize()
-        assert np.array_equal(xd.cpu().numpy(), g["x_ref"])  # exact KAT
-        T.close()
-
-
-@pytest.mark.parametrize("threads", ["64", "128", "192", "256"])
-@pytest.mark.parametrize("algo", [1, 3])
-def test_sptrsv_pull_threads(torch_cuda, sb, monkeypatch, algo, threads):
-    """Waves per CU of the pull executors (SBLAS_TRSV_THREADS, read when the
-    handle is created; defaults 128 natural / 64 level order) change only how
-    many rows are in flight, never the result: exact KAT, and a banded
-    triangle with long dependency chains identical to the default's x."""
-    torch = torch_cuda
-    for name, sub in (("qh768", 0), ("ash85", 1)):
-        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{'fwd' if sub == 0 else 'bwd'}.npz"))
-        cp, ri, cv, b = g["colptr"], g["rowidx"], g["val"], g["b"]
-        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv, b)]
-        xd = torch.zeros(len(cp) - 1, dtype=torch.float64, device="cuda")
-        monkeypatch.setenv("SBLAS_TRSV_THREADS", threads)
-        T = sb.DeviceTRSV(0, len(cp) - 1, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), sub)
-        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
-        torch.cuda.synchronize()
-        assert np.array_equal(xd.cpu().numpy(), g["x_ref"])  # exact KAT
-        T.close()
-    n = 200_000
-    cp, ri, v = sb.gen_lower_banded(n, 5, 4000, 3)
-    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(cp))
-    b = np.bincount(ri, weights=v * (1.0 + cols % 7), minlength=n)
-    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, v, b)]
-    xs = []
-    for th in (None, threads):
-        if th is None:
-            monkeypatch.delenv("SBLAS_TRSV_THREADS", raising=False)
-        else:
-            monkeypatch.setenv("SBLAS_TRSV_THREADS", th)
-        T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), 0)
-        xd = torch.zeros(n, dtype=torch.float64, device="cuda")
-        T.solve(algo, d[3].data_ptr(), xd.data_ptr())
-        torch.cuda.synchronize()
-        xs.append(xd.cpu().numpy())
-        T.close()
-    assert np.array_equal(xs[0], xs[1])  # same sums, same order: bit-identical
-
-
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_sptrsv_random_wellconditioned(torch_cuda, sb, orc, algo):
     """Random lower-triangular with long chains and a long column/row."""
@@ -595,15 +503,6 @@ def _banded_system(sb, n, seed=11):
     return cp, ri, v, b, xref
 
 
-def _block_spans(out):
-    spans = {}
-    for line in out.splitlines():
-        w = line.split()
-        if w and w[0] == "trsv_block":
-            spans[int(w[1])] = (int(w[3]), float(w[7]), float(w[9]))
-    return [spans[d] for d in sorted(spans)]
-
-
 @pytest.mark.parametrize("blocks,rhs,sub", [(1, 1, 0), (4, 1, 0), (3, 1, 1), (4, 3, 0), (2, 5, 1)])
 def test_sptrsv_mgpu_persistent_handle(torch_cuda, sb, orc, blocks, rhs, sub):
     """sblas_trsv_mgpu_create / run / destroy: blocks built once, then several
@@ -625,34 +524,6 @@ def test_sptrsv_mgpu_persistent_handle(torch_cuda, sb, orc, blocks, rhs, sub):
             ser = orc.sptrsv_serial(cp, ri, v, b, sub)
             assert np.abs(x - ser).sum() / np.abs(ser).sum() <= 1e-12
     H.close()
-
-
-@pytest.mark.parametrize("blocks", [2, 4])
-def test_sptrsv_blocks_run_concurrently(torch_cuda, sb, monkeypatch, capfd, blocks):
-    """Blocks of the multi-device executor that wrap onto ONE GPU run at the
-    same time (own streams, co-resident grids): every block starts before its
-    predecessor -- the block it waits on -- has finished, so producer and
-    consumer are live together and the spin-on-peer-store protocol runs as it
-    does across GPUs.  SBLAS_TRSV_MGPU_SERIAL=1 (in order on one stream) is
-    the control: there no block starts before its predecessor ends.  Both
-    solves are bit-identical to the single-block solve."""
-    n = 300_000
-    cp, ri, v, b, xref = _banded_system(sb, n)
-    want, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, 1, 0)
-    monkeypatch.setenv("SBLAS_TRSV_TRACE", "1")
-    capfd.readouterr()
-    x, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, blocks, 0)
-    spans = _block_spans(capfd.readouterr().out)
-    assert np.array_equal(x, want)
-    assert len(spans) == blocks and len({s[0] for s in spans}) == 1
-    for d in range(1, blocks):
-        assert spans[d][1] < spans[d - 1][2], f"block {d} did not overlap block {d - 1}: {spans}"
-    monkeypatch.setenv("SBLAS_TRSV_MGPU_SERIAL", "1")
-    x, _ = sb.trsv_mgpu_solve(cp, ri, v, n, b, blocks, 0)
-    spans = _block_spans(capfd.readouterr().out)
-    assert np.array_equal(x, want)
-    for d in range(1, blocks):
-        assert spans[d][1] >= spans[d - 1][2], f"serial control overlapped: {spans}"
 
 
 @pytest.mark.parametrize("ngpu,tasks", [(1, 4), (2, 3), (3, 2), (4, 2)])
@@ -735,37 +606,6 @@ def test_sptrsm_kat(torch_cuda, sb, name, sub, rhs):
     T.close()
     for ngpu in (1, 3):
         x, _ = sb.trsv_mgpu_solve(cp, ri, cv, n, B, ngpu, 0 if sub == "fwd" else 1, rhs)
-        assert np.array_equal(x, X)
-
-
-@pytest.mark.parametrize("v", ["1", "2", "4", "8"])
-def test_sptrsm_cols_per_lane(torch_cuda, sb, monkeypatch, v):
-    """SpTRSM pull with V right-hand sides per lane (SBLAS_TRSM_V; the
-    default picks V from rhs and the ticket order): exact on the integer KAT
-    systems for ragged rhs (columns past rhs inside a lane's group), natural
-    and level order, one device and the multi-device split."""
-    torch = torch_cuda
-    monkeypatch.setenv("SBLAS_TRSM_V", v)
-    for name, sub in (("qh768", "fwd"), ("ash85", "bwd")):
-        g = np.load(os.path.join(GOLDEN, f"trsv_{name}_{sub}.npz"))
-        cp, ri, cv = g["colptr"], g["rowidx"], g["val"]
-        n = len(cp) - 1
-        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (cp, ri, cv)]
-        T = sb.DeviceTRSV(0, n, len(ri), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
-                          0 if sub == "fwd" else 1)
-        try:
-            for rhs in (2, 5, 13, 64, 67):
-                X = np.random.default_rng(rhs).integers(1, 11, (n, rhs)).astype(np.float64)
-                db = torch.from_numpy(csc_matmat(cp, ri, cv, X)).cuda()
-                for algo in (1, 3):
-                    xd = torch.full((n, rhs), -1.0, dtype=torch.float64, device="cuda")
-                    T.solve_rhs_opt(algo, 0, rhs, db.data_ptr(), xd.data_ptr())
-                    torch.cuda.synchronize()
-                    assert np.array_equal(xd.cpu().numpy(), X), (name, rhs, algo)
-        finally:
-            T.close()
-        X = np.random.default_rng(7).integers(1, 11, (n, 13)).astype(np.float64)
-        x, _ = sb.trsv_mgpu_solve(cp, ri, cv, n, csc_matmat(cp, ri, cv, X), 2, 0 if sub == "fwd" else 1, 13)
         assert np.array_equal(x, X)
 
 
@@ -880,10 +720,10 @@ def block_dense_csr(rng, nblk, width, k, sparse_tail=0):
 
 @pytest.mark.parametrize("fill", ["default", "0", "2"])
 @pytest.mark.parametrize("ncols", [64, 40, 130])
-def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols):
+def test_spmm_mfma_tiles(torch_cuda, sb, orc, fill, ncols):
+    """The v_mfma_f64_16x16x4f64 B-panel tile on block-dense rows (test
+    option spmm_mfma_fill: 0 = every 16-row block on MFMA, 2 = none)."""
     torch = torch_cuda
-    if fill != "default":
-        monkeypatch.setenv("SBLAS_SPMM_MFMA_FILL", fill)
     rng = np.random.default_rng(ncols)
     k = 3000
     rp, col, val = block_dense_csr(rng, 12, 37, k, sparse_tail=21)  # m = 213: partial last block
@@ -894,7 +734,8 @@ def test_spmm_mfma_tiles(torch_cuda, sb, orc, monkeypatch, fill, ncols):
     A = sb.DeviceCSR.upload(0, k, rp, col, val)
     Bd = torch.from_numpy(np.ascontiguousarray(B).ravel()).cuda()
     Cd = torch.from_numpy(np.asfortranarray(C0).ravel(order="F")).cuda()
-    A.spmm(ncols, 0.75, Bd.data_ptr(), ncols, 1, -0.5, Cd.data_ptr(), m)
+    with sb.test_options(**({} if fill == "default" else {"spmm_mfma_fill": float(fill)})):
+        A.spmm(ncols, 0.75, Bd.data_ptr(), ncols, 1, -0.5, Cd.data_ptr(), m)
     torch.cuda.synchronize()
     got = Cd.cpu().numpy().reshape((ncols, m)).T
     # MFMA sums the dense tile in union-column order (the rows' own order here,

@@ -14,51 +14,41 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-# (algorithm, plan environment).  The panel algorithm (4) picks ~4 MiB of x
-# per panel, i.e. one panel for these small matrices; 3 and 8 panels are
-# forced too so the multi-panel path (interleaved grid + partial reduce) runs.
-# The column-sorted algorithm (5) makes every range wide (one sub-item per
-# XCD + the partial reduce) on matrices of <= 6M entries, so these small
-# cases run the all-wide layout by default; ALLWIDE=0 restores the planner's
-# narrow ranges (few, for small matrices; a tiny work target forces many,
-# most of them wide and paired with narrow ones), and PAIR=0 runs one
-# sub-item per workgroup.  Q = 2 / 3
-# column groups per XCD (G = 16 / 24; config 2's default plan has q = 2)
-# cover the wide sub-items' group ranges and the narrow wrap at q > 1.
-ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"SBLAS_CSR5_HOSTPLAN": "1"}),
-         (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "3"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "8"}),
-         (4, {}), (4, {"SBLAS_PANELS": "3"}), (4, {"SBLAS_PANELS": "8"}),
-         (5, {}), (5, {"SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_ALLWIDE": "1"}),
-         (5, {"SBLAS_XS_ALLWIDE": "0"}), (5, {"SBLAS_XS_ALLWIDE": "0", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_PAIR": "0", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_WG": "512", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_WG": "768"}),
-         (5, {"SBLAS_XS_WG": "768", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_WG": "768", "SBLAS_XS_SOLO": "1"}),
-         (5, {"SBLAS_XS_DYN": "0"}), (5, {"SBLAS_XS_DYN": "0", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_Q": "2", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_Q": "3"}),
-         (5, {"SBLAS_XS_Q": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_FUSE": "1", "SBLAS_XS_WSTAR": "50"}), (5, {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_U": "2", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_SOLO": "1"}), (5, {"SBLAS_XS_SOLO": "1", "SBLAS_XS_WSTAR": "50"}),
-         (1, {"SBLAS_RS_SEQ": "0"}), (2, {"SBLAS_CSR5_PANEL": "1", "SBLAS_PANELS": "2"}),
-         (1, {"SBLAS_RS_PANEL": "1", "SBLAS_PANELS": "3"}),
-         (5, {"SBLAS_XS_WG": "1024"}), (5, {"SBLAS_XS_WG": "1024", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_U": "1"}), (5, {"SBLAS_XS_U": "3", "SBLAS_XS_WSTAR": "50"}),
-         (5, {"SBLAS_XS_WG": "512p", "SBLAS_XS_SOLO": "1", "SBLAS_XS_WSTAR": "50"})]
-ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3", "panel8", "xsort", "xsort_w50",
-            "xsort_allwide", "xsort_narrow", "xsort_narrow_w50", "xsort_unpaired", "xsort_wg512", "xsort_wg768",
-            "xsort_wg768_w50", "xsort_wg768_solo", "xsort_static", "xsort_static_w50",
-            "xsort_q2_w50", "xsort_q3", "xsort_q3_w50", "xsort_fused_w50", "xsort_k3_w50",
-            "xsort_u2_w50", "xsort_solo", "xsort_solo_w50", "rowsplit_vec4", "csr5_panel2",
-            "rowsplit_panel3", "xsort_wg1024", "xsort_wg1024_w50", "xsort_u1", "xsort_u3_w50",
-            "xsort_wg512p_solo_w50"]
+# (algorithm, planner test options -- sblas.test_options, never the
+# environment).  The panel algorithm (4) picks ~4 MiB of x per panel, i.e.
+# one panel for these small matrices; 3 and 8 panels are forced too so the
+# multi-panel path (interleaved grid + partial reduce) runs.  The
+# column-sorted algorithm (5) makes every range wide (one sub-item per XCD +
+# the partial reduce) on matrices of <= 6M entries, so these small cases run
+# the all-wide layout by default; xs_allwide=0 restores the planner's narrow
+# ranges (few, for small matrices; a tiny work cap, xs_cap, forces many, most
+# of them wide and paired with narrow ones, claimed dynamically); xs_solo=1
+# the solo narrow items of power-law plans.  "det" runs the handle in
+# deterministic mode (xsort's ordered form).
+ALGOS = [(0, {}), (1, {}), (2, {}), (2, {"csr5_hostplan": 1}),
+         (2, {"csr5_panel": 1, "panels": 3}), (2, {"csr5_panel": 1, "panels": 8}),
+         (4, {}), (4, {"panels": 3}), (4, {"panels": 8}),
+         (5, {}), (5, {"xs_cap": 50}), (5, {"xs_allwide": 1}),
+         (5, {"xs_allwide": 0}), (5, {"xs_allwide": 0, "xs_cap": 50}),
+         (5, {"xs_solo": 1}), (5, {"xs_solo": 1, "xs_cap": 50}),
+         (2, {"csr5_panel": 1, "panels": 2}), (1, {"rs_panel": 1, "panels": 3}),
+         (5, {"det": 1}), (5, {"det": 1, "xs_cap": 50}), (5, {"det": 1, "xs_allwide": 0}),
+         (5, {"det": 1, "xs_solo": 1, "xs_cap": 50}), (0, {"det": 1})]
+ALGO_IDS = ["auto", "rowsplit", "csr5", "csr5_hostplan", "csr5_panel3", "csr5_panel8", "panel", "panel3",
+            "panel8", "xsort", "xsort_cap50", "xsort_allwide", "xsort_narrow", "xsort_narrow_cap50",
+            "xsort_solo", "xsort_solo_cap50", "csr5_panel2", "rowsplit_panel3", "xsort_det",
+            "xsort_det_cap50", "xsort_det_narrow", "xsort_det_solo_cap50", "auto_det"]
+DET = {"on": False}
 
 
 @pytest.fixture(params=ALGOS, ids=ALGO_IDS)
-def algo(request, monkeypatch):
-    a, env = request.param
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    return a
+def algo(request, sb):
+    a, opts = request.param
+    opts = dict(opts)
+    DET["on"] = bool(opts.pop("det", 0))
+    with sb.test_options(**opts):
+        yield a
+    DET["on"] = False
 
 
 def random_csr(rng, m, n, density_rows, long_rows=(), empty_frac=0.1):
@@ -75,8 +65,9 @@ def random_csr(rng, m, n, density_rows, long_rows=(), empty_frac=0.1):
     return rp, col, val
 
 
-def run_gpu(torch, sb, algo, n, rp, col, val, x, alpha, beta, y0):
+def run_gpu(torch, sb, algo, n, rp, col, val, x, alpha, beta, y0, det=None):
     A = sb.DeviceCSR.upload(0, n, rp, col, val)
+    A.deterministic = DET["on"] if det is None else det
     xd = torch.from_numpy(np.ascontiguousarray(x)).cuda()
     yd = torch.from_numpy(np.ascontiguousarray(y0)).cuda()
     A.analyse(algo)
@@ -178,7 +169,7 @@ def test_edge_shapes(torch_cuda, sb, orc, algo):
 def test_csr5_device_plan_matches_host_plan(torch_cuda, sb, orc, monkeypatch, case):
     """CSR5 tile descriptors built on the device (row-start bits, tile rows,
     empty-row segment lists; format_cuda.h:21-300's job) give the same y, bit
-    for bit, as the host-built descriptors (SBLAS_CSR5_HOSTPLAN=1)."""
+    for bit, as the host-built descriptors (test option csr5_hostplan)."""
     rng = np.random.default_rng(11)
     if case == "ragged":
         m, n = 3000, 40000
@@ -204,8 +195,8 @@ def test_csr5_device_plan_matches_host_plan(torch_cuda, sb, orc, monkeypatch, ca
     x = rng.standard_normal(n)
     y0 = rng.standard_normal(m)
     got = run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 1.5, 0.5, y0)
-    monkeypatch.setenv("SBLAS_CSR5_HOSTPLAN", "1")
-    want = run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 1.5, 0.5, y0)
+    with sb.test_options(csr5_hostplan=1):
+        want = run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 1.5, 0.5, y0)
     assert np.array_equal(got, want)
     check(orc, rp, col, val, x, 1.5, 0.5, y0, got)
 
@@ -221,19 +212,45 @@ def test_repeat_deterministic(torch_cuda, sb, orc):
     assert np.array_equal(outs[4], outs[5])
 
 
-@pytest.mark.parametrize("env", [{}, {"SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_PAIR": "0"},
-                                 {"SBLAS_XS_K": "3", "SBLAS_XS_WSTAR": "50"}, {"SBLAS_XS_ALLWIDE": "0"},
-                                 {"SBLAS_XS_ALLWIDE": "0", "SBLAS_XS_U": "2"}])
-def test_xsort_relaunch(torch_cuda, sb, orc, monkeypatch, env):
+@pytest.mark.parametrize("opts", [{}, {"xs_allwide": 0}, {"xs_allwide": 0, "xs_cap": 50},
+                                  {"xs_solo": 1, "xs_cap": 50}])
+def test_xsort_deterministic_mode(torch_cuda, sb, orc, opts):
+    """a deterministic handle's xsort launches give the
+    same y bit for bit (chunk-ordered adds, fixed narrow walk), within the
+    per-row bound; the reference compares repeated runs the same way
+    (spmv/test/dspmv_test.cu:390-401)."""
+    n = 60000
+    rp, col, val = orc.gen_synth(n)
+    x = orc.gen_vector(n, 43)
+    y0 = orc.gen_vector(n, 44)
+    with sb.test_options(**opts):
+        A = sb.DeviceCSR.upload(0, n, rp, col, val)
+        A.deterministic = True
+        A.analyse(5)
+    xd = torch_cuda.from_numpy(x).cuda()
+    outs = []
+    for _ in range(6):
+        yd = torch_cuda.from_numpy(y0.copy()).cuda()
+        A.spmv(5, 0.75, xd.data_ptr(), -1.5, yd.data_ptr())
+        torch_cuda.cuda.synchronize()
+        outs.append(yd.cpu().numpy())
+    A.close()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0], o), f"{np.sum(outs[0] != o)} rows differ"
+    check(orc, rp, col, val, x, 0.75, -1.5, y0, outs[0])
+
+
+@pytest.mark.parametrize("opts", [{}, {"xs_cap": 50}, {"xs_allwide": 0}, {"xs_allwide": 0, "xs_cap": 50},
+                                  {"xs_solo": 1, "xs_cap": 50}])
+def test_xsort_relaunch(torch_cuda, sb, orc, opts):
     """The column-sorted kernel's work queues re-arm themselves at the end of
     each launch (no memset): five launches on one plan, each checked."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     n = 20000
     rp, col, val = orc.gen_synth(n)
     x = orc.gen_vector(n, 43)
-    A = sb.DeviceCSR.upload(0, n, rp, col, val)
-    A.analyse(5)
+    with sb.test_options(**opts):
+        A = sb.DeviceCSR.upload(0, n, rp, col, val)
+        A.analyse(5)
     xd = torch_cuda.from_numpy(x).cuda()
     want = orc.csr_spmv(rp, col, val, x, 1.5, 0.0, np.zeros(n))
     bound = orc.spmv_bound(rp, col, val, x, 1.5, 0.0, np.zeros(n))
@@ -361,31 +378,3 @@ def test_auto_pick(torch_cuda, sb, orc, monkeypatch, case):
         check(orc, rp, col, val, x, alpha, beta, y0, yd2.cpu().numpy())
     finally:
         A.close()
-
-
-@pytest.mark.parametrize("case", ["synth", "empty_rows", "long_rows"])
-def test_csr5_forms_bit_identical(torch_cuda, sb, orc, monkeypatch, case):
-    """The CSR5 tile forms (SBLAS_C5_PF: plain, phased loads, staged y with and
-    without non-temporal accesses) compute the same products and row sums in
-    the same order: their y are bit-identical (plain tiles, no panels)."""
-    rng = np.random.default_rng(77)
-    if case == "synth":
-        n = m = 30000
-        rp, col, val = orc.gen_synth(n)
-    else:
-        m, n = 40000, 50000
-        lens = rng.choice([0, 3, 9, 40] if case == "empty_rows" else [1, 9, 300, 3000], m,
-                          p=[0.3, 0.3, 0.3, 0.1] if case == "empty_rows" else [0.4, 0.5, 0.09, 0.01])
-        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-        col = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
-        val = rng.standard_normal(int(rp[-1]))
-    x = rng.standard_normal(n)
-    y0 = rng.standard_normal(m)
-    monkeypatch.setenv("SBLAS_CSR5_PANEL", "0")
-    outs = []
-    for form in ("0", "1", "2", "3"):
-        monkeypatch.setenv("SBLAS_C5_PF", form)
-        outs.append(run_gpu(torch_cuda, sb, 2, n, rp, col, val, x, 0.75, -1.25, y0))
-    for f, o in zip("123", outs[1:]):
-        assert np.array_equal(outs[0], o), f"form {f}: {np.sum(outs[0] != o)} rows differ"
-    check(orc, rp, col, val, x, 0.75, -1.25, y0, outs[0])
