@@ -137,12 +137,14 @@ __device__ __forceinline__ int xs_claim(const XsArgs &a, int xcc)
 // stream's chunks land in chunk order -- a wave adds claim c only once the
 // stream's LDS turn counter (*done, chunks past c0) has reached c, then
 // advances it -- so every row's sum runs in the same order on every launch
-// whichever waves took which chunks.  The holder of the lowest unfinished
-// claim never waits, so the turns always progress.
+// whichever waves took which chunks.  A narrow sub-item's two segments add
+// into the same rows, so they share one counter: segment 2's turns start at
+// `base` (segment 1's chunks rounded up to whole claims).  The holder of the
+// lowest unfinished claim never waits, so the turns always progress.
 template <bool kDet>
 __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4, const v2d *__restrict__ val2,
-                                              int ks, int vs, int *ctr, int *done, long long c0, long long c1,
-                                              const long long *bnd, int gb, int Wg,
+                                              int ks, int vs, int *ctr, int *done, int base, long long c0,
+                                              long long c1, const long long *bnd, int gb, int Wg,
                                               const double *__restrict__ x, double *acc)
 {
     constexpr int U = kXsU;
@@ -183,7 +185,7 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4, cons
     };
     auto accumulate = [&](long long cb, const v4u *kk, const v2d *va, const v2d *vb, double (*xx)[4]) {
         if constexpr (kDet) {  // wait for this claim's turn
-            const int want = (int)(cb - c0);
+            const int want = base + (int)(cb - c0);
             while (__builtin_amdgcn_readfirstlane(
                        __hip_atomic_load(done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != want)
                 __builtin_amdgcn_s_sleep(1);
@@ -202,7 +204,7 @@ __device__ __forceinline__ void xs_stream_dyn(const v4u *__restrict__ key4, cons
         if constexpr (kDet) {  // the adds complete, then the next claim's turn
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             if (lane == 0)
-                __hip_atomic_store(done, (int)(cb - c0) + U, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(done, base + (int)(cb - c0) + U, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
     v4u ka[U], kb[U];
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(kXsThreads) void k_spmv_xsort(const XsArgs a, const
     __shared__ long long s_rec_all[2][128 + 5];
     __shared__ int s_item;
     __shared__ int s_ctr[2][2];  // claimed chunks per (team, segment)
-    __shared__ int s_done[2][2]; // kDet: chunks added per (team, segment)
+    __shared__ int s_done[2][2]; // kDet: turn counter per team's sub-item ([h][0]; both segments)
     __shared__ int s_par[2][4];  // per team {sub valid, k1, g0, n1}
     const int half = (int)(threadIdx.x >= (unsigned)kXsTeam);
     const int ht = (int)threadIdx.x - half * kXsTeam;
@@ -341,8 +343,10 @@ __global__ __launch_bounds__(kXsThreads) void k_spmv_xsort(const XsArgs a, const
             if (hs < 0 || (seg && (hk1 || hg0 == 0))) continue;  // uniform
             const long long *hb = s_bnd_all[h] + (seg ? 128 : 0);
             const int hn = seg ? hg0 : hn1;
-            xs_stream_dyn<kDet>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], &s_done[h][seg], hb[0], hb[hn],
-                                hb, seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
+            // kDet: segment 2 continues segment 1's turns (the same rows)
+            const int base = seg ? (int)((s_bnd_all[h][hn1] - s_bnd_all[h][0] + kXsU - 1) / kXsU * kXsU) : 0;
+            xs_stream_dyn<kDet>(key4, val2, a.kstride, a.vstride, &s_ctr[h][seg], &s_done[h][0], base, hb[0],
+                                hb[hn], hb, seg ? 0 : hg0, a.Wg, x, acc_all + h * kXsHalfRows);
         }
         // A narrow sub-item alone in its item (the partner team empty: solo
         // items, or a leftover) is written by the whole workgroup: its rows
