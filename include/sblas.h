@@ -196,7 +196,12 @@ long long sblas_spmv_algorithmic_bytes(sblas_csr A, int beta_nonzero);
  * Concurrency: the handle owns the SpMM scratch (the row-major B panel and
  * the split-row partials), so ONE sblas_spmm per handle may be in flight:
  * issue a handle's calls on one stream, or synchronise between calls on
- * different streams or threads.  Distinct handles are independent. */
+ * different streams or threads.  Distinct handles are independent.
+ * The plan is built on the first call and tuned to that call's width n (the
+ * C-tile form sizes its slab sets so that XCDs x sets x row blocks x 16-column
+ * groups of n fill the CUs about once): later calls with another n are
+ * correct but keep the first call's grid and partial slots; for a different
+ * width at full speed, use a second handle. */
 int sblas_spmm(sblas_csr A, int n, double alpha, const double *d_B, int ldb,
                int b_layout, double beta, double *d_C, int ldc, void *stream);
 
