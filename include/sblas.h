@@ -177,6 +177,10 @@ int sblas_csr_pick(sblas_csr A, void *stream, int *algo);
  * once per process); the reference's cusparseDcsrmv
  * (dspmv_mgpu_baseline.cu:163-167) is repeatable the same way. */
 int sblas_csr_set_deterministic(sblas_csr A, int on);
+/* The XSORT plan's shape (8 values): ready, row ranges, wide ranges, work
+ * items, grid (persistent workgroups), solo (power-law layout), 256-entry
+ * chunks, most chunks of one item.  For tools and tests. */
+int sblas_csr_xsort_info(sblas_csr A, long long *info);
 int sblas_csr_get_deterministic(sblas_csr A, int *on);
 /* XCD column panels the analysed plan of `algo` runs over (0: the plain
  * layout / not analysed).  ROWSPLIT and CSR5 build per-panel plans (P = 4

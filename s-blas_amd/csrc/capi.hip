@@ -408,6 +408,16 @@ int sblas_csr_get_deterministic(sblas_csr A, int *on)
     return SBLAS_OK;
 }
 
+int sblas_csr_xsort_info(sblas_csr A, long long *info)
+{
+    if (!A || !info) return SBLAS_ERR_INVALID;
+    const XsPlan &P = A->xs;
+    const long long v[8] = {P.ready ? 1 : 0, P.nranges, P.nwide, P.nitems, P.grid, P.solo ? 1 : 0, P.nchunks,
+                            P.maxc};
+    for (int i = 0; i < 8; ++i) info[i] = v[i];
+    return SBLAS_OK;
+}
+
 int sblas_csr_pick(sblas_csr A, void *stream, int *algo)
 {
     if (!A || !algo) return SBLAS_ERR_INVALID;

@@ -63,7 +63,6 @@ constexpr int kXsThreads = 512;   // two teams of kXsWaves waves
 constexpr int kXsWaves = 4;       // waves per team
 constexpr int kXsTeam = kXsWaves * 64;
 constexpr int kXsU = 2;           // chunks per dynamic claim
-constexpr double kXsSoloSplit = 3.0;  // solo plans: narrow items per CU share (planner)
 constexpr long long kXsAllWideMaxNnz = 6000000;  // all ranges wide up to this many entries (planner)
 // LDS row accumulators per workgroup: 16384 = 128 KiB (default); an
 // experiment build may raise it towards the 160 KiB of a gfx950 CU
@@ -524,7 +523,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
     // its rows average >= 16 entries (the partials then cost <= 8 B per
     // entry); otherwise a narrow range of cost <= cap is cut afresh from r.
     std::vector<XsRange> ranges;
-    double nscale = 1.0;  // narrow cuts at nscale * cap (solo plans: below)
     auto build_ranges = [&](double cap) {
         ranges.clear();
         // cut(r): the first row always, then rows while the range's cost stays
@@ -537,7 +535,7 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
             const int emax = (int)std::min<long long>(m, (long long)start + (wide ? rows_cap : nrows_cap));
             auto fits = [&](int e) {
                 const double c = (double)(rp[e] - rp[start]);
-                return wide ? wide_cost(c) <= cap : narrow_cost(c) <= nfac * nscale * cap;
+                return wide ? wide_cost(c) <= cap : narrow_cost(c) <= nfac * cap;
             };
             int lo = start + 1, hi = emax;  // answer in [lo, hi]; lo always taken
             while (lo < hi) {
@@ -588,22 +586,6 @@ int build_xsort_plan(sblas_csr_s &A, hipStream_t s)
         if (flat >= 50) break;
         if (best_subs < 0 || subs < best_subs) best_subs = subs;
         cap *= 1.02;
-    }
-    // Solo plans (power-law graphs): the slot fit above sizes every sub-item
-    // to one CU's share, but a solo narrow item gathers over all of x (the
-    // Infinity Cache, not the XCD's L2) and runs ~3x a wide pair of the same
-    // modelled cost (R-MAT scale 21: 204 narrow items ~123 us against 48 wide
-    // pairs ~40 us, one item per CU: the chip busy 78% of the span).  The
-    // wide set stays as fitted; the narrow ranges are re-cut at 1/K of the
-    // cap, so ~K narrow items per CU sit behind the XCD queues and the
-    // dynamic claims even the CUs out.
-    if (P.solo && !fixed_cap) {
-        double K = kXsSoloSplit;
-        if (test_option("xs_nsplit", &opt)) K = std::max(1.0, opt);
-        if (K > 1.0) {
-            nscale = 1.0 / K;
-            build_ranges(cap);
-        }
     }
     const int I = (int)ranges.size();
     if ((long long)I >= (1LL << 23)) {

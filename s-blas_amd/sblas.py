@@ -118,6 +118,7 @@ _sig("sblas_test_deny_peer_access", _i, _i)
 _sig("sblas_peer_refs", _i, _i, _i)
 _sig("sblas_test_set_option", _i, C.c_char_p, _d, _i)
 _sig("sblas_csr_set_deterministic", _i, _p, _i)
+_sig("sblas_csr_xsort_info", _i, _p, _p)
 _sig("sblas_csr_get_deterministic", _i, _p, _p)
 _sig("sblas_ctx_create", _i, _p, _i, _p)
 _sig("sblas_ctx_destroy", _i, _p)
@@ -534,6 +535,13 @@ class DeviceCSR:
         a = C.c_int()
         check(lib.sblas_csr_pick(self.h, stream, C.byref(a)), "csr_pick")
         return a.value
+
+    def xsort_info(self) -> dict:
+        """The analysed XSORT plan's shape (sblas_csr_xsort_info)."""
+        v = np.zeros(8, np.int64)
+        check(lib.sblas_csr_xsort_info(self.h, ptr(v)), "csr_xsort_info")
+        keys = ("ready", "ranges", "wide", "items", "grid", "solo", "chunks", "max_item_chunks")
+        return {k: int(x) for k, x in zip(keys, v)}
 
     @property
     def deterministic(self) -> bool:

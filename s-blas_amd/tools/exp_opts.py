@@ -86,12 +86,13 @@ def main():
                         torch.cuda.synchronize()
                         ts.append(A.spmv_timed(a.algo, alpha, x.data_ptr(), beta, y.data_ptr(), sp))
                 abytes = A.algorithmic_bytes(True)
+                plan = A.xsort_info() if a.algo == 5 else None
                 A.close()
                 t = float(np.mean(ts))
                 print(json.dumps({"matrix": mname, "round": rnd, "opts": opts, "algo": a.algo, "n": n,
                                   "nnz": int(rp[-1]), "mean_us": round(t * 1e3, 2),
                                   "min_us": round(min(ts) * 1e3, 2), "frac": round(abytes / (t * 1e-3) / 8e12, 4),
-                                  "check": ok, "build_s": round(build_s, 2)}), flush=True)
+                                  "check": ok, "build_s": round(build_s, 2), "plan": plan}), flush=True)
 
 
 if __name__ == "__main__":
