@@ -257,6 +257,7 @@ void make_row_blocks(const int *rp, int m, std::vector<RowBlock> &blocks,
 // The test hook `opt` ("rs_panel" / "csr5_panel", sblas_test_set_option)
 // = 1 / 0 forces either form.
 constexpr long long kPanelMinNnz = 2000000LL;
+constexpr long long kC5WidePanelNnz = 32000000LL;  // CSR5: 2 MiB x panels from here (build_csr5_plan)
 static int xcd_panels_pay(sblas_csr_s &A, hipStream_t s, const char *opt, long long min_nnz, bool *use)
 {
     *use = false;
@@ -1135,8 +1136,15 @@ int build_csr5_plan(sblas_csr_s &A, hipStream_t s)
     // uniform config 2 4 panels beat 2 and 8 on short rows (N = 8 light rank
     // 60 vs 68 / 67 us) and are within 4-8% of 8 on 96-entry rows
     // (profiles/r05/c5P/).  Test hooks "csr5_panel" (1 / 0 forces either
-    // form) and "panels" (the count).
-    const int npanels = default_panels(A);
+    // form) and "panels" (the count).  From 32M entries the panels halve to
+    // ~2 MiB of x (P = 8, one per XCD): the x re-fetch the panel's entry
+    // stream forces through a 4 MiB L2 grows with the entries, the partial
+    // y (16 B per row and panel) with the rows -- config 2 at N = 1 (39.75M
+    // entries, 2M rows): 284.6-285.1 us at P = 4, 273.7-274.6 at P = 8
+    // (profiles/r06/panels/); the N = 8 light slice keeps P = 4.
+    int npanels = default_panels(A);
+    double popt = 0.0;
+    if (A.nnz >= kC5WidePanelNnz && !test_option("panels", &popt)) npanels = std::min(8, 2 * npanels);
     bool panels = false;
     SBLAS_TRY(xcd_panels_pay(A, s, "csr5_panel", kPanelMinNnz, &panels));
     if (panels && npanels >= 2 && !hostplan) {

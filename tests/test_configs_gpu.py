@@ -107,16 +107,17 @@ def test_config2_auto_deterministic(torch_cuda, sb, cfg2):
 
 
 def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
-    """Row split and CSR5 run over 4 XCD column panels on config 2's random
-    columns (x = 16 MB > 8 MiB, 39.75M nnz, rows spanning most of x) and keep
-    the plain layout on the reference generator's prefix columns; PANEL
-    always uses panels (sblas_csr_panels, spmv.hip xcd_panels_pay)."""
+    """Row split and CSR5 run over XCD column panels on config 2's random
+    columns (x = 16 MB > 8 MiB, 39.75M nnz, rows spanning most of x): 4 for
+    the row split, 8 for CSR5 from 32M entries; both keep the plain layout on
+    the reference generator's prefix columns; PANEL always uses panels
+    (sblas_csr_panels, spmv.hip xcd_panels_pay)."""
     A = sb.DeviceCSR.upload(0, N2, cfg2["rp"], cfg2["col"], cfg2["val"])
     try:
         for algo in (sb.ROWSPLIT, sb.CSR5, sb.PANEL):
             A.analyse(algo)
         want = 0 if cfg2["prefix"] else 4
-        assert A.panels(sb.ROWSPLIT) == want and A.panels(sb.CSR5) == want
+        assert A.panels(sb.ROWSPLIT) == want and A.panels(sb.CSR5) == 2 * want
         assert A.panels(sb.PANEL) == 4 or cfg2["prefix"]
     finally:
         A.close()
