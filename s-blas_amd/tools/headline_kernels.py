@@ -6,7 +6,10 @@ so the per-name stats csv mixes those launches into k_spmv_xsort's average;
 the headline's launches are the ones before the first launch of the row-split
 leg (`rowsplit_beside`, the next leg: k_spmv_panel / k_spmv_rowsplit).
 
-  python headline_kernels.py gpurun_out/r05_end/prof/run_kernel_trace.csv [--out f.json]
+  python headline_kernels.py gpurun_out/r05_end/prof/run_kernel_trace.csv [--out f.json] [--rows-out f.csv]
+
+--rows-out keeps the headline's own trace rows (kernel, start, end, duration)
+so the averages can be recomputed from the committed file alone.
 """
 import argparse
 import csv
@@ -19,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--out")
+    ap.add_argument("--rows-out")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     stop = next((i for i, r in enumerate(rows)
@@ -31,6 +35,15 @@ def main():
         out[key] = {"calls": int(d.size), "avg_us": round(float(d.mean()), 2) if d.size else None,
                     "min_us": round(float(d.min()), 2) if d.size else None,
                     "max_us": round(float(d.max()), 2) if d.size else None}
+    if a.rows_out:
+        with open(a.rows_out, "w", newline="") as fh:
+            wr = csv.writer(fh)
+            wr.writerow(["dispatch", "Kernel_Name", "Start_Timestamp", "End_Timestamp", "duration_us"])
+            for i, r in enumerate(head):
+                if any(key in r["Kernel_Name"] for key in ("k_spmv_xsort", "k_xsort_reduce")):
+                    st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                    wr.writerow([i, r["Kernel_Name"], st, en, round((en - st) * 1e-3, 3)])
+        out["rows_file"] = a.rows_out
     s = json.dumps(out, indent=1)
     print(s)
     if a.out:
