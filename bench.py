@@ -1305,7 +1305,9 @@ def run_ctx(args) -> int:
         "nnz_per_device": [int(z) for _, z, _ in info],
         "algo_per_device": dev_algos,
         "host_gen_s": round(t_gen, 2),
-        "plan": {"upload_and_build_s": round(plan_s, 3)},
+        "plan": {"upload_and_build_s": round(plan_s, 3),
+                 # the one-off plan in SpMV steps: calls before it is paid back
+                 "equals_steps": int(round(plan_s / max(step_ms * 1e-3, 1e-12)))},
         "exchange_ms_max_over_ranks": round(xch_max, 5),
         "timing": ("cold steps: per-device span (start event .. end of exchange) after a device-side "
                    "hold and a one-word all-reduce that align the devices (sblas_ctx_spmv_ex), max "
@@ -1744,6 +1746,8 @@ def main() -> int:
             "algorithmic_bytes_all_ranks": int(tot_bytes),
             "host_gen_s": round(t_gen, 2),
             "plan": {"build_s_max_over_ranks": round(plan_s_max, 3),
+                     # the one-off plan in SpMV steps (excluded from the timed region)
+                     "equals_steps": int(round(plan_s_max / max(ms_step * 1e-3, 1e-12))),
                      "device_bytes_rank0": int(op.A.plan_bytes(algo)),
                      "csr_device_bytes_rank0": int(12 * local_nnz + 4 * (op.A.info()[0] + 1))},
             "exchange_ms_max_over_ranks": round(xch_max, 5),

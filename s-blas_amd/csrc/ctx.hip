@@ -113,8 +113,8 @@ int peer_acquire(int a, int b, const char *who)
         set_error("%s: peer access %d -> %d refused (sblas_test_deny_peer_access)", who, a, b);
         return SBLAS_ERR_UNSUPPORTED;
     }
-    PeerLink &L = g_peer[{a, b}];
-    if (L.refs == 0) {
+    auto it = g_peer.find({a, b});
+    if (it == g_peer.end()) {  // first user: enable the link
         int can = 0;
         if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
             (void)hipGetLastError();
@@ -123,6 +123,7 @@ int peer_acquire(int a, int b, const char *who)
         }
         DeviceGuard g(a);
         const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        PeerLink L;
         if (e == hipErrorPeerAccessAlreadyEnabled) {  // enabled outside the library: use, never disable
             (void)hipGetLastError();
             L.owned = false;
@@ -132,8 +133,9 @@ int peer_acquire(int a, int b, const char *who)
         } else {
             L.owned = true;
         }
+        it = g_peer.emplace(std::make_pair(a, b), L).first;
     }
-    ++L.refs;
+    ++it->second.refs;
     return SBLAS_OK;
 }
 
