@@ -247,3 +247,11 @@ def test_torchrun_8_ranks_full_size():
     c3 = line["config3"]
     assert c3["check"] is True and c3["n_gpus"] == 8 and c3["exchange"] == "allreduce", c3
     assert len(c3["kernel_ms_per_device"]) == 8 and sum(c3["nnz_per_device"]) == 39_750_000
+    # first contact: the communicator and devices the line ran on
+    topo = line["topology"]
+    assert topo["comm_ranks"] == 8 and topo["backend"] == "gloo", topo
+    nd = topo["visible_devices"]
+    assert topo["device_ordinals"] == [r % nd for r in range(8)] and len(topo["pci_bus"]) == 8, topo
+    assert len(topo["peer_access"]) == nd
+    b4 = line["config5"]["blocks4"]
+    assert b4["check_exact_vs_xref"] and len(b4["block_devices"]) == 4 and sum(b4["block_rows"]) == 5_558_326, b4
