@@ -106,6 +106,53 @@ def test_config2_auto_deterministic(torch_cuda, sb, cfg2):
         assert np.array_equal(ys[0], y), f"launch {it}: {np.sum(ys[0] != y)} rows differ"
 
 
+@pytest.fixture(scope="module")
+def rmat21(sb, orc, torch_cuda):
+    """bench.py's structured R-MAT leg: 2^21 vertices, edge factor 16, seed 50."""
+    rp, col, val = sb.gen_rmat(21, 16, seed=50)
+    n = len(rp) - 1
+    x = sb.gen_vector(n, 43)
+    y0 = sb.gen_vector(n, 44)
+    alpha, beta = orc.alpha_beta()
+    want = orc.csr_spmv_omp(rp, col, val, x, alpha, beta, y0.copy())
+    bound = orc.spmv_bound(rp, col, val, x, alpha, beta, y0)
+    yield dict(n=n, rp=rp, col=col, val=val, alpha=alpha, beta=beta, want=want, bound=bound,
+               xd=torch_cuda.from_numpy(x).cuda(), y0d=torch_cuda.from_numpy(y0).cuda())
+
+
+@pytest.mark.parametrize("opts", [{}, {"det": 1}, {"xs_cap": 2000}])
+def test_rmat21_xsort(torch_cuda, sb, rmat21, opts):
+    """the R-MAT scale-21 stand-in at full size (the
+    bench's structured leg) through AUTO's xsort plan (solo narrow items),
+    every row within the per-row bound; relaunched so the self-rearming
+    queues run; a deterministic handle's launches bitwise equal; a small
+    sub-item cap (many more items than workgroups: the dynamic claims)."""
+    c = rmat21
+    opts = dict(opts)
+    det = bool(opts.pop("det", 0))
+    with sb.test_options(**opts):
+        A = sb.DeviceCSR.upload(0, c["n"], c["rp"], c["col"], c["val"])
+    A.deterministic = det
+    try:
+        with sb.test_options(**opts):
+            assert A.pick() == sb.XSORT
+            A.analyse(sb.XSORT)
+        info = A.xsort_info()
+        assert info["solo"] == 1
+        ys = []
+        yd = torch_cuda.empty_like(c["y0d"])
+        for it in range(3):
+            yd.copy_(c["y0d"])
+            A.spmv(sb.XSORT, c["alpha"], c["xd"].data_ptr(), c["beta"], yd.data_ptr())
+            torch_cuda.cuda.synchronize()
+            ys.append(yd.cpu().numpy())
+            _check_spmv(c["want"], c["bound"], ys[-1], f"rmat21 {opts} det={det} launch {it}")
+        if det:
+            assert all(np.array_equal(ys[0], y) for y in ys[1:])
+    finally:
+        A.close()
+
+
 def test_config2_xcd_panel_choice(torch_cuda, sb, cfg2):
     """Row split and CSR5 run over XCD column panels on config 2's random
     columns (x = 16 MB > 8 MiB, 39.75M nnz, rows spanning most of x): 4 for
