@@ -25,6 +25,19 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def matrix(sblas, name):
+    """(rowptr, col, val, ncols): ncols None = square."""
+    if name.startswith("slice"):  # rank 0's cyclic slice of config 2 at N = int(name[5:]) (bench.py N > 1)
+        import sblas_dist
+        n, world = 2_000_000, int(name[5:])
+        rp = sblas.gen_synth_rowptr(n, 96, 9)
+        plan = sblas_dist.make_cyclic_plan(rp, n, world)
+        lrp, col, val = sblas_dist.cyclic_local_csr(
+            rp, plan, 0, lambda a, b: sblas.gen_synth_rows(n, rp, a, b, 96, 9, seed=42))
+        return lrp, col, val, n
+    return matrix_sq(sblas, name) + (None,)
+
+
+def matrix_sq(sblas, name):
     if name == "rmat21":
         return sblas.gen_rmat(21, 16, seed=50)
     if name == "synth":
@@ -54,10 +67,11 @@ def main():
     sp = stream.cuda_stream
     alpha, beta = 0.8401877171547095, 0.39438292681909304
     for mname in a.mats.split(","):
-        rp, col, val = matrix(sblas, mname)
-        n = len(rp) - 1
+        rp, col, val, ncols = matrix(sblas, mname)
+        m = len(rp) - 1
+        n = ncols or m
         xh = sblas.gen_vector(n, 43)
-        y0 = sblas.gen_vector(n, 44)
+        y0 = sblas.gen_vector(m, 44)
         x = torch.from_numpy(xh).to(dev)
         want = bound = None
         if not a.no_check:
