@@ -8,7 +8,7 @@ handle in deterministic mode), builds the plan and times --reps cold calls
 N = 1 protocol), checks one y against the oracle's per-row bound, and prints
 one JSON line.  Experiment tooling only; the oracle is the checker.
 
-  python exp_opts.py --mats rmat21,synth --algo 5 --opts '[{}, {"xs_nsplit": 1}]'
+  python exp_opts.py --mats rmat21,synth,slice8 --algo 5 --opts '[{}, {"xs_solo": 1}]'
 """
 import argparse
 import json
